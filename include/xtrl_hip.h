@@ -1,0 +1,248 @@
+/*
+ * libxtrl_hip — C ABI of the MI355X (gfx950) Learner hot path.
+ *
+ * The reference (tinycrops/x-transformers-rl) is pure Python: there is no FFI of its own.  Each
+ * entry point below replaces a cluster of ATen calls on the reference's rollout/update path; the
+ * reference line it stands in for is cited per function ("xtrl.py" = x_transformers_rl/
+ * x_transformers_rl.py).  The Python host layer (x-transformers-rl_amd/xtrl_amd) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every function returns 0 (XTRL_OK) or an XTRL_E_* code; xtrl_last_error() has the message
+ *   - all buffers are caller-allocated device memory; plain pointers + sizes, row-major, fp32
+ *     unless the name says otherwise; the library keeps no state beyond its code objects
+ *   - `stream` is a hipStream_t passed as void*; every call is asynchronous on it and is safe to
+ *     capture into a hipGraph (no allocation, no synchronisation inside)
+ */
+#ifndef XTRL_HIP_H
+#define XTRL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XTRL_OK 0
+#define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
+#define XTRL_E_HIP 2    /* HIP launch or runtime error */
+
+#define XTRL_ABI_VERSION 1
+
+int xtrl_abi_version(void);
+const char* xtrl_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused fp32 MFMA GEMM  (every nn.Linear on the path: x-transformers to_q/k/v/out, FeedForward,
+ * WorldModelActorCritic heads; xtrl.py:315-369, 553-557)
+ *   Y[m, n] = act( LN?(X)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])
+ *   X [M][K] (ldx), W [N][K] (ldw, nn.Linear layout), Y [M][N] (ldy; Y += (*t_dev) * y_t_stride)
+ *   ln_gamma != NULL -> X rows are layer-normalised (eps 1e-5, no beta) and scaled by gamma
+ *   act: 0 none, 1 GELU(erf), 2 SiLU;  R may alias Y (in-place residual add)
+ * ------------------------------------------------------------------------------------------- */
+#define XTRL_ACT_NONE 0
+#define XTRL_ACT_GELU 1
+#define XTRL_ACT_SILU 2
+
+int xtrl_gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
+                  const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M,
+                  int N, int K, int act, void* stream);
+
+/* Y[m, :] = layer_norm(X[m, :]) * gamma  (x-transformers LayerNorm, final norm of the Decoder) */
+int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rollout: one timestep of the vectorised policy for E concurrent episodes.
+ * Replaces the per-step body of Learner.forward (xtrl.py:1250-1341): RSNorm eval (:1254-1259),
+ * WorldModelActorCritic.forward with KV cache (:479-559 -> x-transformers decode), Discrete
+ * sample/log_prob (:1280-1289), env.step (:1297-1313), Memory write (:1315).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct XtrlDecodeLayer {
+  const float* ln_attn;  /* [d]  pre-attention LayerNorm gamma */
+  const float* w_qkv;    /* [n_qkv][d]  rows: to_q | to_k | to_v | to_v_gate (opt) | value-residual mix (opt) */
+  const float* b_qkv;    /* [n_qkv]     zeros for q/k/v */
+  const float* w_out;    /* [d][I]      to_out */
+  const float* ln_ff;    /* [d] */
+  const float* w_ff1;    /* [ff][d] */
+  const float* b_ff1;    /* [ff] */
+  const float* w_ff2;    /* [d][ff] */
+  const float* b_ff2;    /* [d] */
+  float* k_cache;        /* [E][H][Tmax][dh]  keys (post-rotary) */
+  float* v_cache;        /* [E][H][Tmax][dh]  values (post value-residual mix) */
+} XtrlDecodeLayer;
+
+typedef struct XtrlRngState {   /* device memory; read by the sampling / sim kernels */
+  uint64_t seed;
+  uint32_t update;
+  uint32_t slot_offset;
+} XtrlRngState;
+
+typedef struct XtrlDecodeDesc {
+  /* shapes */
+  int E, S, A, B, d, L, H, dh, Tmax, G, ff, in_dim, n_qkv;
+  /* switches */
+  int continuous, squash, evolutionary, gate_values, value_residual, learned_mix;
+  int rotary_abs;       /* 0: rotary positions restart at 0 for every cached token (reference), 1: absolute */
+  int rot_dim;          /* dh / 2 */
+  int sim_mode;         /* 0 readme, 1 lander, -1 host env (no device sim step) */
+  int hazard_log2;
+  int no_reward_cond;   /* 1: model called with rewards=None (deploy without reward, xtrl.py:1042-1061) */
+  float rs_eps;
+  float clamp_lo, clamp_hi; int has_clamp;
+  /* weights (EMA model for the rollout, xtrl.py:1194) */
+  const float* w_pin; const float* b_pin;           /* project_in [d][S] (+[d] or NULL) */
+  const float* act_emb; const float* act_emb_b;     /* discrete [A][d]; continuous Linear [d][A] + [d] */
+  const float* reward_embed;                        /* [d] */
+  const float* w_se; const float* b_se;             /* to_state_embed [d][S], [d] */
+  const float* ln_final;                            /* [d] */
+  const float* w_h1; const float* b_h1;             /* [4d][in_dim]: action_head.0 rows then critic_head.0 rows */
+  const float* w_a2; const float* b_a2;             /* action_head.2 [A or 2A][2d] */
+  const float* w_c2; const float* b_c2;             /* critic_head.2 [B][2d] */
+  const float* inv_freq;                            /* [rot_dim/2] rotary inverse frequencies */
+  const XtrlDecodeLayer* layers;                    /* HOST array of L layer descriptors */
+  const float* rs_mean; const float* rs_var;        /* RSNorm running stats [S+1] */
+  /* env / episode state (device) */
+  float* state;            /* [E][S] current raw state */
+  int32_t* prev_action;    /* [E] (-1 at t = 0) */
+  float* prev_action_f;    /* [E][A] continuous */
+  float* prev_reward;      /* [E] */
+  uint8_t* alive;          /* [E] */
+  int32_t* lens;           /* [E] episode length so far */
+  double* cum_reward;      /* [E] cumulative reward (fitness, xtrl.py:1310, 1345-1346) */
+  const int32_t* episode_of_slot;  /* [E] episode index keying the Sim stream */
+  const XtrlRngState* rng;
+  /* trajectory (device), row e = one episode, padded with zeros past its length */
+  float* traj_states;      /* [E][Tmax][S] */
+  int32_t* traj_actions;   /* [E][Tmax] */
+  float* traj_actions_f;   /* [E][Tmax][A] continuous */
+  float* traj_logp;        /* [E][Tmax] (continuous: [E][Tmax][A]) */
+  float* traj_rewards;     /* [E][Tmax] */
+  uint8_t* traj_bounds;    /* [E][Tmax] terminated flags */
+  float* traj_values;      /* [E][Tmax][B] critic logits */
+  /* scratch (device) */
+  float* x;      /* [E][d] residual stream */
+  float* qkv;    /* [E][n_qkv] */
+  float* att;    /* [E][I] */
+  float* hff;    /* [E][max(ff, 4d)] */
+  float* ac_in;  /* [E][in_dim]  (final-normed embed | state embed | latent embed) */
+  float* logits; /* [E][A or 2A] */
+  float* v1;     /* [E][I] first layer's values (value residual) */
+} XtrlDecodeDesc;
+
+/* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
+ * the latent embedding columns of ac_in must already hold latent_to_embed(gene) (evolutionary). */
+int xtrl_rollout_begin(const XtrlDecodeDesc* desc, void* stream);
+/* one timestep t for all E episodes; with sim_mode == -1 the env step happens on the host and
+ * xtrl_rollout_env_feedback() writes its results back. */
+int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream);
+int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state, const float* reward,
+                              const uint8_t* terminated, void* stream);
+
+/* Attention for one decode step (exposed for tests): reads q|k|v|gate|mix rows, applies value
+ * residual + rotary, appends k/v at position t and attends over positions 0..t. */
+int xtrl_attn_decode(const XtrlDecodeDesc* desc, int layer, int t, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * HL-Gauss value decode + GAE   (xtrl.py:843-852 -> calc_gae :616-640, HLGaussLoss value)
+ *   values[e, t] = softmax(logits[e, t, :]) . centres     (B bins over [lo, hi])
+ *   returns = reverse scan of delta_t = r_t + gamma v_{t+1} m_t - v_t, gate = gamma lam m_t;
+ *   m_t = !bounds[e, t]; sequential order per row (bitwise stable)
+ *   logits row (e, t) at logits + e*ld_row + t*B; rewards / bounds at e*ld_seq + t;
+ *   values / returns written densely [E][n]; gamma_lam = float32(gamma * lam) as the reference
+ *   multiplies the Python product into the mask
+ * ------------------------------------------------------------------------------------------- */
+int xtrl_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, const uint8_t* bounds,
+                     int64_t ld_seq, const float* centers, float* values, float* returns, int E, int n, int B,
+                     float gamma, float gamma_lam, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Training attention (x-transformers Attend with causal + key-padding mask, post-softmax dropout)
+ *   q, k, v: [b][H][n][dh]; lens[b] valid keys per row; out o [b][H][n][dh]; lse [b][H][n]
+ * ------------------------------------------------------------------------------------------- */
+int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o, float* lse,
+                  int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset,
+                  void* stream);
+int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
+                  const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b,
+                  int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused PPO / critic / world-model / done loss   (xtrl.py:398-477 losses, :939-978 combination)
+ * ------------------------------------------------------------------------------------------- */
+typedef struct XtrlLossDesc {
+  int b, n, A, B, S1;     /* S1 = state_dim + 1 */
+  int continuous, squash, hl_reduction_mean;
+  float eps_clip, value_clip, entropy_weight, w_actor, w_critic, w_autoreg, lo, hi, sigma;
+  /* inputs */
+  const float* raw_actions;   /* [b][n][A or 2A] */
+  const float* values;        /* [b][n][B] */
+  const float* pred_raw;      /* [b][n][2 S1]  to_pred output (interleaved mean / log-var) */
+  const float* done_logit;    /* [b][n] */
+  const int32_t* actions;     /* [b][n] discrete */
+  const float* actions_f;     /* [b][n][A] continuous */
+  const float* old_logp;      /* [b][n] (continuous [b][n][A]) */
+  const float* returns;       /* [b][n] */
+  const float* old_values;    /* [b][n][B] */
+  const uint8_t* dones;       /* [b][n] */
+  const int32_t* lens;        /* [b] */
+  const float* real;          /* [b][n][S1] normalised states-with-rewards */
+  const float* support;       /* [B + 1] HL-Gauss bin edges (torch.linspace, host-computed) */
+  const float* centers;       /* [B]     bin centres */
+  /* workspace + outputs */
+  float* tok;                 /* [b][n][XTRL_LOSS_TOK] per-token scratch */
+  float* stats;               /* [XTRL_LOSS_STATS] scalars, see XTRL_LS_* */
+  /* gradients (backward) */
+  float* d_raw_actions; float* d_values; float* d_pred_raw; float* d_done_logit;
+} XtrlLossDesc;
+
+#define XTRL_LOSS_TOK 10
+#define XTRL_LOSS_STATS 32
+/* stats[] slots */
+#define XTRL_LS_LOSS 0         /* total loss (xtrl.py:975-978) */
+#define XTRL_LS_ACTOR 1        /* actor_loss.mean() over all b*n (log, xtrl.py:997) */
+#define XTRL_LS_CRITIC 2       /* critic_loss.mean() over all b*n */
+#define XTRL_LS_AUTOREG 3      /* world_model_loss.mean() over the masked elements */
+#define XTRL_LS_DONE 4         /* pred_done_loss.mean() over the mask */
+#define XTRL_LS_ADV_MEAN 5
+#define XTRL_LS_ADV_DEN 6      /* sqrt(clamp(unbiased var, 1e-5)) */
+#define XTRL_LS_L 7            /* HL-Gauss CE(values, returns), mean reduction */
+#define XTRL_LS_LC 8           /* HL-Gauss CE(values, clamp(returns)), mean reduction */
+#define XTRL_LS_NMASK 9
+#define XTRL_LS_NWM 10         /* number of world-model loss elements */
+#define XTRL_LS_KCRIT 11       /* masked tokens whose critic loss is not clipped to 0 */
+#define XTRL_LS_DL 12          /* d loss / d L   (per unit upstream gradient) */
+#define XTRL_LS_DLC 13         /* d loss / d Lc */
+
+int xtrl_loss_fwd(const XtrlLossDesc* desc, void* stream);
+int xtrl_loss_bwd(const XtrlLossDesc* desc, float grad_scale, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimiser path over one flat fp32 parameter buffer  (xtrl.py:987-992, 747-753)
+ * ------------------------------------------------------------------------------------------- */
+/* clip_grad_norm_ (xtrl.py:987): ws = 512 doubles of scratch; out[0] = total L2 norm,
+ * out[1] = min(max_norm / (norm + 1e-6), 1) */
+int xtrl_grad_norm(const float* g, int64_t n, double* ws, float max_norm, float* out, void* stream);
+/* AdoptAtan2 step (xtrl.py:749, 991) on n parameters split into n_seg tensors
+ * (seg_start[n_seg + 1] device offsets); g is scaled in place by clip[1] (clip may be NULL);
+ * seg_ws = n_seg ints of scratch; first_step != 0 initialises m = 0, v = g^2, p_init = p. */
+int xtrl_adopt_atan2(float* p, float* g, float* m, float* v, float* p_init, int64_t n, const int64_t* seg_start,
+                     int n_seg, int* seg_ws, const float* clip, float lr, float init_lr, float beta1, float beta2,
+                     float a, float b, float weight_decay, float regen_rate, float cautious, int first_step,
+                     void* stream);
+/* ema = lerp(ema, p, 1 - decay) */
+int xtrl_ema_lerp(float* ema, const float* p, int64_t n, float weight, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Synthetic vectorised Sim (stands in for gym LunarLander, which is not available)
+ * ------------------------------------------------------------------------------------------- */
+/* host-side evaluation of the device random streams (csrc/philox.h), e.g. the reward-dropout coin */
+float xtrl_rng_uniform(uint64_t seed, uint32_t update, uint32_t slot, uint32_t t, uint32_t field, uint32_t sub);
+float xtrl_rng_normal(uint64_t seed, uint32_t update, uint32_t slot, uint32_t t, uint32_t field, uint32_t sub);
+
+int xtrl_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const int32_t* episode_of_slot,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XTRL_HIP_H */

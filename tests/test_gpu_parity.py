@@ -1,0 +1,416 @@
+"""MI355X parity tests: every HIP kernel through the C ABI vs the oracle / an fp64 torch reference.
+
+Tolerances: integer / index / mask outputs bit-exact; fp32 outputs within 1e-4 relative (BASELINE
+north_star), tighter where the computation is short."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_port as R
+from oracle import thirdparty as tp
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def tol(a, b, rtol=1e-4, atol=1e-5):
+    a = a.detach().double().cpu() if torch.is_tensor(a) else torch.as_tensor(a).double()
+    b = b.detach().double().cpu() if torch.is_tensor(b) else torch.as_tensor(b).double()
+    np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=rtol, atol=atol)
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM (decode projections, FF, heads)
+# ----------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize('M,N,K', [(1, 5, 8), (37, 100, 96), (64, 64, 64), (130, 257, 48), (1024, 1024, 256),
+                                   (515, 4, 512)])
+@pytest.mark.parametrize('mode', ['plain', 'ln_gelu', 'silu', 'residual', 'ln'])
+def test_gemm_f32(M, N, K, mode):
+    from xtrl_amd import _lib as L, ops
+    g = torch.Generator(device='cpu').manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    gam = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    xd, wd = x.double(), w.double()
+    if mode == 'plain':
+        out, ref = ops.gemm(x, w, b), xd @ wd.T + b.double()
+    elif mode == 'silu':
+        out, ref = ops.gemm(x, w, b, act=L.ACT_SILU), torch.nn.functional.silu(xd @ wd.T + b.double())
+    elif mode == 'residual':
+        r2 = res.clone()
+        out = ops.gemm(x, w, None, residual=r2, out=r2)
+        ref = xd @ wd.T + res.double()
+    else:
+        xn = torch.nn.functional.layer_norm(xd, (K,), eps=1e-5) * gam.double()
+        if mode == 'ln':
+            out, ref = ops.gemm(x, w, b, ln_gamma=gam), xn @ wd.T + b.double()
+        else:
+            out, ref = ops.gemm(x, w, b, ln_gamma=gam, act=L.ACT_GELU), torch.nn.functional.gelu(xn @ wd.T + b.double())
+    torch.cuda.synchronize()
+    tol(out, ref, 1e-5, 1e-5)
+
+
+# ----------------------------------------------------------------------------------------------
+# training attention
+# ----------------------------------------------------------------------------------------------
+
+
+def attn_ref(q, k, v, lens, scale):
+    b, H, n, dh = q.shape
+    s = torch.einsum('bhid,bhjd->bhij', q, k) * scale
+    i = torch.arange(n, device=q.device)
+    mask = (i[None, :] <= i[:, None])[None, None] & (i[None, None, None, :] < lens[:, None, None, None])
+    s = s.masked_fill(~mask, -torch.finfo(s.dtype).max)
+    return torch.einsum('bhij,bhjd->bhid', s.softmax(-1), v)
+
+
+@pytest.mark.parametrize('b,H,n,dh', [(3, 4, 37, 16), (2, 2, 130, 16), (2, 3, 64, 32), (1, 2, 70, 64), (4, 4, 128, 16)])
+def test_attention_fwd_bwd(b, H, n, dh):
+    from xtrl_amd import ops
+    g = torch.Generator().manual_seed(n + dh)
+    q, k, v, do = (torch.randn(b, H, n, dh, generator=g).to(DEV) for _ in range(4))
+    lens = torch.randint(1, n + 1, (b,), generator=g).to(torch.int32)
+    lens[0] = n
+    lens = lens.to(DEV)
+    scale = dh ** -0.5
+    qd, kd, vd = (t.double().requires_grad_() for t in (q, k, v))
+    ref = attn_ref(qd, kd, vd, lens, scale)
+    (ref * do.double()).sum().backward()
+    qf, kf, vf = (t.clone().requires_grad_() for t in (q, k, v))
+    out = ops.attention(qf, kf, vf, lens, scale)
+    (out * do).sum().backward()
+    torch.cuda.synchronize()
+    tol(out, ref, 1e-5, 1e-5)
+    tol(qf.grad, qd.grad, 1e-4, 1e-5)
+    tol(kf.grad, kd.grad, 1e-4, 1e-5)
+    tol(vf.grad, vd.grad, 1e-4, 1e-5)
+
+
+def test_attention_dropout_consistent():
+    """Same seed -> same mask; the backward differentiates exactly the forward's dropped product."""
+    from xtrl_amd import ops
+    g = torch.Generator().manual_seed(5)
+    b, H, n, dh = 2, 2, 50, 16
+    q, k, v = (torch.randn(b, H, n, dh, generator=g).to(DEV) for _ in range(3))
+    lens = torch.tensor([50, 31], dtype=torch.int32, device=DEV)
+    o1 = ops.attention(q, k, v, lens, 0.25, 0.25, seed=11, offset=3)
+    o2 = ops.attention(q, k, v, lens, 0.25, 0.25, seed=11, offset=3)
+    o3 = ops.attention(q, k, v, lens, 0.25, 0.25, seed=12, offset=3)
+    assert torch.equal(o1, o2) and not torch.equal(o1, o3)
+    # directional derivative check in v (output is linear in v given the mask)
+    dv = torch.randn_like(v)
+    vv = v.clone().requires_grad_()
+    w = torch.randn_like(o1)
+    (ops.attention(q, k, vv, lens, 0.25, 0.25, seed=11, offset=3) * w).sum().backward()
+    fd = ((ops.attention(q, k, v + dv, lens, 0.25, 0.25, seed=11, offset=3) - o1) * w).sum()
+    tol((vv.grad * dv).sum(), fd, 1e-4, 1e-4)
+    # expectation: dropout keeps ~75 %
+    o0 = ops.attention(q, k, torch.ones_like(v), lens, 0.25, 0.25, seed=7, offset=0)
+    assert abs(float(o0.mean()) - 1.0) < 0.05
+
+
+# ----------------------------------------------------------------------------------------------
+# rollout (decode step, sampling, synthetic Sim) vs the oracle's batch-1 reference loop
+# ----------------------------------------------------------------------------------------------
+
+
+def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
+                 hazard=3, mode='lander', dim=48, reward_dropout=0.5):
+    from xtrl_amd import Learner, SynthVecSim
+    torch.manual_seed(seed)
+    wm = dict(attn_dim_head=16, heads=4, depth=depth)
+    if gates:
+        wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
+    gp = dict(dim=8, num_genes_per_island=3, num_selected=2, tournament_size=2)
+    learner = Learner(state_dim=S, num_actions=A, reward_range=(-2., 2.), world_model=wm, max_timesteps=T,
+                      batch_size=batch, num_episodes_per_update=episodes, evolutionary=evo, evolve_every=1,
+                      evolve_after_step=0, latent_gene_pool=gp, continuous_actions=cont,
+                      continuous_actions_clamp=(-1., 1.) if cont else None,
+                      agent_kwargs=dict(dropout=0., seed=seed, hidden_dim=dim, reward_dropout=reward_dropout),
+                      use_graph=False)
+    with torch.no_grad():   # non-trivial gate / mix weights (their init is constant)
+        g = torch.Generator().manual_seed(seed + 1)
+        for name, p in learner.agent.model.named_parameters():
+            if 'to_v_gate' in name or 'to_value_residual_mix' in name:
+                p.copy_((torch.randn(p.shape, generator=g) * 0.3).to(p.device))
+        learner.agent.ema_flat.copy_(learner.agent.flat.flat)
+    env = SynthVecSim(S, A, mode, hazard_log2=hazard)
+    c = R.LearnerConfig(S, A, (-2., 2.), dim=dim, depth=depth, gate_values=gates, value_residual=gates,
+                        learned_mix=gates, continuous=cont, clamp=(-1., 1.) if cont else None, evolutionary=evo,
+                        evolve_every=1, evolve_after_step=0, gene_pool=gp, max_timesteps=T, batch_size=batch,
+                        num_episodes_per_update=episodes, sim_mode=mode, hazard_log2=hazard, seed=seed,
+                        reward_dropout=reward_dropout)
+    sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
+    genes = learner.agent.gene_pool.genes.clone() if evo else None
+    oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes)
+    return learner, env, oracle
+
+
+def compare_rollout(traj, lens, episodes, cont=False):
+    lens = lens.cpu().numpy()
+    for i, ep in enumerate(episodes):
+        n = ep['len']
+        assert lens[i] == n, (i, lens[i], n)
+        mem = ep['mem']
+        states = torch.stack([m[0] for m in mem])
+        np.testing.assert_array_equal(traj['states'][i, :n].cpu().numpy(), states.numpy())
+        if cont:
+            tol(traj['actions_f'][i, :n], torch.stack([m[1] for m in mem]), 1e-4, 1e-5)
+            tol(traj['logp'][i, :n], torch.stack([m[2] for m in mem]), 1e-4, 1e-4)
+        else:
+            np.testing.assert_array_equal(traj['actions'][i, :n].cpu().numpy(), np.array([int(m[1]) for m in mem]))
+            tol(traj['logp'][i, :n], torch.stack([m[2] for m in mem]), 1e-4, 1e-5)
+        rw = torch.stack([m[3] for m in mem])
+        if not cont:
+            np.testing.assert_array_equal(traj['rewards'][i, :n].cpu().numpy(), rw.numpy())
+        np.testing.assert_array_equal(traj['bounds'][i, :n].cpu().numpy().astype(bool),
+                                      torch.stack([m[4] for m in mem]).numpy())
+        tol(traj['values'][i, :n], torch.stack([m[5] for m in mem]), 1e-4, 1e-4)
+        # padding past the episode is zero, as pad_sequence leaves it (xtrl.py:837)
+        assert float(traj['values'][i, n:].abs().sum()) == 0.
+
+
+@pytest.mark.parametrize('depth,gates,evo', [(1, False, False), (2, True, False), (2, True, True), (3, True, True)])
+def test_rollout_matches_oracle(depth, gates, evo):
+    learner, env, oracle = make_learner(depth=depth, gates=gates, evo=evo)
+    traj, lens, _, cum = learner.rollout_device(env, 0, 12)
+    torch.cuda.synchronize()
+    episodes, fitness = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes)
+    if evo:
+        tol(learner.fitness(cum, torch.tensor([g for _, g in learner.episode_genes])), fitness, 1e-5, 1e-5)
+
+
+def test_rollout_continuous_matches_oracle():
+    learner, env, oracle = make_learner(cont=True, gates=True)
+    traj, lens, _, _ = learner.rollout_device(env, 0, 12)
+    torch.cuda.synchronize()
+    episodes, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes, cont=True)
+
+
+def test_rollout_graph_replay_equals_eager():
+    learner, env, _ = make_learner(depth=2, T=16, episodes=16)
+    traj, lens, _, _ = learner.rollout_device(env, 0, 16)
+    eager = {k: v.clone() for k, v in traj.items() if v is not None}
+    learner.use_graph = True
+    learner._engine = None
+    for update in (0, 0):   # capture, then replay
+        traj, lens2, _, _ = learner.rollout_device(env, update, 16)
+    torch.cuda.synchronize()
+    for k, v in eager.items():
+        assert torch.equal(v, traj[k]), k
+
+
+# ----------------------------------------------------------------------------------------------
+# GAE + HL-Gauss value decode
+# ----------------------------------------------------------------------------------------------
+
+
+def test_hlgauss_gae_matches_oracle():
+    from xtrl_amd import ops
+    g = torch.Generator().manual_seed(9)
+    E, T, B, n = 33, 40, 100, 37
+    logits = torch.randn(E, T, B, generator=g)
+    rewards = torch.randn(E, T, generator=g)
+    bounds = (torch.rand(E, T, generator=g) < 0.1).to(torch.uint8)
+    hl = tp.HLGaussLoss(-2., 2., B, clamp_to_range=True)
+    vals, rets = ops.hlgauss_gae(logits.to(DEV), rewards.to(DEV), bounds.to(DEV), hl.centers.to(DEV), n, 0.99, 0.95)
+    torch.cuda.synchronize()
+    v_ref = hl(logits[:, :n])
+    r_ref = R.calc_gae(rewards[:, :n], v_ref, (bounds[:, :n] == 0).float(), 0.99, 0.95)
+    tol(vals, v_ref, 1e-5, 1e-6)
+    tol(rets, r_ref, 1e-5, 1e-5)
+
+
+# ----------------------------------------------------------------------------------------------
+# fused loss forward / backward vs autograd through the oracle's loss restatement
+# ----------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize('cont,hl_mean', [(False, True), (True, True), (False, False)])
+def test_fused_loss_matches_oracle(cont, hl_mean):
+    from xtrl_amd import ops
+    g = torch.Generator().manual_seed(21 + cont)
+    b, n, A, B, S1 = 5, 23, 3, 100, 6
+    lens = torch.tensor([23, 17, 1, 9, 22], dtype=torch.int32)
+    raw = torch.randn(b, n, 2 * A if cont else A, generator=g)
+    values = torch.randn(b, n, B, generator=g)
+    pred_raw = torch.randn(b, n, 2 * S1, generator=g)
+    done_logit = torch.randn(b, n, generator=g) * 2
+    if cont:
+        actions = torch.rand(b, n, A, generator=g) * 1.8 - 0.9
+        old_lp = torch.randn(b, n, A, generator=g) * 0.3 - 1.
+    else:
+        actions = torch.randint(0, A, (b, n), generator=g)
+        old_lp = torch.log(torch.rand(b, n, generator=g) * 0.8 + 0.1)
+    returns = torch.randn(b, n, generator=g)
+    old_values = torch.randn(b, n, B, generator=g)
+    dones = torch.rand(b, n, generator=g) < 0.2
+    real = torch.randn(b, n, S1, generator=g)
+    lo, hi = -2., 2.
+    cfg = R.ModelConfig(S1 - 1, A, 32, continuous=cont, squash=True, reward_range=(lo, hi))
+    hl = tp.HLGaussLoss(lo, hi, B, clamp_to_range=True)
+    hl_prev = tp.HLGaussLoss.default_reduction
+    tp.HLGaussLoss.default_reduction = 'mean' if hl_mean else 'none'
+    try:
+        ins = [t.clone().double().requires_grad_() for t in (raw, values, pred_raw, done_logit)]
+        r_, v_, p_, d_ = ins
+        mask = torch.arange(n)[None] < lens[:, None]
+        mean, lv = p_.reshape(b, n, S1, 2).unbind(-1)
+        var = (torch.tanh(lv / 3.) * 3.).exp()
+        wm = R.autoregressive_loss(torch.stack((mean, var)), real.double())[mask[:, :-1]]
+        dl = R.done_loss(torch.sigmoid(d_), dones)[mask]
+        hld = tp.HLGaussLoss(lo, hi, B, clamp_to_range=True).double()
+        al = R.actor_loss(cfg, hld, r_, actions.double() if cont else actions, old_lp.double(), returns.double(),
+                          old_values.double(), mask)
+        cl = R.critic_loss(cfg, hld, v_, returns.double(), old_values.double())
+        ac = (al * 0.5 + cl * 1.)[mask]
+        ref = ac.mean() + (wm.mean() + dl.mean()) * 0.7
+        ref.backward()
+    finally:
+        tp.HLGaussLoss.default_reduction = hl_prev
+    K = ops.LossConsts(actions=(actions.float() if cont else actions.to(torch.int32)).to(DEV).contiguous(),
+                       old_logp=old_lp.to(DEV), returns=returns.to(DEV), old_values=old_values.to(DEV),
+                       dones=dones.to(torch.uint8).to(DEV), lens=lens.to(DEV), real=real.to(DEV),
+                       support=hl.support.to(DEV), centers=hl.centers.to(DEV), continuous=cont, squash=True,
+                       hl_mean=hl_mean, eps_clip=0.2, value_clip=0.4, entropy_weight=0.01, w_actor=0.5, w_critic=1.,
+                       w_autoreg=0.7, lo=lo, hi=hi, sigma=float(hl.sigma))
+    outs = [t.clone().to(DEV).requires_grad_() for t in (raw, values, pred_raw, done_logit)]
+    loss, stats = ops.fused_loss(*outs, K)
+    loss.backward()
+    torch.cuda.synchronize()
+    tol(loss, ref, 1e-5, 1e-6)
+    tol(stats[1], al.mean(), 1e-5, 1e-6)
+    tol(stats[2], cl.mean(), 1e-5, 1e-6)
+    tol(stats[3], wm.mean(), 1e-5, 1e-6)
+    tol(stats[4], dl.mean(), 1e-5, 1e-6)
+    for ours, theirs in zip(outs, ins):
+        tol(ours.grad, theirs.grad, 1e-4, 1e-6)
+
+
+# ----------------------------------------------------------------------------------------------
+# optimiser path vs the restated AdoptAtan2 / clip_grad_norm_
+# ----------------------------------------------------------------------------------------------
+
+
+def test_adopt_atan2_and_clip_match_oracle():
+    from xtrl_amd import ops
+    g = torch.Generator().manual_seed(4)
+    shapes = [(7, 5), (13,), (3, 4, 2), (1,)]
+    params = [torch.randn(s, generator=g) for s in shapes]
+    ref_params = [torch.nn.Parameter(p.clone()) for p in params]
+    opt = tp.AdoptAtan2(ref_params, lr=8e-4, betas=(0.9, 0.99), regen_reg_rate=1e-4, cautious_factor=0.1)
+    sizes = [p.numel() for p in params]
+    offs = np.cumsum([0] + sizes)
+    flat = torch.cat([p.reshape(-1) for p in params]).to(DEV)
+    m, v, pinit = (torch.zeros_like(flat) for _ in range(3))
+    seg = torch.tensor(offs, dtype=torch.int64, device=DEV)
+    seg_ws = torch.zeros(len(shapes), dtype=torch.int32, device=DEV)
+    ws = torch.zeros(512, dtype=torch.float64, device=DEV)
+    clip = torch.zeros(2, device=DEV)
+    for step in range(4):
+        grads = [torch.randn(s, generator=g) * (3. if step == 2 else 0.05) for s in shapes]
+        for p, gr in zip(ref_params, grads):
+            p.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref_params, 0.5)
+        opt.step()
+        gflat = torch.cat([gr.reshape(-1) for gr in grads]).to(DEV)
+        ops.grad_norm(gflat, 0.5, ws, clip)
+        ops.adopt_atan2(flat, gflat, m, v, pinit, seg, seg_ws, clip, lr=8e-4, init_lr=8e-4, betas=(0.9, 0.99),
+                        a=1.27, b=1., weight_decay=0., regen_rate=1e-4, cautious=0.1, first_step=step == 0)
+        torch.cuda.synchronize()
+        tol(flat, torch.cat([p.detach().reshape(-1) for p in ref_params]), 1e-5, 1e-6)
+
+
+# ----------------------------------------------------------------------------------------------
+# end to end: rollout + learn (two updates) vs the oracle Learner
+# ----------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize('evo,gates', [(False, False), (True, True)])
+def test_learner_two_updates_match_oracle(evo, gates):
+    learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, T=10, episodes=6, batch=2, seed=5, hazard=2)
+    agent = learner.agent
+    for u in range(2):
+        traj, lens, genes, cum = learner.rollout_device(env, u, 10)
+        episodes, fitness = oracle.rollout(u)
+        compare_rollout(traj, lens, episodes)
+        fit = learner.fitness(cum, genes)
+        agent.learn(traj, lens, genes, fit, update=u)
+        oracle.learn(episodes, fitness, u)
+        logs = agent.pop_logs()
+        ours = np.array([[lg[k] for k in ('loss', 'actor_loss', 'critic_loss', 'autoreg_loss', 'pred_done_loss')]
+                         for lg in logs])
+        theirs = np.array([[lg[k] for k in ('loss', 'actor_loss', 'critic_loss', 'autoreg_loss', 'pred_done_loss')]
+                           for lg in oracle.logs])
+        oracle.logs = []
+        np.testing.assert_allclose(ours, theirs, rtol=1e-4, atol=1e-5)
+    torch.cuda.synchronize()
+    for k, p in agent.model.state_dict().items():
+        tol(p, oracle.model.state_dict()[k], 1e-4, 1e-5)
+    tol(agent.rs_mean, oracle.rsnorm.mean, 1e-4, 1e-5)
+    tol(agent.rs_var, oracle.rsnorm.var, 1e-4, 1e-5)
+    if evo:
+        tol(agent.gene_pool.genes, oracle.genes, 1e-5, 1e-6)
+
+
+# ----------------------------------------------------------------------------------------------
+# the reference's own test contract (tests/test_x_transformers_rl.py:4-53) on the host-env path
+# ----------------------------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize('evolutionary', (False, True))
+@pytest.mark.parametrize('continuous_actions', (False, True))
+def test_e2e_reference_contract(evolutionary, continuous_actions, tmp_path):
+    from xtrl_amd import Learner
+
+    class Sim:
+        def reset(self, seed=None):
+            return np.random.randn(5)
+
+        def step(self, actions):
+            return np.random.randn(5), np.random.randn(1), False
+
+    learner = Learner(state_dim=5, num_actions=2, reward_range=(-1., 1.), max_timesteps=10, batch_size=2,
+                      num_episodes_per_update=2, continuous_actions=continuous_actions, evolutionary=evolutionary,
+                      latent_gene_pool=dict(dim=32, num_genes_per_island=3, num_selected=2, tournament_size=2),
+                      world_model=dict(attn_dim_head=16, heads=4, depth=1),
+                      agent_kwargs=dict(save_path=str(tmp_path / 'ppo.pt')))
+    learner(Sim(), 1)
+    agent = learner.agent
+    hiddens = None
+    actions, hiddens = agent(np.random.randn(5), hiddens=hiddens)
+    actions, hiddens = agent(np.random.randn(5), hiddens=hiddens)
+    assert actions.shape == ((4,) if continuous_actions else (2,))
+    assert torch.isfinite(actions).all()
+    assert (tmp_path / 'ppo.pt').exists()
+
+
+def test_deploy_forward_matches_oracle_cached_decode():
+    """Agent.forward (online model, KV cache threaded through hiddens) vs the oracle module."""
+    learner, env, oracle = make_learner(depth=2, gates=True)
+    agent = learner.agent
+    agent.rs_mean.copy_(torch.linspace(-0.5, 0.5, 9))
+    agent.rs_var.copy_(torch.linspace(0.5, 2., 9))
+    rs = R.RSNormState(9)
+    rs.mean, rs.var = agent.rs_mean.cpu().clone(), agent.rs_var.cpu().clone()
+    m = oracle.model
+    m.eval()
+    g = torch.Generator().manual_seed(2)
+    hiddens, cache = None, None
+    for t in range(4):
+        s = torch.randn(8, generator=g)
+        reward = None if t % 2 == 0 else float(torch.randn((), generator=g))
+        raw, hiddens = agent(s.numpy(), reward=reward, hiddens=hiddens)
+        swr = rs.apply(torch.cat((s, torch.tensor([0. if reward is None else reward]))))
+        with torch.no_grad():
+            r, _, _, _, cache = m(swr[:-1].reshape(1, 1, -1), rewards=None if reward is None else swr[-1],
+                                  cache=cache)
+        tol(raw, r.reshape(-1), 1e-4, 1e-5)

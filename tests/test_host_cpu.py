@@ -1,0 +1,136 @@
+"""CPU-only checks of the product's host side and of the C-ABI library (no kernel launches)."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import philox as OP
+from oracle import ref_port as R
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def test_library_exports_every_declared_symbol():
+    from xtrl_amd import _lib
+    lib = _lib.load()
+    header = (REPO / 'include' / 'xtrl_hip.h').read_text()
+    declared = set(re.findall(r'^\s*(?:int|float|const char\*)\s+(xtrl_\w+)\s*\(', header, re.M))
+    assert len(declared) >= 18
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(_lib.SIGNATURES) <= declared | {'xtrl_last_error'}
+    assert lib.xtrl_abi_version() == _lib.ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    """ctypes mirrors of the C structs: field order / count as declared in include/xtrl_hip.h."""
+    from xtrl_amd import _lib
+    header = (REPO / 'include' / 'xtrl_hip.h').read_text()
+    for cname, py in (('XtrlDecodeLayer', _lib.DecodeLayer), ('XtrlDecodeDesc', _lib.DecodeDesc),
+                      ('XtrlLossDesc', _lib.LossDesc), ('XtrlRngState', _lib.RngState)):
+        body = re.search(r'typedef struct %s \{(.*?)\} %s;' % (cname, cname), header, re.S).group(1)
+        body = re.sub(r'/\*.*?\*/', '', body, flags=re.S)
+        names = []
+        for decl in body.split(';'):
+            decl = decl.strip()
+            if not decl:
+                continue
+            decl = re.sub(r'^(const\s+)?\w+\s*\**', '', decl)   # drop the type of the first declarator
+            for part in decl.split(','):
+                part = part.strip().lstrip('*').strip()
+                part = re.sub(r'^(const\s+)?(int|float|uint8_t|int32_t|uint32_t|uint64_t|double|XtrlDecodeLayer|XtrlRngState)\s*\**\s*', '', part)
+                if part:
+                    names.append(part)
+        assert names == [f[0] for f in py._fields_], (cname, names, [f[0] for f in py._fields_])
+
+
+@pytest.mark.parametrize('args', [(0, 0, 0, 0, 4, 0), (7, 3, 11, 5, 1, 2), (2 ** 40 + 5, 9, 1000, 499, 2, 0)])
+def test_host_rng_matches_oracle_philox(args):
+    from xtrl_amd import _lib
+    seed, upd, slot, t, field, sub = args
+    lib = _lib.load()
+    u = lib.xtrl_rng_uniform(seed, upd, slot, t, field, sub)
+    z = lib.xtrl_rng_normal(seed, upd, slot, t, field, sub)
+    assert np.float32(u) == OP.philox_uniform(seed, upd, slot, t, field, sub + 1)[sub]
+    assert np.float32(z) == OP.philox_uniform(seed, upd, slot, t, field, sub + 1, normal=True)[sub]
+
+
+def test_minibatch_order_and_reward_coin_match_oracle():
+    from xtrl_amd.learner import epoch_permutation, reward_coin
+    for args in ((0, 0, 0, 10), (5, 3, 2, 129), (123, 7, 3, 1024)):
+        assert torch.equal(epoch_permutation(*args), OP.epoch_permutation(*args))
+    for seed in range(5):
+        for mb in range(6):
+            for p in (0., 0.25, 0.5):
+                assert reward_coin(seed, 1, 2, mb, p) == OP.reward_coin(seed, 1, 2, mb, p)
+
+
+def test_shard_pairs_is_torch_chunk():
+    from xtrl_amd.distributed import shard_pairs
+    for n, world in ((64, 1), (64, 8), (30, 4), (3, 3), (10, 3)):
+        pairs = torch.cartesian_prod(torch.arange(n), torch.arange(1))
+        chunks = pairs.chunk(world, dim=0)
+        for rank in range(world):
+            mine, start = shard_pairs([tuple(p) for p in pairs.tolist()], world, rank)
+            ref = chunks[rank].tolist() if rank < len(chunks) else []
+            assert [list(p) for p in mine] == ref
+            if mine:
+                assert [list(p) for p in [tuple(x) for x in pairs.tolist()][start:start + len(mine)]] == ref
+
+
+def test_gene_pool_matches_reference_golden(golden):
+    """Product LatentGenePool.evolve_ vs the reference's evolve_ (golden, same generator seeds)."""
+    from xtrl_amd.evolution import LatentGenePool
+    g = golden('evolve')
+    for case in range(3):
+        islands, per, sel, tourn, steps = (int(x) for x in g[f'c{case}_cfg'])
+        pool = LatentGenePool(dim=8, num_genes_per_island=per, num_selected=sel, tournament_size=tourn,
+                              num_islands=islands, migrate_genes_every=10)
+        pool.genes = torch.from_numpy(g[f'c{case}_genes0'])
+        for s in range(steps):
+            gen = torch.Generator().manual_seed(1000 + 10 * case + s)
+            selected = pool.evolve_(torch.from_numpy(g[f'c{case}_fitnesses'][s]), generator=gen)
+            np.testing.assert_allclose(pool.genes.numpy(), g[f'c{case}_genes'][s], rtol=1e-6, atol=1e-6)
+            np.testing.assert_array_equal(selected.numpy(), g[f'c{case}_selected'][s])
+
+
+@pytest.mark.parametrize('evo,gates,cont', [(False, False, False), (True, True, False), (False, True, True)])
+def test_state_dict_layout_matches_reference_names(evo, gates, cont):
+    from xtrl_amd.model import ModelConfig, WorldModelActorCritic
+    mc = ModelConfig(5, 3, 32, depth=2, evolutionary=evo, dim_gene=8 if evo else 0, continuous=cont,
+                     gate_values=gates, value_residual=gates, learned_mix=gates)
+    ours = WorldModelActorCritic(mc).state_dict()
+    rc = R.ModelConfig(5, 3, 32, depth=2, evolutionary=evo, dim_gene=8 if evo else 0, continuous=cont,
+                       gate_values=gates, value_residual=gates, learned_mix=gates)
+    ref = R.OracleWMAC(rc).state_dict()
+    assert list(ours.keys()) == list(ref.keys())
+    for k in ours:
+        assert ours[k].shape == ref[k].shape, k
+
+
+def test_model_state_dict_loads_golden_reference_weights(golden):
+    """The reference's own WorldModelActorCritic state_dict (golden) loads into the product model."""
+    from xtrl_amd.model import ModelConfig, WorldModelActorCritic
+    g = golden('model_forward')
+    mc = ModelConfig(6, 4, 32, depth=2, evolutionary=True, dim_gene=8, gate_values=True, value_residual=True,
+                     learned_mix=True, reward_range=(-2., 2.))
+    m = WorldModelActorCritic(mc)
+    sd = {k[3:]: torch.from_numpy(g[k]) for k in g.files if k.startswith('sd.')}
+    m.load_state_dict(sd, strict=True)
+
+
+def test_flat_params_views():
+    from xtrl_amd.model import ModelConfig, WorldModelActorCritic
+    from xtrl_amd.params import FlatParams
+    m = WorldModelActorCritic(ModelConfig(5, 2, 16, depth=1))
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    fp = FlatParams(m, 'cpu')
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k])
+    fp.flat.add_(1.)
+    assert torch.equal(m.reward_embed, before['reward_embed'] + 1)
+    (m.reward_embed.sum() * 2).backward()
+    assert torch.equal(fp.grad[:m.reward_embed.numel()], torch.full_like(m.reward_embed, 2.))

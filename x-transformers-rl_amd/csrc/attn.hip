@@ -1,0 +1,404 @@
+// Training attention for the learn step: causal + key-padding mask, softmax in fp32, post-softmax
+// dropout (x-transformers Attend, called from WorldModelActorCritic.forward in Agent.learn,
+// x_transformers_rl.py:928-935 with mask = arange(n) < episode_lens, :908-909).
+//
+// All products run on the f32 matrix cores (v_mfma_f32_16x16x4_f32):
+//   forward   S = Q K^T, online softmax, O = P~ V              (flash style, no n x n in HBM)
+//   backward  D = rowsum(dO * O); dK, dV per key tile; dQ per query tile (no atomics, deterministic)
+// Geometry: 64-row tiles, 4 waves x 16 rows; K/V (or Q/dO) tiles staged in LDS with a 2-float
+// row pad; the probability tile crosses LDS once per wave to turn the MFMA C layout (rows on
+// lane groups) into the A layout (rows on lanes), in a 66-float-stride image (conflict-free read).
+// Dropout keep bits: philox(seed; c0 = i >> 2, c1 = j, c2 = offset + b*H + h) word (i & 3).
+#include "common.h"
+#include "philox.h"
+
+namespace xtrl {
+namespace {
+
+constexpr int TQ = 64, TK = 64, PST = 66;
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, int i, int j) {
+  const u32x4_t r = philox4x32_10((uint32_t)(i >> 2), (uint32_t)j, off, rng_c3(FIELD_DROPOUT, 0), seed);
+  const int w = i & 3;
+  return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
+}
+
+struct AttnArgs {
+  const float *Q, *K, *V, *O, *LSE, *dO, *Dl;
+  float *Oout, *LSEout, *dQ, *dK, *dV, *Dout;
+  const int32_t* lens;
+  int H, n;
+  float scale, inv_keep;
+  uint32_t thresh;    // keep iff word >= thresh (thresh = 0: no dropout)
+  uint64_t seed;
+  uint32_t offset;
+};
+
+// ---------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
+  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
+  __shared__ float Ks[TK][KST], Vs[TK][KST];
+  __shared__ float Ps[4][16][PST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int q0 = blockIdx.x * TQ;
+  const int len = a.lens[b];
+  const int64_t base = (int64_t)bh * n * DH;
+  const int lr = lane & 15, lg = lane >> 4;
+  const uint32_t off = a.offset + (uint32_t)bh;
+
+  float qa[KS];
+  {
+    const int i = q0 + 16 * w + lr;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qa[s] = (i < n) ? a.Q[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
+  }
+  float m[4], l[4];
+  f32x4v o[ND];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+#pragma unroll
+  for (int d = 0; d < ND; ++d) o[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const int last_key = min(min(q0 + TQ - 1, n - 1), len - 1);
+  for (int kt = 0; kt * TK <= last_key; ++kt) {
+    __syncthreads();
+    for (int x = tid; x < TK * DH; x += 256) {
+      const int j = x / DH, c = x - j * DH, jj = kt * TK + j;
+      Ks[j][c] = jj < n ? a.K[base + (int64_t)jj * DH + c] : 0.f;
+      Vs[j][c] = jj < n ? a.V[base + (int64_t)jj * DH + c] : 0.f;
+    }
+    __syncthreads();
+    f32x4v sacc[4];
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      sacc[sub] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) sacc[sub] = mfma16(qa[s], Ks[16 * sub + lr][4 * s + lg], sacc[sub]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = q0 + 16 * w + 4 * lg + r;
+      float sv[4];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const int j = kt * TK + 16 * sub + lr;
+        const bool ok = (j <= i) && (j < len);
+        sv[sub] = ok ? sacc[sub][r] * a.scale : -INFINITY;
+        mx = fmaxf(mx, sv[sub]);
+      }
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o2, 64));
+      const float mnew = fmaxf(m[r], mx);
+      const float alpha = (m[r] == -INFINITY) ? 0.f : expf(m[r] - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const float p = (sv[sub] == -INFINITY) ? 0.f : expf(sv[sub] - mnew);
+        rs += p;
+        float pd = p;
+        if (a.thresh) {
+          const int j = kt * TK + 16 * sub + lr;
+          pd = (keep_word(a.seed, off, i, j) >= a.thresh) ? p * a.inv_keep : 0.f;
+        }
+        Ps[w][4 * lg + r][16 * sub + lr] = pd;
+      }
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) rs += __shfl_xor(rs, o2, 64);
+      l[r] = l[r] * alpha + rs;
+      m[r] = mnew;
+#pragma unroll
+      for (int d = 0; d < ND; ++d) o[d][r] *= alpha;
+    }
+    wave_sync();
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int s = 0; s < TK / 4; ++s) o[d] = mfma16(Ps[w][lr][4 * s + lg], Vs[4 * s + lg][16 * d + lr], o[d]);
+    wave_sync();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q0 + 16 * w + 4 * lg + r;
+    if (i < n) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d) a.Oout[base + (int64_t)i * DH + 16 * d + lr] = o[d][r] / l[r];
+      if (lr == 0) a.LSEout[(int64_t)bh * n + i] = m[r] + logf(l[r]);
+    }
+  }
+}
+
+// D_i = rowsum(dO_i * O_i)
+__global__ void k_attn_delta(const AttnArgs a, int rows, int DH) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int c = 0; c < DH; ++c) s += a.dO[(int64_t)r * DH + c] * a.O[(int64_t)r * DH + c];
+  a.Dout[r] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
+  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
+  __shared__ float Qs[TQ][KST], dOs[TQ][KST];
+  __shared__ float Ls[TQ], Dls[TQ];
+  __shared__ float Ps[4][16][PST], Ds[4][16][PST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int j0 = blockIdx.x * TK;
+  const int len = a.lens[b];
+  const int64_t base = (int64_t)bh * n * DH;
+  const int lr = lane & 15, lg = lane >> 4;
+  const uint32_t off = a.offset + (uint32_t)bh;
+
+  float ka[KS], va[KS];
+  {
+    const int j = j0 + 16 * w + lr;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      ka[s] = (j < n) ? a.K[base + (int64_t)j * DH + 4 * s + lg] : 0.f;
+      va[s] = (j < n) ? a.V[base + (int64_t)j * DH + 4 * s + lg] : 0.f;
+    }
+  }
+  f32x4v dk[ND], dv[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    dk[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+  if (j0 < len) {
+    for (int qt = j0 / TQ; qt * TQ < n; ++qt) {
+      __syncthreads();
+      for (int x = tid; x < TQ * DH; x += 256) {
+        const int i = x / DH, c = x - i * DH, ii = qt * TQ + i;
+        Qs[i][c] = ii < n ? a.Q[base + (int64_t)ii * DH + c] : 0.f;
+        dOs[i][c] = ii < n ? a.dO[base + (int64_t)ii * DH + c] : 0.f;
+      }
+      if (tid < TQ) {
+        const int ii = qt * TQ + tid;
+        Ls[tid] = ii < n ? a.LSE[(int64_t)bh * n + ii] : 0.f;
+        Dls[tid] = ii < n ? a.Dl[(int64_t)bh * n + ii] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        f32x4v st = f32x4v{0.f, 0.f, 0.f, 0.f}, dpt = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          st = mfma16(ka[s], Qs[16 * sub + lr][4 * s + lg], st);
+          dpt = mfma16(va[s], dOs[16 * sub + lr][4 * s + lg], dpt);
+        }
+        const int il = 16 * sub + lr, i = qt * TQ + il;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = j0 + 16 * w + 4 * lg + r;
+          const bool ok = (j <= i) && (j < len) && (i < n);
+          const float p = ok ? expf(st[r] * a.scale - Ls[il]) : 0.f;
+          float z = 1.f;
+          if (a.thresh && ok) z = (keep_word(a.seed, off, i, j) >= a.thresh) ? a.inv_keep : 0.f;
+          Ps[w][4 * lg + r][il] = p * z;
+          Ds[w][4 * lg + r][il] = p * (dpt[r] * z - Dls[il]);
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int s = 0; s < TQ / 4; ++s) {
+          dv[d] = mfma16(Ps[w][lr][4 * s + lg], dOs[4 * s + lg][16 * d + lr], dv[d]);
+          dk[d] = mfma16(Ds[w][lr][4 * s + lg], Qs[4 * s + lg][16 * d + lr], dk[d]);
+        }
+      wave_sync();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = j0 + 16 * w + 4 * lg + r;
+    if (j < n) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        a.dK[base + (int64_t)j * DH + 16 * d + lr] = dk[d][r] * a.scale;
+        a.dV[base + (int64_t)j * DH + 16 * d + lr] = dv[d][r];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
+  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
+  __shared__ float Ks[TK][KST], Vs[TK][KST];
+  __shared__ float Ds[4][16][PST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int q0 = blockIdx.x * TQ;
+  const int len = a.lens[b];
+  const int64_t base = (int64_t)bh * n * DH;
+  const int lr = lane & 15, lg = lane >> 4;
+  const uint32_t off = a.offset + (uint32_t)bh;
+
+  float qa[KS], da[KS];
+  {
+    const int i = q0 + 16 * w + lr;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qa[s] = (i < n) ? a.Q[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
+      da[s] = (i < n) ? a.dO[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
+    }
+  }
+  float lse[4], dl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q0 + 16 * w + 4 * lg + r;
+    lse[r] = i < n ? a.LSE[(int64_t)bh * n + i] : 0.f;
+    dl[r] = i < n ? a.Dl[(int64_t)bh * n + i] : 0.f;
+  }
+  f32x4v dq[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) dq[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  const int last_key = min(min(q0 + TQ - 1, n - 1), len - 1);
+  for (int kt = 0; kt * TK <= last_key; ++kt) {
+    __syncthreads();
+    for (int x = tid; x < TK * DH; x += 256) {
+      const int j = x / DH, c = x - j * DH, jj = kt * TK + j;
+      Ks[j][c] = jj < n ? a.K[base + (int64_t)jj * DH + c] : 0.f;
+      Vs[j][c] = jj < n ? a.V[base + (int64_t)jj * DH + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 4; ++sub) {
+      f32x4v s_ = f32x4v{0.f, 0.f, 0.f, 0.f}, dp = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        s_ = mfma16(qa[s], Ks[16 * sub + lr][4 * s + lg], s_);
+        dp = mfma16(da[s], Vs[16 * sub + lr][4 * s + lg], dp);
+      }
+      const int jl = 16 * sub + lr, j = kt * TK + jl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = q0 + 16 * w + 4 * lg + r;
+        const bool ok = (j <= i) && (j < len) && (i < n);
+        const float p = ok ? expf(s_[r] * a.scale - lse[r]) : 0.f;
+        float z = 1.f;
+        if (a.thresh && ok) z = (keep_word(a.seed, off, i, j) >= a.thresh) ? a.inv_keep : 0.f;
+        Ds[w][4 * lg + r][jl] = p * (dp[r] * z - dl[r]);
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int s = 0; s < TK / 4; ++s) dq[d] = mfma16(Ds[w][lr][4 * s + lg], Ks[4 * s + lg][16 * d + lr], dq[d]);
+    wave_sync();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = q0 + 16 * w + 4 * lg + r;
+    if (i < n) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d) a.dQ[base + (int64_t)i * DH + 16 * d + lr] = dq[d][r] * a.scale;
+    }
+  }
+}
+
+int fill_args(AttnArgs& a, const int32_t* lens, int H, int n, int dh, float scale, float p, uint64_t seed,
+              uint32_t offset) {
+  XTRL_REQUIRE(dh == 16 || dh == 32 || dh == 64, "attn: dim_head %d unsupported (16/32/64)", dh);
+  XTRL_REQUIRE(lens && H > 0 && n > 0, "attn: bad arguments");
+  XTRL_REQUIRE(p >= 0.f && p < 1.f, "attn: dropout %f outside [0, 1)", p);
+  a.lens = lens;
+  a.H = H;
+  a.n = n;
+  a.scale = scale;
+  a.inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const double th = (double)p * 4294967296.0;
+  a.thresh = p > 0.f ? (uint32_t)fmin(th, 4294967295.0) : 0u;
+  if (p > 0.f && a.thresh == 0) a.thresh = 1;
+  a.seed = seed;
+  a.offset = offset;
+  return XTRL_OK;
+}
+
+}  // namespace
+
+int attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o, float* lse, int b, int H,
+             int n, int dh, float scale, float p, uint64_t seed, uint32_t offset, hipStream_t s) {
+  AttnArgs a{};
+  if (int rc = fill_args(a, lens, H, n, dh, scale, p, seed, offset)) return rc;
+  XTRL_REQUIRE(q && k && v && o && lse && b > 0, "attn_fwd: null operand");
+  a.Q = q;
+  a.K = k;
+  a.V = v;
+  a.Oout = o;
+  a.LSEout = lse;
+  dim3 grid((n + TQ - 1) / TQ, b * H);
+  if (dh == 16) hipLaunchKernelGGL(k_attn_fwd<16>, grid, dim3(256), 0, s, a);
+  else if (dh == 32) hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, s, a);
+  XTRL_LAUNCHED("attn_fwd");
+  return XTRL_OK;
+}
+
+int attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o, const float* lse,
+             const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b, int H, int n, int dh,
+             float scale, float p, uint64_t seed, uint32_t offset, hipStream_t s) {
+  AttnArgs a{};
+  if (int rc = fill_args(a, lens, H, n, dh, scale, p, seed, offset)) return rc;
+  XTRL_REQUIRE(q && k && v && o && lse && dout && dq && dk && dv && delta_ws && b > 0, "attn_bwd: null operand");
+  a.Q = q;
+  a.K = k;
+  a.V = v;
+  a.O = o;
+  a.LSE = lse;
+  a.dO = dout;
+  a.Dl = delta_ws;
+  a.Dout = delta_ws;
+  a.dQ = dq;
+  a.dK = dk;
+  a.dV = dv;
+  const int rows = b * H * n;
+  hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, s, a, rows, dh);
+  XTRL_LAUNCHED("attn_delta");
+  dim3 grid((n + TQ - 1) / TQ, b * H);
+  if (dh == 16) {
+    hipLaunchKernelGGL(k_attn_bwd_dkdv<16>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<16>, grid, dim3(256), 0, s, a);
+  } else if (dh == 32) {
+    hipLaunchKernelGGL(k_attn_bwd_dkdv<32>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<32>, grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_dkdv<64>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<64>, grid, dim3(256), 0, s, a);
+  }
+  XTRL_LAUNCHED("attn_bwd");
+  return XTRL_OK;
+}
+
+}  // namespace xtrl
+
+extern "C" int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o,
+                             float* lse, int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
+                             uint32_t offset, void* stream) {
+  return xtrl::attn_fwd(q, k, v, lens, o, lse, b, H, n, dh, scale, dropout_p, seed, offset, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
+                             const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
+                             int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
+                             uint32_t offset, void* stream) {
+  return xtrl::attn_bwd(q, k, v, lens, o, lse, dout, dq, dk, dv, delta_ws, b, H, n, dh, scale, dropout_p, seed,
+                        offset, xtrl::as_stream(stream));
+}

@@ -1,0 +1,42 @@
+// C-ABI housekeeping for libxtrl_hip: version and the per-thread last-error message.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "../../include/xtrl_hip.h"
+#include "philox.h"
+
+namespace xtrl {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return XTRL_E_HIP;
+  }
+  return XTRL_OK;
+}
+
+}  // namespace xtrl
+
+extern "C" int xtrl_abi_version(void) { return XTRL_ABI_VERSION; }
+extern "C" const char* xtrl_last_error(void) { return xtrl::g_err; }
+
+// host-side views of the device random streams (reward-dropout coin, tests)
+extern "C" float xtrl_rng_uniform(uint64_t seed, uint32_t update, uint32_t slot, uint32_t t, uint32_t field,
+                                  uint32_t sub) {
+  return xtrl::rng_uniform(seed, update, slot, t, field, sub);
+}
+extern "C" float xtrl_rng_normal(uint64_t seed, uint32_t update, uint32_t slot, uint32_t t, uint32_t field,
+                                 uint32_t sub) {
+  return xtrl::rng_normal(seed, update, slot, t, field, sub);
+}

@@ -1,0 +1,72 @@
+// Shared device helpers for libxtrl_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/xtrl_hip.h"
+
+namespace xtrl {
+
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ----------------------------------------------------------------------------------------------
+// error reporting (host)
+// ----------------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define XTRL_REQUIRE(cond, ...)                                                                   \
+  do {                                                                                            \
+    if (!(cond)) {                                                                                \
+      ::xtrl::set_error(__VA_ARGS__);                                                             \
+      return XTRL_E_ARG;                                                                          \
+    }                                                                                             \
+  } while (0)
+
+#define XTRL_LAUNCHED(what)                                                                       \
+  do {                                                                                            \
+    int rc__ = ::xtrl::check_launch(what);                                                        \
+    if (rc__) return rc__;                                                                        \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ----------------------------------------------------------------------------------------------
+// wave reductions (64 lanes)
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// LDS hand-off between lanes of ONE wave (no workgroup barrier: waves of a block may have exited)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// activations, written the way PyTorch's CPU kernels evaluate them
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float geluf_(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x)); }
+// torch.lerp(start, end, w): two-branch form
+__device__ __forceinline__ float lerpf_(float s, float e, float w) {
+  return (fabsf(w) < 0.5f) ? s + w * (e - s) : e - (e - s) * (1.0f - w);
+}
+
+}  // namespace xtrl

@@ -1,0 +1,479 @@
+// Fused PPO / critic / world-model / done loss of one learn minibatch, forward and backward.
+//
+// Restates (x_transformers_rl.py):
+//   compute_actor_loss   :413-444   ratio, clipped surrogate, masked advantage normalisation
+//                                   (normalize :103-112), entropy bonus
+//   compute_critic_loss  :446-477   HL-Gauss value / cross-entropy (hl-gauss-pytorch), returns
+//                                   clamped to +-value_clip, "between" zeroing
+//   compute_autoregressive_loss :398-404 (F.gaussian_nll_loss, var clamped 1e-6 without grad)
+//   compute_done_loss    :406-411   (sigmoid + F.binary_cross_entropy, log clamped at -100)
+//   combination          :939-978   ((w_a actor + w_c critic)[mask].mean() + (wm.mean() + done.mean()) w_ar)
+//
+// k_loss_tokens (one wave per token, lanes over the value bins) -> k_loss_reduce (one workgroup:
+// deterministic masked statistics + the per-token actor / critic terms + final scalars) ->
+// k_loss_bwd (one wave per token) writes d/draw_actions, d/dvalues, d/dpred_raw, d/ddone_logit.
+// Gradients follow PyTorch's autograd rules for min (ties split), clamp (inclusive bounds),
+// gaussian_nll_loss (straight-through var clamp) and binary_cross_entropy (eps 1e-12).
+#include "common.h"
+
+namespace xtrl {
+namespace {
+
+constexpr float F32_EPS = 1.1920928955078125e-07f;
+constexpr int NT = XTRL_LOSS_TOK;
+enum Tok { T_ADV = 0, T_V = 1, T_VOLD = 2, T_CEU = 3, T_CEC = 4, T_LP = 5, T_ENT = 6, T_WM = 7, T_BCE = 8, T_ACT = 9 };
+
+// softmax statistics of a B-bin logit row held by a wave (lanes strided over bins)
+struct RowStats {
+  float mx, lse, dot_centers;   // max, log-sum-exp, sum softmax * centres
+};
+
+__device__ RowStats row_stats(const float* x, const float* centers, int B, int lane) {
+  float mx = -INFINITY;
+  for (int k = lane; k < B; k += 64) mx = fmaxf(mx, x[k]);
+  mx = wave_max(mx);
+  float s = 0.f, sc = 0.f;
+  for (int k = lane; k < B; k += 64) {
+    const float e = expf(x[k] - mx);
+    s += e;
+    sc += e * centers[k];
+  }
+  s = wave_sum(s);
+  sc = wave_sum(sc);
+  return {mx, mx + logf(s), sc / s};
+}
+
+// HL-Gauss target bin probability k for target y (already clamped): (cdf[k+1] - cdf[k]) / z
+__device__ __forceinline__ float hl_cdf(const float* support, int k, float y, float inv) {
+  return erff((support[k] - y) * inv);
+}
+
+// cross entropy -sum_k t_k log_softmax(x)_k and (optionally) its gradient softmax * sum(t) - t
+__device__ float hl_ce(const XtrlLossDesc& D, const float* x, float lse, float y, int lane) {
+  const int B = D.B;
+  y = fminf(fmaxf(y, D.lo), D.hi);
+  const float inv = 1.0f / (1.41421356237309505f * D.sigma);
+  const float c0 = hl_cdf(D.support, 0, y, inv), cB = hl_cdf(D.support, B, y, inv);
+  const float z = cB - c0;
+  float acc = 0.f;
+  for (int k = lane; k < B; k += 64) {
+    const float tk = (hl_cdf(D.support, k + 1, y, inv) - hl_cdf(D.support, k, y, inv)) / z;
+    acc += tk * (x[k] - lse);
+  }
+  return -wave_sum(acc);
+}
+
+// discrete policy terms from raw action logits (A <= 32): torch Categorical(probs = softmax)
+struct DiscreteTerms {
+  float p[32];
+  float S;
+  float lp, ent;
+};
+
+__device__ void discrete_terms(const float* raw, int A, int a, DiscreteTerms& T) {
+  float mx = -INFINITY;
+  for (int i = 0; i < A; ++i) mx = fmaxf(mx, raw[i]);
+  float s = 0.f;
+  for (int i = 0; i < A; ++i) {
+    T.p[i] = expf(raw[i] - mx);
+    s += T.p[i];
+  }
+  float S = 0.f;
+  for (int i = 0; i < A; ++i) {
+    T.p[i] = T.p[i] / s;
+    S += T.p[i];
+  }
+  T.S = S;
+  float ent = 0.f;
+  for (int i = 0; i < A; ++i) {
+    const float q = T.p[i] / S;
+    const float lg = logf(fminf(fmaxf(q, F32_EPS), 1.f - F32_EPS));
+    ent += lg * q;
+    if (i == a) T.lp = lg;
+  }
+  T.ent = -ent;
+}
+
+struct ContTerms {
+  float lp, ent;
+};
+
+__device__ void cont_terms(const float* raw, float x, int i, int squash, ContTerms& C) {
+  const float mean = raw[2 * i], lv = raw[2 * i + 1];
+  const float var = expf(tanhf(lv / 3.f) * 3.f);
+  const float sd = sqrtf(fmaxf(var, 1e-5f));
+  float lp = -((x - mean) * (x - mean)) / (2.f * sd * sd) - logf(sd) - 0.91893853320467274f;
+  if (squash) lp -= logf(fmaxf(1.f - x * x, 1e-20f));
+  C.lp = lp;
+  C.ent = squash ? -lp : 0.5f + 0.91893853320467274f + logf(sd);
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
+  const int lane = threadIdx.x & 63;
+  const int tk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int N = D.b * D.n;
+  if (tk >= N) return;
+  const int bi = tk / D.n, ti = tk - bi * D.n;
+  const bool mask = ti < D.lens[bi];
+  float* tok = D.tok + (int64_t)tk * NT;
+  const float* vals = D.values + (int64_t)tk * D.B;
+  const float* ovals = D.old_values + (int64_t)tk * D.B;
+  const RowStats rn = row_stats(vals, D.centers, D.B, lane);
+  const RowStats ro = row_stats(ovals, D.centers, D.B, lane);
+  const float ret = D.returns[tk];
+  const float ceu = hl_ce(D, vals, rn.lse, ret, lane);
+  const float cec = hl_ce(D, vals, rn.lse, fminf(fmaxf(ret, -D.value_clip), D.value_clip), lane);
+  // world model: predictions at t predict the normalised state-with-reward at t + 1
+  float wm = 0.f;
+  if (mask && ti < D.n - 1) {
+    for (int c = lane; c < D.S1; c += 64) {
+      const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
+      const float mean = pr[2 * c];
+      const float var = expf(tanhf(pr[2 * c + 1] / 3.f) * 3.f);
+      const float vv = fmaxf(var, 1e-6f);
+      const float y = D.real[((int64_t)tk + 1) * D.S1 + c];
+      wm += 0.5f * (logf(vv) + (mean - y) * (mean - y) / vv);
+    }
+    wm = wave_sum(wm);
+  }
+  if (lane == 0) {
+    tok[T_ADV] = ret - ro.dot_centers;
+    tok[T_V] = rn.dot_centers;
+    tok[T_VOLD] = ro.dot_centers;
+    tok[T_CEU] = ceu;
+    tok[T_CEC] = cec;
+    if (!D.continuous) {
+      DiscreteTerms T;
+      discrete_terms(D.raw_actions + (int64_t)tk * D.A, D.A, D.actions[tk], T);
+      tok[T_LP] = T.lp;
+      tok[T_ENT] = T.ent;
+    }
+    tok[T_WM] = wm;
+    const float pd = sigmoidf_(D.done_logit[tk]);
+    const float y = D.dones[tk] ? 1.f : 0.f;
+    const float l1 = fmaxf(logf(pd), -100.f), l0 = fmaxf(logf(1.f - pd), -100.f);
+    tok[T_BCE] = -(y * l1 + (1.f - y) * l0);
+  }
+}
+
+// block-wide sum over 1024 threads (deterministic tree)
+__device__ double block_sum(double v, double* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (w == 0) {
+    r = lane < (int)(blockDim.x >> 6) ? sh[lane] : 0.0;
+    r = wave_sum_d(r);
+    if (lane == 0) sh[0] = r;
+  }
+  __syncthreads();
+  r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ float dmin_dr(float r, float adv, float lo, float hi) {
+  const float rc = fminf(fmaxf(r, lo), hi);
+  const float s1 = r * adv, s2 = rc * adv;
+  const float inr = (r >= lo && r <= hi) ? 1.f : 0.f;
+  if (s1 < s2) return adv;
+  if (s1 > s2) return adv * inr;
+  return 0.5f * adv + 0.5f * adv * inr;
+}
+
+__device__ __forceinline__ bool critic_zeroed(float v, float ret, float vold, float clip) {
+  const float lo = vold - clip, hi = vold + clip;
+  return ((ret < v) && (v < lo)) || ((hi < v) && (v < ret));
+}
+
+__global__ __launch_bounds__(1024) void k_loss_reduce(const XtrlLossDesc D) {
+  __shared__ double sh[16];
+  const int N = D.b * D.n;
+  // pass 1: masked counts and sums
+  double n_mask = 0, s_adv = 0, s_ceu = 0, s_cec = 0, s_wm = 0, n_wm = 0, s_bce = 0;
+  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
+    const int bi = tk / D.n, ti = tk - bi * D.n;
+    const float* tok = D.tok + (int64_t)tk * NT;
+    const bool mask = ti < D.lens[bi];
+    s_ceu += tok[T_CEU];
+    s_cec += tok[T_CEC];
+    if (mask) {
+      n_mask += 1;
+      s_adv += tok[T_ADV];
+      s_bce += tok[T_BCE];
+      if (ti < D.n - 1) {
+        s_wm += tok[T_WM];
+        n_wm += D.S1;
+      }
+    }
+  }
+  n_mask = block_sum(n_mask, sh);
+  s_adv = block_sum(s_adv, sh);
+  s_ceu = block_sum(s_ceu, sh);
+  s_cec = block_sum(s_cec, sh);
+  s_wm = block_sum(s_wm, sh);
+  n_wm = block_sum(n_wm, sh);
+  s_bce = block_sum(s_bce, sh);
+  const float adv_mean = (float)(s_adv / n_mask);
+  // pass 2: unbiased variance of the masked advantages
+  double s_var = 0;
+  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
+    const int bi = tk / D.n, ti = tk - bi * D.n;
+    if (ti < D.lens[bi]) {
+      const float dlt = D.tok[(int64_t)tk * NT + T_ADV] - adv_mean;
+      s_var += (double)dlt * dlt;
+    }
+  }
+  s_var = block_sum(s_var, sh);
+  const float var = n_mask > 1 ? (float)(s_var / (n_mask - 1)) : NAN;
+  const float den = sqrtf(fmaxf(var, 1e-5f));
+  const float L = (float)(s_ceu / N), Lc = (float)(s_cec / N);
+  const float lo = 1.f - D.eps_clip, hi = 1.f + D.eps_clip;
+  // pass 3: per-token actor / critic terms
+  double s_actor_all = 0, s_critic_all = 0, s_ac = 0, k_crit = 0;
+  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
+    const int bi = tk / D.n, ti = tk - bi * D.n;
+    float* tok = D.tok + (int64_t)tk * NT;
+    const bool mask = ti < D.lens[bi];
+    const float advn = (tok[T_ADV] - adv_mean) / den;
+    float actor = 0.f;
+    if (!D.continuous) {
+      const float r = expf(tok[T_LP] - D.old_logp[tk]);
+      const float rc = fminf(fmaxf(r, lo), hi);
+      actor = -fminf(r * advn, rc * advn) - D.entropy_weight * tok[T_ENT];
+    } else {
+      for (int i = 0; i < D.A; ++i) {
+        ContTerms C;
+        cont_terms(D.raw_actions + (int64_t)tk * 2 * D.A, D.actions_f[(int64_t)tk * D.A + i], i, D.squash, C);
+        const float r = expf(C.lp - D.old_logp[(int64_t)tk * D.A + i]);
+        const float rc = fminf(fmaxf(r, lo), hi);
+        actor += -fminf(r * advn, rc * advn) - D.entropy_weight * C.ent;
+      }
+    }
+    const bool zero = critic_zeroed(tok[T_V], D.returns[tk], tok[T_VOLD], D.value_clip);
+    float critic;
+    if (D.hl_reduction_mean) critic = zero ? 0.f : fminf(L, Lc);
+    else critic = zero ? 0.f : fminf(tok[T_CEU], tok[T_CEC]);
+    tok[T_ACT] = actor;
+    s_actor_all += actor;
+    s_critic_all += critic;
+    if (mask) {
+      s_ac += actor * D.w_actor + critic * D.w_critic;
+      if (!zero) k_crit += 1;
+    }
+  }
+  s_actor_all = block_sum(s_actor_all, sh);
+  s_critic_all = block_sum(s_critic_all, sh);
+  s_ac = block_sum(s_ac, sh);
+  k_crit = block_sum(k_crit, sh);
+  if (threadIdx.x == 0) {
+    const float wm_mean = (float)(s_wm / n_wm), done_mean = (float)(s_bce / n_mask);
+    float* st = D.stats;
+    st[XTRL_LS_LOSS] = (float)(s_ac / n_mask) + (wm_mean + done_mean) * D.w_autoreg;
+    st[XTRL_LS_ACTOR] = (float)(s_actor_all / N);
+    st[XTRL_LS_CRITIC] = (float)(s_critic_all / N);
+    st[XTRL_LS_AUTOREG] = wm_mean;
+    st[XTRL_LS_DONE] = done_mean;
+    st[XTRL_LS_ADV_MEAN] = adv_mean;
+    st[XTRL_LS_ADV_DEN] = den;
+    st[XTRL_LS_L] = L;
+    st[XTRL_LS_LC] = Lc;
+    st[XTRL_LS_NMASK] = (float)n_mask;
+    st[XTRL_LS_NWM] = (float)n_wm;
+    st[XTRL_LS_KCRIT] = (float)k_crit;
+    const float dmin = D.w_critic * (float)(k_crit / n_mask);
+    st[XTRL_LS_DL] = L < Lc ? dmin : (L > Lc ? 0.f : 0.5f * dmin);
+    st[XTRL_LS_DLC] = Lc < L ? dmin : (Lc > L ? 0.f : 0.5f * dmin);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g) {
+  const int lane = threadIdx.x & 63;
+  const int tk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int N = D.b * D.n;
+  if (tk >= N) return;
+  const int bi = tk / D.n, ti = tk - bi * D.n;
+  const bool mask = ti < D.lens[bi];
+  const float* st = D.stats;
+  const float* tok = D.tok + (int64_t)tk * NT;
+  const float n_mask = st[XTRL_LS_NMASK];
+  const float coef_ac = mask ? g / n_mask : 0.f;
+  const float advn = (tok[T_ADV] - st[XTRL_LS_ADV_MEAN]) / st[XTRL_LS_ADV_DEN];
+  const float lo = 1.f - D.eps_clip, hi = 1.f + D.eps_clip;
+
+  // ---- critic: d/dvalues
+  {
+    const float* x = D.values + (int64_t)tk * D.B;
+    float du, dc;   // weights of the unclipped / clipped CE gradients
+    if (D.hl_reduction_mean) {
+      du = g * st[XTRL_LS_DL] / (float)N;
+      dc = g * st[XTRL_LS_DLC] / (float)N;
+    } else {
+      const bool zero = critic_zeroed(tok[T_V], D.returns[tk], tok[T_VOLD], D.value_clip);
+      const float w = zero ? 0.f : coef_ac * D.w_critic;
+      const float a = tok[T_CEU], b = tok[T_CEC];
+      du = a < b ? w : (a > b ? 0.f : 0.5f * w);
+      dc = b < a ? w : (b > a ? 0.f : 0.5f * w);
+    }
+    const RowStats rn = row_stats(x, D.centers, D.B, lane);
+    const float inv = 1.0f / (1.41421356237309505f * D.sigma);
+    const float yu = fminf(fmaxf(D.returns[tk], D.lo), D.hi);
+    const float yc = fminf(fmaxf(fminf(fmaxf(D.returns[tk], -D.value_clip), D.value_clip), D.lo), D.hi);
+    const float zu = hl_cdf(D.support, D.B, yu, inv) - hl_cdf(D.support, 0, yu, inv);
+    const float zc = hl_cdf(D.support, D.B, yc, inv) - hl_cdf(D.support, 0, yc, inv);
+    // sum_k t_k (= 1 up to rounding) for the exact softmax * sum(t) - t gradient
+    float su = 0.f, sc = 0.f;
+    for (int k = lane; k < D.B; k += 64) {
+      su += (hl_cdf(D.support, k + 1, yu, inv) - hl_cdf(D.support, k, yu, inv)) / zu;
+      sc += (hl_cdf(D.support, k + 1, yc, inv) - hl_cdf(D.support, k, yc, inv)) / zc;
+    }
+    su = wave_sum(su);
+    sc = wave_sum(sc);
+    for (int k = lane; k < D.B; k += 64) {
+      const float p = expf(x[k] - rn.lse);
+      const float tu = (hl_cdf(D.support, k + 1, yu, inv) - hl_cdf(D.support, k, yu, inv)) / zu;
+      const float tc = (hl_cdf(D.support, k + 1, yc, inv) - hl_cdf(D.support, k, yc, inv)) / zc;
+      D.d_values[(int64_t)tk * D.B + k] = du * (p * su - tu) + dc * (p * sc - tc);
+    }
+  }
+
+  // ---- world model: d/dpred_raw (interleaved mean / log-var)
+  {
+    const float coef = (mask && ti < D.n - 1) ? g * D.w_autoreg / st[XTRL_LS_NWM] : 0.f;
+    const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
+    for (int c = lane; c < D.S1; c += 64) {
+      float dm = 0.f, dlv = 0.f;
+      if (coef != 0.f) {
+        const float mean = pr[2 * c], lv = pr[2 * c + 1];
+        const float th = tanhf(lv / 3.f);
+        const float var = expf(th * 3.f);
+        const float vv = fmaxf(var, 1e-6f);
+        const float y = D.real[((int64_t)tk + 1) * D.S1 + c];
+        const float df = mean - y;
+        dm = coef * df / vv;
+        const float dvar = coef * 0.5f * (1.f / vv - df * df / (vv * vv));
+        dlv = dvar * var * (1.f - th * th);
+      }
+      D.d_pred_raw[(int64_t)tk * 2 * D.S1 + 2 * c] = dm;
+      D.d_pred_raw[(int64_t)tk * 2 * D.S1 + 2 * c + 1] = dlv;
+    }
+  }
+
+  if (lane != 0) return;
+  // ---- done: BCE(sigmoid(z), y)
+  {
+    const float coef = mask ? g * D.w_autoreg / n_mask : 0.f;
+    const float p = sigmoidf_(D.done_logit[tk]);
+    const float y = D.dones[tk] ? 1.f : 0.f;
+    const float dp = coef * (p - y) / fmaxf((1.f - p) * p, 1e-12f);
+    D.d_done_logit[tk] = dp * (1.f - p) * p;
+  }
+  // ---- actor: d/draw_actions
+  const float ca = coef_ac * D.w_actor;
+  if (!D.continuous) {
+    const int A = D.A;
+    float* dr = D.d_raw_actions + (int64_t)tk * A;
+    if (ca == 0.f) {
+      for (int i = 0; i < A; ++i) dr[i] = 0.f;
+      return;
+    }
+    DiscreteTerms T;
+    const int a = D.actions[tk];
+    discrete_terms(D.raw_actions + (int64_t)tk * A, A, a, T);
+    const float r = expf(T.lp - D.old_logp[tk]);
+    const float dlp = -dmin_dr(r, advn, lo, hi) * r * ca;   // d tok / d logp
+    const float dent = -D.entropy_weight * ca;               // d tok / d entropy
+    float gq[32];
+    for (int i = 0; i < A; ++i) {
+      const float q = T.p[i] / T.S;
+      const bool inr = (q >= F32_EPS) && (q <= 1.f - F32_EPS);
+      const float lg = logf(fminf(fmaxf(q, F32_EPS), 1.f - F32_EPS));
+      const float dlg = inr ? 1.f / fminf(fmaxf(q, F32_EPS), 1.f - F32_EPS) : 0.f;
+      float gqi = dent * -(lg + q * dlg);
+      if (i == a) gqi += dlp * dlg;
+      gq[i] = gqi;
+    }
+    float sgp = 0.f;
+    for (int i = 0; i < A; ++i) sgp += gq[i] * T.p[i];
+    float gp[32], sg = 0.f;
+    for (int i = 0; i < A; ++i) {
+      gp[i] = gq[i] / T.S - sgp / (T.S * T.S);
+      sg += gp[i] * T.p[i];
+    }
+    for (int i = 0; i < A; ++i) dr[i] = T.p[i] * (gp[i] - sg);
+  } else {
+    const int A = D.A;
+    const float* raw = D.raw_actions + (int64_t)tk * 2 * A;
+    float* dr = D.d_raw_actions + (int64_t)tk * 2 * A;
+    for (int i = 0; i < A; ++i) {
+      if (ca == 0.f) {
+        dr[2 * i] = 0.f;
+        dr[2 * i + 1] = 0.f;
+        continue;
+      }
+      const float x = D.actions_f[(int64_t)tk * A + i];
+      ContTerms C;
+      cont_terms(raw, x, i, D.squash, C);
+      const float r = expf(C.lp - D.old_logp[(int64_t)tk * A + i]);
+      float dlp = -dmin_dr(r, advn, lo, hi) * r * ca;
+      float dsd_extra = 0.f;
+      if (D.squash) dlp += D.entropy_weight * ca;   // entropy = -logp
+      const float mean = raw[2 * i], lv = raw[2 * i + 1];
+      const float th = tanhf(lv / 3.f);
+      const float var = expf(th * 3.f);
+      const float sd = sqrtf(fmaxf(var, 1e-5f));
+      if (!D.squash) dsd_extra = -D.entropy_weight * ca / sd;   // d(-beta * log sd)/d sd
+      const float df = x - mean;
+      const float dmean = dlp * df / (sd * sd);
+      const float dsd = dlp * (df * df / (sd * sd * sd) - 1.f / sd) + dsd_extra;
+      const float dvar = var >= 1e-5f ? dsd * 0.5f / sd : 0.f;
+      dr[2 * i] = dmean;
+      dr[2 * i + 1] = dvar * var * (1.f - th * th);
+    }
+  }
+}
+
+int check(const XtrlLossDesc* D) {
+  XTRL_REQUIRE(D, "loss: null descriptor");
+  XTRL_REQUIRE(D->b > 0 && D->n > 0 && D->A > 0 && D->A <= 32 && D->B > 0 && D->S1 > 0, "loss: bad shape");
+  XTRL_REQUIRE(D->raw_actions && D->values && D->pred_raw && D->done_logit && D->old_logp && D->returns &&
+                   D->old_values && D->dones && D->lens && D->real && D->support && D->centers && D->tok && D->stats,
+               "loss: null operand");
+  XTRL_REQUIRE(D->continuous ? D->actions_f != nullptr : D->actions != nullptr, "loss: null actions");
+  return XTRL_OK;
+}
+
+}  // namespace
+
+int loss_fwd(const XtrlLossDesc* D, hipStream_t s) {
+  if (int rc = check(D)) return rc;
+  const int N = D->b * D->n;
+  hipLaunchKernelGGL(k_loss_tokens, dim3((N + 3) / 4), dim3(256), 0, s, *D);
+  XTRL_LAUNCHED("loss_tokens");
+  hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(1024), 0, s, *D);
+  XTRL_LAUNCHED("loss_reduce");
+  return XTRL_OK;
+}
+
+int loss_bwd(const XtrlLossDesc* D, float g, hipStream_t s) {
+  if (int rc = check(D)) return rc;
+  XTRL_REQUIRE(D->d_raw_actions && D->d_values && D->d_pred_raw && D->d_done_logit, "loss_bwd: null gradient");
+  const int N = D->b * D->n;
+  hipLaunchKernelGGL(k_loss_bwd, dim3((N + 3) / 4), dim3(256), 0, s, *D, g);
+  XTRL_LAUNCHED("loss_bwd");
+  return XTRL_OK;
+}
+
+}  // namespace xtrl
+
+extern "C" int xtrl_loss_fwd(const XtrlLossDesc* desc, void* stream) {
+  return xtrl::loss_fwd(desc, xtrl::as_stream(stream));
+}
+extern "C" int xtrl_loss_bwd(const XtrlLossDesc* desc, float grad_scale, void* stream) {
+  return xtrl::loss_bwd(desc, grad_scale, xtrl::as_stream(stream));
+}

@@ -1,0 +1,154 @@
+// Optimiser path over ONE flat fp32 parameter buffer (every nn.Parameter of the model is a view
+// into it, so clip / step / EMA are three streaming passes instead of ~60 per-tensor launches).
+//
+//   xtrl_grad_norm   clip_grad_norm_ (xtrl.py:987): total L2 norm, clip coefficient
+//                    min(max_norm / (norm + 1e-6), 1)  -> out[0] norm, out[1] coefficient
+//   xtrl_adopt_atan2 AdoptAtan2.step (xtrl.py:749, 991; adam-atan2-pytorch, restated in
+//                    oracle/thirdparty.py) with the clip coefficient folded into the gradient and
+//                    the cautious-mask mean taken per parameter tensor (segment)
+//   xtrl_ema_lerp    EMA post-step update (xtrl.py:747-753; ema-pytorch lerp)
+// All are HBM-bound elementwise passes (16-28 B per parameter).
+#include "common.h"
+
+namespace xtrl {
+namespace {
+
+constexpr int NB = 512;   // partial-sum blocks for the norm
+
+__global__ __launch_bounds__(256) void k_sumsq(const float* g, int64_t n, double* ws) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = g[i];
+    s += v * v;
+  }
+  __shared__ double sh[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__global__ void k_norm_final(const double* ws, int nb, float max_norm, float* out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nb; ++i) s += ws[i];
+  const float norm = (float)sqrt(s);
+  out[0] = norm;
+  out[1] = fminf(max_norm / (norm + 1e-6f), 1.0f);
+}
+
+struct AdoptArgs {
+  float *p, *g, *m, *v, *p_init;
+  int64_t n;
+  const int64_t* seg;
+  int n_seg;
+  int* cnt;
+  const float* clip;
+  float lr, init_lr, beta1, beta2, a, b, wd, regen, cautious;
+  int first;
+};
+
+__device__ __forceinline__ int find_seg(const int64_t* seg, int n_seg, int64_t i) {
+  int lo = 0, hi = n_seg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (seg[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// pass A: regen / weight decay, first-step init, m update, cautious alignment counts
+__global__ __launch_bounds__(256) void k_adopt_a(const AdoptArgs A) {
+  const float coef = A.clip ? A.clip[1] : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * 256) {
+    const float g = A.g[i] * coef;
+    A.g[i] = g;
+    float p = A.p[i];
+    if (A.regen > 0.f && !A.first) p = lerpf_(p, A.p_init[i], A.lr / A.init_lr * A.regen);
+    if (A.wd > 0.f) p = p * (1.f - A.lr * A.wd);
+    A.p[i] = p;
+    if (A.first) {
+      A.m[i] = 0.f;
+      A.v[i] = g * g;
+      if (A.regen > 0.f) A.p_init[i] = p;
+      continue;
+    }
+    const float u = atan2f(g, A.b * sqrtf(A.v[i]));
+    const float m = lerpf_(A.m[i], u, 1.f - A.beta1);
+    A.m[i] = m;
+    if (A.cautious < 1.f && m * g > 0.f) atomicAdd(&A.cnt[find_seg(A.seg, A.n_seg, i)], 1);
+  }
+}
+
+// pass B: p -= lr * a * m * scale; v = lerp(v, g^2, 1 - beta2)
+__global__ __launch_bounds__(256) void k_adopt_b(const AdoptArgs A) {
+  if (A.first) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * 256) {
+    const float g = A.g[i], m = A.m[i];
+    float upd = m;
+    if (A.cautious < 1.f) {
+      const int s = find_seg(A.seg, A.n_seg, i);
+      const double len = (double)(A.seg[s + 1] - A.seg[s]);
+      const double k = (double)A.cnt[s];
+      const float mean = (float)((k + (double)A.cautious * (len - k)) / len);
+      const float sc = (m * g > 0.f) ? 1.f : A.cautious;
+      upd = m * (sc / fmaxf(mean, 1e-5f));
+    }
+    A.p[i] = A.p[i] + (-A.lr) * (upd * A.a);
+    A.v[i] = lerpf_(A.v[i], g * g, 1.f - A.beta2);
+  }
+}
+
+__global__ void k_ema(float* ema, const float* p, int64_t n, float w) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    ema[i] = lerpf_(ema[i], p[i], w);
+}
+
+int grid_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 4096); }
+
+}  // namespace
+
+int grad_norm(const float* g, int64_t n, double* ws, float max_norm, float* out, hipStream_t s) {
+  XTRL_REQUIRE(g && ws && out && n > 0, "grad_norm: bad arguments");
+  hipLaunchKernelGGL(k_sumsq, dim3(NB), dim3(256), 0, s, g, n, ws);
+  hipLaunchKernelGGL(k_norm_final, dim3(1), dim3(64), 0, s, ws, NB, max_norm, out);
+  XTRL_LAUNCHED("grad_norm");
+  return XTRL_OK;
+}
+
+int adopt_atan2(const AdoptArgs& A, hipStream_t s) {
+  XTRL_REQUIRE(A.p && A.g && A.m && A.v && A.n > 0 && A.seg && A.n_seg > 0 && A.cnt, "adopt_atan2: bad arguments");
+  XTRL_REQUIRE(A.regen <= 0.f || A.p_init, "adopt_atan2: regen needs p_init");
+  if (hipMemsetAsync(A.cnt, 0, sizeof(int) * A.n_seg, s) != hipSuccess) return check_launch("adopt_atan2 memset");
+  hipLaunchKernelGGL(k_adopt_a, dim3(grid_for(A.n)), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(k_adopt_b, dim3(grid_for(A.n)), dim3(256), 0, s, A);
+  XTRL_LAUNCHED("adopt_atan2");
+  return XTRL_OK;
+}
+
+int ema_lerp(float* ema, const float* p, int64_t n, float w, hipStream_t s) {
+  XTRL_REQUIRE(ema && p && n > 0, "ema_lerp: bad arguments");
+  hipLaunchKernelGGL(k_ema, dim3(grid_for(n)), dim3(256), 0, s, ema, p, n, w);
+  XTRL_LAUNCHED("ema_lerp");
+  return XTRL_OK;
+}
+
+}  // namespace xtrl
+
+extern "C" int xtrl_grad_norm(const float* g, int64_t n, double* ws, float max_norm, float* out, void* stream) {
+  return xtrl::grad_norm(g, n, ws, max_norm, out, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_adopt_atan2(float* p, float* g, float* m, float* v, float* p_init, int64_t n,
+                                const int64_t* seg_start, int n_seg, int* seg_ws, const float* clip, float lr,
+                                float init_lr, float beta1, float beta2, float a, float b, float weight_decay,
+                                float regen_rate, float cautious, int first_step, void* stream) {
+  xtrl::AdoptArgs A{p,   g,       m,     v,     p_init, n, seg_start, n_seg, seg_ws, clip, lr, init_lr, beta1,
+                    beta2, a, b, weight_decay, regen_rate, cautious, first_step};
+  return xtrl::adopt_atan2(A, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_ema_lerp(float* ema, const float* p, int64_t n, float weight, void* stream) {
+  return xtrl::ema_lerp(ema, p, n, weight, xtrl::as_stream(stream));
+}

@@ -1,0 +1,129 @@
+"""ctypes binding of libxtrl_hip.so (include/xtrl_hip.h).
+
+The library is the product's compute path.  There is no CPU fallback: if the shared object is
+missing or no MI355X is visible, every compute call raises.  ``load()`` itself only needs the file
+(the CPU test-suite checks the exported symbols without running kernels).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
+
+LIB_PATH = Path(__file__).resolve().parent / 'libxtrl_hip.so'
+ABI_VERSION = 1
+
+P = C.c_void_p
+I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
+
+ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
+
+# stats[] slots of the fused loss (XTRL_LS_*)
+LS = dict(loss=0, actor=1, critic=2, autoreg=3, done=4, adv_mean=5, adv_den=6, L=7, Lc=8, nmask=9, nwm=10,
+          kcrit=11, dL=12, dLc=13)
+LOSS_TOK, LOSS_STATS = 10, 32
+
+
+class DecodeLayer(C.Structure):
+    _fields_ = [(n, P) for n in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2',
+                                 'k_cache', 'v_cache')]
+
+
+class RngState(C.Structure):
+    _fields_ = [('seed', U64), ('update', U32), ('slot_offset', U32)]
+
+
+class DecodeDesc(C.Structure):
+    _fields_ = ([(n, I32) for n in ('E', 'S', 'A', 'B', 'd', 'L', 'H', 'dh', 'Tmax', 'G', 'ff', 'in_dim', 'n_qkv',
+                                    'continuous', 'squash', 'evolutionary', 'gate_values', 'value_residual',
+                                    'learned_mix', 'rotary_abs', 'rot_dim', 'sim_mode', 'hazard_log2', 'no_reward_cond')]
+                + [('rs_eps', F32), ('clamp_lo', F32), ('clamp_hi', F32), ('has_clamp', I32)]
+                + [(n, P) for n in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se',
+                                    'ln_final', 'w_h1', 'b_h1', 'w_a2', 'b_a2', 'w_c2', 'b_c2', 'inv_freq')]
+                + [('layers', C.POINTER(DecodeLayer))]
+                + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
+                                    'alive', 'lens', 'cum_reward', 'episode_of_slot', 'rng', 'traj_states',
+                                    'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
+                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1')])
+
+
+class LossDesc(C.Structure):
+    _fields_ = ([(n, I32) for n in ('b', 'n', 'A', 'B', 'S1', 'continuous', 'squash', 'hl_reduction_mean')]
+                + [(n, F32) for n in ('eps_clip', 'value_clip', 'entropy_weight', 'w_actor', 'w_critic', 'w_autoreg',
+                                      'lo', 'hi', 'sigma')]
+                + [(n, P) for n in ('raw_actions', 'values', 'pred_raw', 'done_logit', 'actions', 'actions_f',
+                                    'old_logp', 'returns', 'old_values', 'dones', 'lens', 'real', 'support', 'centers',
+                                    'tok', 'stats', 'd_raw_actions', 'd_values', 'd_pred_raw', 'd_done_logit')])
+
+
+SIGNATURES = {
+    'xtrl_abi_version': (I32, []),
+    'xtrl_last_error': (C.c_char_p, []),
+    'xtrl_gemm_f32': (I32, [P, I32, P, I32, P, P, P, I32, P, I32, P, I64, I32, I32, I32, I32, P]),
+    'xtrl_layernorm_f32': (I32, [P, I32, P, P, I32, I32, I32, P]),
+    'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
+    'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
+    'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P]),
+    'xtrl_attn_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
+    'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P]),
+    'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, P]),
+    'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, P]),
+    'xtrl_loss_fwd': (I32, [C.POINTER(LossDesc), P]),
+    'xtrl_loss_bwd': (I32, [C.POINTER(LossDesc), F32, P]),
+    'xtrl_grad_norm': (I32, [P, I64, P, F32, P, P]),
+    'xtrl_adopt_atan2': (I32, [P, P, P, P, P, I64, P, I32, P, P, F32, F32, F32, F32, F32, F32, F32, F32, F32, I32,
+                               P]),
+    'xtrl_ema_lerp': (I32, [P, P, I64, F32, P]),
+    'xtrl_sim_reset': (I32, [P, I32, I32, U64, U32, P, P]),
+    'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
+    'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
+}
+
+_lib = None
+
+
+def load():
+    """Load and declare the library (no GPU needed)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f'{LIB_PATH} is missing: build it with `make -C x-transformers-rl_amd` '
+                               f'or __graft_entry__.build() (the MI355X path has no CPU fallback)')
+        lib = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        if lib.xtrl_abi_version() != ABI_VERSION:
+            raise RuntimeError(f'libxtrl_hip ABI {lib.xtrl_abi_version()} != {ABI_VERSION}')
+        _lib = lib
+    return _lib
+
+
+def lib():
+    """The library, for a compute call: requires an MI355X."""
+    if not torch.cuda.is_available():
+        raise RuntimeError('xtrl_amd needs a ROCm GPU (gfx950); no CPU fallback exists by design')
+    return load()
+
+
+def check(rc, what=''):
+    if rc != 0:
+        msg = load().xtrl_last_error().decode(errors='replace')
+        raise RuntimeError(f'libxtrl_hip {what} failed (code {rc}): {msg}')
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def rng_uniform(seed, update, slot, t, field, sub=0):
+    return load().xtrl_rng_uniform(seed & 0xFFFFFFFFFFFFFFFF, update, slot, t, field, sub)
+
+
+FIELD_STATE, FIELD_REWARD, FIELD_TERM, FIELD_SAMPLE, FIELD_COIN, FIELD_DROPOUT = 1, 2, 3, 4, 5, 6

@@ -1,0 +1,72 @@
+"""Data-parallel plumbing (replaces x_transformers_rl/distributed.py + HF accelerate's DDP wrap).
+
+One process per GPU, torch.distributed over RCCL (backend "nccl" on ROCm) / gloo on CPU.
+Sharding follows the reference: the (episode, gene) pairs are torch.chunk-ed over processes
+(xtrl.py:1143-1154).  Deliberate deviation: no trajectory all-gather (:868-871) —
+each rank learns on its own episodes and the flat gradient is all-reduced once per optimiser step
+(the DDP gradient all-reduce of :885/:981); RSNorm batch means (:601) and fitnesses (:1362) are
+all-reduced as in the reference.  Everything here works on CPU or GPU tensors."""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_distributed():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def world_and_rank():
+    if not is_distributed():
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
+
+
+class DistContext:
+    """The handful of ``accelerator`` attributes the reference scripts read (train_lander.py:56-59)."""
+
+    def __init__(self, device=None):
+        self.num_processes, self.process_index = world_and_rank()
+        self.is_main_process = self.process_index == 0
+        if device is None:
+            if torch.cuda.is_available():
+                local = int(os.environ.get('LOCAL_RANK', 0))
+                device = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
+            else:
+                device = torch.device('cpu')
+        self.device = torch.device(device)
+
+    def wait_for_everyone(self):
+        if is_distributed():
+            dist.barrier()
+
+
+def shard_pairs(pairs, world, rank):
+    """torch.chunk semantics of xtrl.py:1153 -> (this rank's pairs, index of its first pair)."""
+    n = len(pairs)
+    assert n >= world, 'need at least one (episode, gene) pair per process (xtrl.py:1151)'
+    size = -(-n // world)
+    start = min(rank * size, n)
+    return pairs[start:start + size], start
+
+
+def mean_(t):
+    """In-place mean over ranks (maybe_distributed_mean, distributed.py:34-40)."""
+    if is_distributed():
+        dist.all_reduce(t)
+        t.div_(dist.get_world_size())
+    return t
+
+
+def sum_(t):
+    if is_distributed():
+        dist.all_reduce(t)
+    return t
+
+
+def broadcast_(t, src=0):
+    if is_distributed():
+        dist.broadcast(t, src)
+    return t

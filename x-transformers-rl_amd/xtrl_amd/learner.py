@@ -1,0 +1,470 @@
+"""Learner / Agent with the reference API (x_transformers_rl.py:644-1380), MI355X-native inside.
+
+    learner = Learner(state_dim, num_actions, reward_range, world_model=dict(...), ...)
+    learner(env, num_learning_updates, seed=None, max_timesteps=None)
+    raw_actions, hiddens = learner.agent(state, reward=None, hiddens=None, latent_gene_id=0)
+
+Environments
+  * ``SynthVecSim`` (or anything with ``xtrl_device_sim = True``): the synthetic LunarLander-shaped
+    Sim runs on the device inside the rollout step; all (episode, gene) pairs of an update are
+    rolled out as one vectorised batch (the reference runs them one by one, xtrl.py:1220).
+  * any reference-style env (``reset(seed=?) -> state | (state, ...)``, ``step(action) ->
+    (state, reward, terminated[, truncated, ...])``, xtrl.py:1232-1305): episodes are rolled
+    out one at a time with batch 1, exactly like the reference loop, the policy step still on
+    the device.
+
+Randomness protocol (shared with the oracle, see oracle/ref_port.py):
+  sampling uniforms  philox(seed; slot, t, update, FIELD_SAMPLE)   slot = global pair index
+  minibatch order    torch.randperm with a generator seeded from (seed, update, epoch)
+  reward-drop coin   philox(seed; minibatch, epoch, update, FIELD_COIN)
+  EPO evolve_        private generator seeded from (seed, update, epoch, minibatch)
+"""
+from __future__ import annotations
+
+import copy
+import math
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib as L
+from . import distributed as dist_
+from . import ops
+from .evolution import LatentGenePool, evolve_seed
+from .model import ModelConfig, WorldModelActorCritic
+from .params import FlatParams
+from .rollout import SIM_HOST, SIM_LANDER, SIM_README, RolloutEngine
+
+
+def epoch_permutation(seed, update, epoch, n):
+    g = torch.Generator().manual_seed((int(seed) * 1000003 + int(update)) * 1000003 + int(epoch) & (2 ** 62 - 1))
+    return torch.randperm(n, generator=g)
+
+
+def reward_coin(seed, update, epoch, minibatch, p):
+    if p <= 0.:
+        return True
+    u = L.rng_uniform(int(seed), int(update), int(minibatch), int(epoch), L.FIELD_COIN, 0)
+    return bool(np.float32(u) >= np.float32(p))
+
+
+class SynthVecSim:
+    """Descriptor of the device-resident synthetic Sim (csrc/philox.h, oracle/philox.py):
+    'lander': S-dim N(0,1) states, reward N(0,1) * (1 + 0.1 a), termination hazard 2^-hazard_log2;
+    'readme': the README Sim (N(0,1) states and rewards, never terminates)."""
+
+    xtrl_device_sim = True
+
+    def __init__(self, state_dim, num_actions, mode='lander', hazard_log2=6):
+        assert mode in ('lander', 'readme')
+        self.state_dim, self.num_actions, self.mode, self.hazard_log2 = state_dim, num_actions, mode, hazard_log2
+
+
+# ----------------------------------------------------------------------------------------------
+# Agent (xtrl.py:644-1065)
+# ----------------------------------------------------------------------------------------------
+
+
+class Agent(nn.Module):
+    def __init__(self, state_dim, num_actions, reward_range, epochs, max_timesteps, batch_size, lr, betas, lam,
+                 gamma, beta_s, regen_reg_rate, cautious_factor, eps_clip, value_clip, ema_decay,
+                 continuous_actions=False, squash_continuous=True, critic_pred_num_bins=100, hidden_dim=48,
+                 evolutionary=False, evolve_every=1, evolve_after_step=20,
+                 latent_gene_pool: dict = dict(dim=128, num_genes_per_island=3, num_selected=2, tournament_size=2),
+                 world_model: dict = dict(attn_dim_head=16, heads=4, depth=4, attn_gate_values=True,
+                                          add_value_residual=True, learned_value_residual_mix=True),
+                 dropout=0.25, max_grad_norm=0.5, frac_actor_critic_head_gradient=0.5,
+                 ema_kwargs: dict = dict(update_model_with_ema_every=1250), save_path='./ppo.pt', accelerator=None,
+                 actor_loss_weight=1., critic_loss_weight=1., autoregressive_loss_weight=1.,
+                 # extensions (decision log in DESIGN.md)
+                 reward_dropout=0.5, seed=0, rotary_abs_rollout=False, hl_reduction_mean=True, hl_sigma_ratio=2.0,
+                 device=None):
+        super().__init__()
+        self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
+        dev = self.accelerator.device
+        wm = dict(world_model)
+        known = {'attn_dim_head', 'heads', 'depth', 'attn_gate_values', 'add_value_residual',
+                 'learned_value_residual_mix'}
+        unknown = set(wm) - known
+        if unknown:
+            raise NotImplementedError(f'world_model options {sorted(unknown)} are not supported by the MI355X decoder')
+        self.seed = int(seed)
+        self.evolutionary = evolutionary
+        self.evolve_every, self.evolve_after_step = evolve_every, evolve_after_step
+        self.gene_pool = LatentGenePool(**latent_gene_pool) if evolutionary else None
+        c = ModelConfig(state_dim=state_dim, num_actions=num_actions, dim=hidden_dim, depth=wm.get('depth', 1),
+                        heads=wm.get('heads', 8), dim_head=wm.get('attn_dim_head', 64), num_bins=critic_pred_num_bins,
+                        reward_range=tuple(reward_range), continuous=continuous_actions, squash=squash_continuous,
+                        evolutionary=evolutionary, dim_gene=self.gene_pool.dim_gene if evolutionary else 0,
+                        frac_head_grad=frac_actor_critic_head_gradient, entropy_weight=beta_s, eps_clip=eps_clip,
+                        value_clip=value_clip, dropout=dropout, reward_dropout=reward_dropout,
+                        gate_values=wm.get('attn_gate_values', False), value_residual=wm.get('add_value_residual', False),
+                        learned_mix=wm.get('learned_value_residual_mix', False), rotary_abs_rollout=rotary_abs_rollout,
+                        hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
+        self.cfg = c
+        self.model = WorldModelActorCritic(c).to(dev)
+        self.flat = FlatParams(self.model, dev)
+        # EMA copy (ema-pytorch semantics restated: update_after_step 100, update_every 10, power 2/3)
+        self.ema_model = copy.deepcopy(self.model)
+        for p in self.ema_model.parameters():
+            p.grad = None
+        self.ema_flat = self.flat.flat.clone()
+        self.flat.rebind(self.ema_model, self.ema_flat)
+        self.ema_beta = ema_decay
+        self.ema_update_every, self.ema_update_after = 10, 100
+        self.ema_model_every = (ema_kwargs or {}).get('update_model_with_ema_every', None)
+        self.ema_step, self.ema_initted = 0, False
+        # AdoptAtan2 state over the flat buffer
+        n = self.flat.n
+        self.opt_m = torch.zeros(n, device=dev)
+        self.opt_v = torch.zeros(n, device=dev)
+        self.opt_p_init = torch.zeros(n, device=dev) if regen_reg_rate > 0 else None
+        self.opt_first = True
+        self.opt_cfg = dict(lr=lr, init_lr=lr, betas=tuple(betas), a=1.27, b=1.0, weight_decay=0.,
+                            regen_rate=regen_reg_rate, cautious=cautious_factor)
+        self.seg_ws = torch.zeros(len(self.flat.params), device=dev, dtype=torch.int32)
+        self.norm_ws = torch.zeros(512, device=dev, dtype=torch.float64)
+        self.clip_out = torch.zeros(2, device=dev)
+        self.max_grad_norm = max_grad_norm
+        # RSNorm over [state, reward] (xtrl.py:565-612)
+        self.rs_mean = torch.zeros(state_dim + 1, device=dev)
+        self.rs_var = torch.ones(state_dim + 1, device=dev)
+        self.rs_step = 1
+        self.batch_size, self.epochs = batch_size, epochs
+        self.lam, self.gamma = lam, gamma
+        self.continuous_actions = continuous_actions
+        self.save_path = Path(save_path)
+        self.actor_loss_weight, self.critic_loss_weight = actor_loss_weight, critic_loss_weight
+        self.autoregressive_loss_weight = autoregressive_loss_weight
+        self.step = 0
+        self.logs = []
+        self._deploy = None
+        self._genes_dev = None
+
+    @property
+    def device(self):
+        return self.accelerator.device
+
+    # ---- checkpoint (xtrl.py:792-806) -----------------------------------------------------------
+    def save(self):
+        if not self.accelerator.is_main_process:
+            return
+        torch.save({'model': self.model.state_dict()}, str(self.save_path))
+
+    def load(self):
+        if not self.save_path.exists():
+            return
+        data = torch.load(str(self.save_path), weights_only=True, map_location=self.device)
+        with torch.no_grad():
+            for k, v in data['model'].items():
+                self.model.state_dict()[k].copy_(v)
+
+    # ---- genes ------------------------------------------------------------------------------------
+    def latent(self, gene_ids):
+        return F.normalize(self.genes_device()[gene_ids], dim=-1)
+
+    def genes_device(self):
+        if self._genes_dev is None:
+            self._genes_dev = self.gene_pool.genes.to(self.device)
+        return self._genes_dev
+
+    # ---- EMA (ema-pytorch update(), restated) ---------------------------------------------------------
+    def _ema_update(self):
+        step = self.ema_step
+        self.ema_step += 1
+        if step % self.ema_update_every != 0:
+            return
+        if step <= self.ema_update_after:
+            self.ema_flat.copy_(self.flat.flat)
+            return
+        if not self.ema_initted:
+            self.ema_flat.copy_(self.flat.flat)
+            self.ema_initted = True
+        epoch = max(self.ema_step - self.ema_update_after - 1, 0)
+        decay = 0. if epoch <= 0 else min(max(1 - (1 + epoch) ** (-2 / 3), 0.), self.ema_beta)
+        ops.ema_lerp(self.ema_flat, self.flat.flat, 1. - decay)
+        if self.ema_model_every is not None and step % self.ema_model_every == 0:
+            self.flat.flat.copy_(self.ema_flat)
+
+    # ---- optimiser step: clip_grad_norm_ + AdoptAtan2 + EMA hook (xtrl.py:987-992) ---------------------
+    def optimizer_step(self):
+        ops.grad_norm(self.flat.grad, self.max_grad_norm, self.norm_ws, self.clip_out)
+        o = self.opt_cfg
+        ops.adopt_atan2(self.flat.flat, self.flat.grad, self.opt_m, self.opt_v, self.opt_p_init, self.flat.seg,
+                        self.seg_ws, self.clip_out, lr=o['lr'], init_lr=o['init_lr'], betas=o['betas'], a=o['a'],
+                        b=o['b'], weight_decay=o['weight_decay'], regen_rate=o['regen_rate'], cautious=o['cautious'],
+                        first_step=self.opt_first)
+        self.opt_first = False
+        self._ema_update()
+
+    # ---- learn (xtrl.py:808-1023) -----------------------------------------------------------------
+    def learn(self, traj, episode_lens, gene_ids, fitnesses=None, update=None):
+        """traj: dict of device tensors [N][Tmax][.] (rollout buffers, padded with zeros)."""
+        c, dev = self.cfg, self.device
+        update = self.step if update is None else update
+        lens = episode_lens.to(dev, torch.int32)
+        N = lens.shape[0]
+        n = int(lens.max().item())
+        model = self.model
+        _, returns = ops.hlgauss_gae(traj['values'], traj['rewards'], traj['bounds'], model.hl_centers, n,
+                                     self.gamma, self.lam)
+        states = traj['states'][:, :n]
+        actions = (traj['actions_f'] if c.continuous else traj['actions'])[:, :n]
+        rewards = traj['rewards'][:, :n]
+        old_lp = traj['logp'][:, :n]
+        bounds = traj['bounds'][:, :n]
+        old_values = traj['values'][:, :n]
+        gene_ids = gene_ids.to(dev)
+        rs_mean, rs_var, rs_step = self.rs_mean.clone(), self.rs_var.clone(), self.rs_step
+        model.train()
+        perms = [epoch_permutation(self.seed, update, e, N) for e in range(self.epochs)]
+        perms = torch.stack(perms).to(dev)
+        sd = self.rs_var.sqrt().clamp(min=1e-5)
+        lo, hi = c.reward_range
+        for epoch in range(self.epochs):
+            for mbi, k in enumerate(range(0, N, self.batch_size)):
+                idx = perms[epoch, k:k + self.batch_size]
+                b = idx.shape[0]
+                mb_lens = lens[idx].contiguous()
+                mb_act = actions[idx].contiguous()
+                mb_rew = rewards[idx]
+                prev_act = torch.full_like(mb_act, 0. if c.continuous else -1)
+                prev_act[:, 1:] = mb_act[:, :-1]
+                prev_rew = torch.zeros_like(mb_rew)
+                prev_rew[:, 1:] = mb_rew[:, :-1]
+                swr = (torch.cat((states[idx], prev_rew[..., None]), dim=-1) - self.rs_mean) / sd
+                swr = swr.contiguous()
+                keep = reward_coin(self.seed, update, epoch, mbi, c.reward_dropout)
+                latent = self.latent(gene_ids[idx]) if c.evolutionary else None
+                act_in = prev_act if c.continuous else prev_act.long()
+                nxt = mb_act if c.continuous else mb_act.long()
+                raw, values, pred_raw, done_logit = model.forward_train(
+                    swr[..., :-1], act_in, swr[..., -1], nxt, latent, mb_lens, keep,
+                    attn_seed=self.seed * 1000003 + update, attn_offset=(epoch * 4096 + mbi) * 1024)
+                K = ops.LossConsts(actions=mb_act, old_logp=old_lp[idx].contiguous(), returns=returns[idx].contiguous(),
+                                   old_values=old_values[idx].contiguous(), dones=bounds[idx].contiguous(),
+                                   lens=mb_lens, real=swr, support=model.hl_support, centers=model.hl_centers,
+                                   continuous=c.continuous, squash=c.squash, hl_mean=c.hl_reduction_mean,
+                                   eps_clip=c.eps_clip, value_clip=c.value_clip, entropy_weight=c.entropy_weight,
+                                   w_actor=self.actor_loss_weight, w_critic=self.critic_loss_weight,
+                                   w_autoreg=self.autoregressive_loss_weight, lo=float(lo), hi=float(hi),
+                                   sigma=float(model.hl_sigma))
+                loss, stats = ops.fused_loss(raw, values, pred_raw, done_logit, K)
+                self.flat.zero_grad()
+                loss.backward()
+                dist_.mean_(self.flat.grad)
+                self.optimizer_step()
+                # RSNorm copy update with the normalised masked rows (xtrl.py:1005, 598-610)
+                with torch.no_grad():
+                    mask = (torch.arange(n, device=dev)[None, :] < mb_lens[:, None]).float()
+                    m = (swr * mask[..., None]).sum((0, 1)) / mask.sum()
+                    m = dist_.mean_(m)
+                    t = rs_step
+                    delta = m - rs_mean
+                    rs_mean = rs_mean + delta / t
+                    rs_var = (t - 1) / t * (rs_var + delta ** 2 / t)
+                    rs_step += 1
+                if (c.evolutionary and fitnesses is not None and self.step > self.evolve_after_step
+                        and self.step % self.evolve_every == 0):
+                    g = torch.Generator().manual_seed(evolve_seed(self.seed, update, epoch, mbi))
+                    self.gene_pool.evolve_(fitnesses, generator=g)
+                    self._genes_dev = None
+                self.logs.append(stats)
+        self.rs_mean, self.rs_var, self.rs_step = rs_mean, rs_var, rs_step
+        self.step += 1
+
+    def pop_logs(self):
+        """Per-minibatch dict(loss, actor_loss, critic_loss, autoreg_loss, pred_done_loss)."""
+        if not self.logs:
+            return []
+        s = torch.stack(self.logs).cpu()
+        self.logs = []
+        return [dict(loss=float(r[L.LS['loss']]), actor_loss=float(r[L.LS['actor']]),
+                     critic_loss=float(r[L.LS['critic']]), autoreg_loss=float(r[L.LS['autoreg']]),
+                     pred_done_loss=float(r[L.LS['done']])) for r in s]
+
+    # ---- deploy (xtrl.py:1025-1065): online model, one token per call with a KV cache --------------
+    @torch.no_grad()
+    def forward(self, state, reward=None, hiddens=None, latent_gene_id=0):
+        c = self.cfg
+        if self._deploy is None or self._deploy[1] != self.step:
+            eng = RolloutEngine(self.model, 1, 4096 if c.dim_head == 16 else 1024, sim_mode=SIM_HOST)
+            self._deploy = (eng, self.step)
+        eng = self._deploy[0]
+        eng.pack(self.model, self.rs_mean, self.rs_var)
+        t = 0 if hiddens is None else hiddens['t']
+        if hiddens is not None:
+            for (k, v), (hk, hv) in zip(eng.kv, hiddens['kv']):
+                k.copy_(hk)
+                v.copy_(hv)
+            eng.v1.copy_(hiddens['v1'])
+        state = torch.as_tensor(np.asarray(state), dtype=torch.float32, device=self.device).reshape(1, -1)
+        eng.state.copy_(state)
+        latent = self.latent(torch.tensor([latent_gene_id], device=self.device)) if c.evolutionary else None
+        eng._begin(self.seed, 0, 0, torch.zeros(1, dtype=torch.int32), latent)
+        eng.prev_reward.fill_(0. if reward is None else float(reward))
+        eng.desc.no_reward_cond = int(reward is None)
+        eng.prev_action.fill_(-1)     # the deploy forward passes no actions (xtrl.py:1056-1061)
+        eng.step(t)
+        raw = eng.logits[0].clone()
+        new_h = dict(t=t + 1, kv=[(k.clone(), v.clone()) for k, v in eng.kv], v1=eng.v1.clone())
+        return raw, new_h
+
+
+# ----------------------------------------------------------------------------------------------
+# Learner (xtrl.py:1069-1380)
+# ----------------------------------------------------------------------------------------------
+
+
+class Learner(nn.Module):
+    def __init__(self, state_dim, num_actions, reward_range, world_model: dict, continuous_actions=False,
+                 squash_continuous=True, continuous_actions_clamp=None, evolutionary=False, evolve_every=10,
+                 evolve_after_step=20, latent_gene_pool: dict | None = None, max_timesteps=500, batch_size=8,
+                 num_episodes_per_update=64, lr=0.0008, betas=(0.9, 0.99), lam=0.95, gamma=0.99, eps_clip=0.2,
+                 value_clip=0.4, beta_s=.01, regen_reg_rate=1e-4, cautious_factor=0.1, epochs=4, ema_decay=0.9,
+                 save_every=100, frac_actor_critic_head_gradient=0.5, accelerate_kwargs: dict = dict(),
+                 agent_kwargs: dict = dict(), use_graph=True):
+        super().__init__()
+        assert num_episodes_per_update % batch_size == 0   # xtrl.py:1104
+        self.accelerator = dist_.DistContext(accelerate_kwargs.get('device') if accelerate_kwargs else None)
+        gp = latent_gene_pool if latent_gene_pool is not None else dict(dim=128, num_genes_per_island=3,
+                                                                           num_selected=2, tournament_size=2)
+        self.agent = Agent(state_dim=state_dim, num_actions=num_actions, continuous_actions=continuous_actions,
+                           squash_continuous=squash_continuous, reward_range=reward_range, world_model=world_model,
+                           evolutionary=evolutionary, evolve_every=evolve_every, evolve_after_step=evolve_after_step,
+                           latent_gene_pool=gp, epochs=epochs, max_timesteps=max_timesteps, batch_size=batch_size,
+                           lr=lr, betas=betas, lam=lam, gamma=gamma, beta_s=beta_s, regen_reg_rate=regen_reg_rate,
+                           cautious_factor=cautious_factor, eps_clip=eps_clip, value_clip=value_clip,
+                           ema_decay=ema_decay, frac_actor_critic_head_gradient=frac_actor_critic_head_gradient,
+                           accelerator=self.accelerator, **agent_kwargs)
+        self.num_episodes_per_update = num_episodes_per_update
+        self.max_timesteps = max_timesteps
+        n_genes = self.agent.gene_pool.num_genes if evolutionary else 1
+        self.episode_genes = [(e, g) for e in range(num_episodes_per_update) for g in range(n_genes)]
+        world, rank = self.accelerator.num_processes, self.accelerator.process_index
+        self.episode_genes_for_process, self.slot_offset = dist_.shard_pairs(self.episode_genes, world, rank)
+        self.num_actions, self.continuous_actions = num_actions, continuous_actions
+        self.continuous_actions_clamp = continuous_actions_clamp
+        self.save_every = save_every
+        self.use_graph = use_graph
+        self._engine = None
+        self.last_rollout = None
+
+    @property
+    def device(self):
+        return self.accelerator.device
+
+    # ---- device-sim rollout: all of this rank's (episode, gene) pairs in one batch ----------------
+    def _engine_for(self, env, T):
+        key = (env.mode, env.hazard_log2, T)
+        if self._engine is None or self._engine[0] != key:
+            E = len(self.episode_genes_for_process)
+            mode = SIM_LANDER if env.mode == 'lander' else SIM_README
+            eng = RolloutEngine(self.agent.model, E, T, sim_mode=mode, hazard_log2=env.hazard_log2,
+                                clamp=self.continuous_actions_clamp, use_graph=self.use_graph)
+            self._engine = (key, eng)
+        return self._engine[1]
+
+    def rollout_device(self, env, update, T):
+        agent = self.agent
+        eng = self._engine_for(env, T)
+        eng.pack(agent.ema_model, agent.rs_mean, agent.rs_var)
+        pairs = self.episode_genes_for_process
+        ep = torch.tensor([e for e, _ in pairs], dtype=torch.int32)
+        genes = torch.tensor([g for _, g in pairs], dtype=torch.long, device=self.device)
+        latent = agent.latent(genes) if agent.evolutionary else None
+        traj = eng.run(agent.seed, update, ep, latent, slot_offset=self.slot_offset)
+        return traj, eng.lens, genes, eng.cum_reward
+
+    # ---- host-env rollout (reference loop, batch 1) -----------------------------------------------
+    def rollout_host(self, env, update, T, episode_seeds=None):
+        agent = self.agent
+        c = agent.cfg
+        eng = self._engine_for_host(T)
+        eng.pack(agent.ema_model, agent.rs_mean, agent.rs_var)
+        pairs = self.episode_genes_for_process
+        N, dev = len(pairs), self.device
+        S, A, B = c.state_dim, c.num_actions, c.num_bins
+        out = dict(states=torch.zeros(N, T, S, device=dev), actions=torch.zeros(N, T, dtype=torch.int32, device=dev),
+                   actions_f=torch.zeros(N, T, A, device=dev) if c.continuous else None,
+                   logp=torch.zeros(N, T, A, device=dev) if c.continuous else torch.zeros(N, T, device=dev),
+                   rewards=torch.zeros(N, T, device=dev), bounds=torch.zeros(N, T, dtype=torch.uint8, device=dev),
+                   values=torch.zeros(N, T, B, device=dev))
+        lens = torch.zeros(N, dtype=torch.int32)
+        cum = torch.zeros(N, dtype=torch.float64)
+        genes = torch.tensor([g for _, g in pairs], dtype=torch.long, device=dev)
+
+        def reset(kw):
+            r = env.reset(**kw)
+            return r[0] if isinstance(r, tuple) else r
+
+        def step(action):
+            o = env.step(action.tolist() if hasattr(action, 'tolist') else action)
+            if len(o) >= 4:
+                ns, r, term, trunc = o[:4]
+            elif len(o) == 3:
+                ns, r, term = o
+                trunc = False
+            else:
+                raise RuntimeError('invalid number of returns from environment .step')
+            return ns, float(np.asarray(r).reshape(-1)[0]), bool(term or trunc)
+
+        for i, (episode, gene) in enumerate(pairs):
+            kw = {}
+            if agent.evolutionary and episode_seeds is not None:
+                kw = dict(seed=int(episode_seeds[episode]))
+            latent = agent.latent(torch.tensor([gene], device=dev)) if agent.evolutionary else None
+            traj, n_steps, total = eng.run_host_env(lambda: reset(kw), step, agent.seed, update, latent,
+                                                    slot_offset=self.slot_offset + i, max_steps=T)
+            for k, v in traj.items():
+                if v is not None:
+                    out[k][i].copy_(v[0])
+            lens[i] = n_steps
+            cum[i] = total
+        return out, lens.to(dev), genes, cum
+
+    def _engine_for_host(self, T):
+        key = ('host', T)
+        if self._engine is None or self._engine[0] != key:
+            eng = RolloutEngine(self.agent.model, 1, T, sim_mode=SIM_HOST, clamp=self.continuous_actions_clamp)
+            self._engine = (key, eng)
+        return self._engine[1]
+
+    # ---- fitness per gene in pair order (xtrl.py:1345-1346, 1362) -------------------------------------
+    def fitness(self, cum_reward, genes):
+        agent = self.agent
+        if not agent.evolutionary:
+            return None
+        fit = torch.zeros(agent.gene_pool.num_genes, dtype=torch.float32)
+        for c_, g in zip(cum_reward.cpu().tolist(), genes.cpu().tolist()):
+            fit[g] += np.float32(c_)
+        return dist_.sum_(fit.to(self.device)).cpu()
+
+    def forward(self, env, num_learning_updates: int, seed=None, max_timesteps=None):
+        T = max_timesteps or self.max_timesteps
+        agent = self.agent
+        if seed is not None:
+            torch.manual_seed(seed)
+            np.random.seed(seed)
+            agent.seed = int(seed)
+        device_sim = getattr(env, 'xtrl_device_sim', False)
+        for update in range(num_learning_updates):
+            u = agent.step
+            if device_sim:
+                traj, lens, genes, cum = self.rollout_device(env, u, T)
+            else:
+                seeds = None
+                if agent.evolutionary:
+                    g = torch.Generator().manual_seed(agent.seed * 31 + u)
+                    seeds = torch.randint(0, int(1e7), (self.num_episodes_per_update,), generator=g)
+                traj, lens, genes, cum = self.rollout_host(env, u, T, seeds)
+            self.last_rollout = (traj, lens, genes)
+            self.accelerator.wait_for_everyone()
+            fit = self.fitness(cum, genes)
+            agent.learn(traj, lens, genes, fit, update=u)
+            if update % self.save_every == 0:
+                agent.save()
+        agent.save()

@@ -1,0 +1,221 @@
+"""WorldModelActorCritic for the MI355X learner.
+
+Parameter names and shapes follow the reference state_dict (x_transformers_rl.py:281-392 with the
+x-transformers ContinuousTransformerWrapper/Decoder inside), so checkpoints interchange with
+``Agent.save`` / ``Agent.load`` of the reference (xtrl.py:792-806).
+
+Compute: the rollout never calls this module — it runs the packed weights through
+libxtrl_hip's decode step (rollout.py).  The learn step (``forward_train``) keeps PyTorch autograd
+for the dense layers and routes the attention core through the HIP flash kernel (ops.attention)
+and the losses through the fused HIP loss (ops.fused_loss).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import ops
+
+
+@dataclass
+class ModelConfig:
+    state_dim: int
+    num_actions: int
+    dim: int = 48
+    depth: int = 1
+    heads: int = 4
+    dim_head: int = 16
+    num_bins: int = 100
+    reward_range: tuple = (-1., 1.)
+    continuous: bool = False
+    squash: bool = True
+    evolutionary: bool = False
+    dim_gene: int = 0
+    frac_head_grad: float = 0.5
+    entropy_weight: float = 0.01
+    eps_clip: float = 0.2
+    value_clip: float = 0.4
+    dropout: float = 0.25
+    reward_dropout: float = 0.5
+    gate_values: bool = False
+    value_residual: bool = False
+    learned_mix: bool = False
+    ff_mult: int = 4
+    rotary_abs_rollout: bool = False     # decision log: reference semantics = rotary position 0 in rollout
+    hl_reduction_mean: bool = True       # decision log: hl-gauss-pytorch default reduction
+    hl_sigma_ratio: float = 2.0
+
+    @property
+    def inner(self):
+        return self.heads * self.dim_head
+
+    @property
+    def in_dim(self):
+        return self.dim * (3 if self.evolutionary else 2)
+
+
+class XLayerNorm(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.gamma = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return F.layer_norm(x, (self.dim,), eps=1e-5) * self.gamma
+
+
+class XAttention(nn.Module):
+    def __init__(self, c: ModelConfig, mix: bool):
+        super().__init__()
+        d, inner = c.dim, c.inner
+        self.to_q = nn.Linear(d, inner, bias=False)
+        self.to_k = nn.Linear(d, inner, bias=False)
+        self.to_v = nn.Linear(d, inner, bias=False)
+        self.to_out = nn.Linear(inner, d, bias=False)
+        self.to_v_gate = None
+        if c.gate_values:
+            self.to_v_gate = nn.Linear(d, inner)
+            nn.init.constant_(self.to_v_gate.weight, 0.)
+            nn.init.constant_(self.to_v_gate.bias, 10.)
+        self.to_value_residual_mix = None
+        if mix:
+            self.to_value_residual_mix = nn.Sequential(nn.Linear(d, c.heads))
+            nn.init.zeros_(self.to_value_residual_mix[0].weight)
+            nn.init.zeros_(self.to_value_residual_mix[0].bias)
+
+
+class XFeedForward(nn.Module):
+    def __init__(self, c: ModelConfig):
+        super().__init__()
+        inner = c.dim * c.ff_mult
+        self.ff = nn.Sequential(nn.Sequential(nn.Linear(c.dim, inner), nn.GELU()), nn.Dropout(c.dropout),
+                                nn.Linear(inner, c.dim))
+
+
+class _Residual(nn.Module):
+    pass
+
+
+class XDecoder(nn.Module):
+    def __init__(self, c: ModelConfig):
+        super().__init__()
+        self.dim = c.dim
+        self.layers = nn.ModuleList()
+        for ind in range(c.depth):
+            mix = c.value_residual and c.learned_mix and ind > 0
+            self.layers.append(nn.ModuleList([nn.ModuleList([XLayerNorm(c.dim), None, None]), XAttention(c, mix),
+                                              _Residual()]))
+            self.layers.append(nn.ModuleList([nn.ModuleList([XLayerNorm(c.dim), None, None]), XFeedForward(c),
+                                              _Residual()]))
+        self.rotary_pos_emb = nn.Module()
+        rot = c.dim_head // 2
+        self.rotary_pos_emb.register_buffer('inv_freq', 1. / (10000 ** (torch.arange(0, rot, 2).float() / rot)))
+        self.final_norm = XLayerNorm(c.dim)
+
+
+class XTransformer(nn.Module):
+    def __init__(self, c: ModelConfig):
+        super().__init__()
+        self.attn_layers = XDecoder(c)
+        self.project_in = nn.Linear(c.state_dim, c.dim, bias=False)
+
+
+def _rotate_half(x):
+    x = x.reshape(*x.shape[:-1], -1, 2)
+    x1, x2 = x.unbind(-1)
+    return torch.stack((-x2, x1), dim=-1).reshape(*x.shape[:-2], -1)
+
+
+class WorldModelActorCritic(nn.Module):
+    def __init__(self, c: ModelConfig):
+        super().__init__()
+        d = c.dim
+        self.cfg = c
+        self.transformer = XTransformer(c)
+        self.reward_embed = nn.Parameter(torch.ones(d) * 1e-2)
+        if c.continuous:
+            self.action_embeds = nn.Linear(c.num_actions, d)
+        else:
+            self.action_embeds = nn.Module()
+            self.action_embeds.embed = nn.Embedding(c.num_actions, d)
+        self.to_state_embed = nn.Linear(c.state_dim, d)
+        self.to_pred_done = nn.Sequential(nn.Linear(2 * d, 1))
+        self.to_pred = nn.Sequential(nn.Linear(2 * d, d), nn.SiLU(), nn.Linear(d, 2 * (c.state_dim + 1)))
+        if c.evolutionary:
+            self.latent_to_embed = nn.Linear(c.dim_gene, d)
+        n_out = c.num_actions * (2 if c.continuous else 1)
+        self.critic_head = nn.Sequential(nn.Linear(c.in_dim, 2 * d), nn.SiLU(), nn.Linear(2 * d, c.num_bins))
+        self.action_head = nn.Sequential(nn.Linear(c.in_dim, 2 * d), nn.SiLU(), nn.Linear(2 * d, n_out))
+        lo, hi = c.reward_range
+        support = torch.linspace(lo, hi, c.num_bins + 1, dtype=torch.float32)
+        self.register_buffer('hl_support', support, persistent=False)
+        self.register_buffer('hl_centers', (support[:-1] + support[1:]) / 2, persistent=False)
+        self.hl_sigma = c.hl_sigma_ratio * (hi - lo) / c.num_bins
+
+    # ---- pieces shared with the rollout weight packing -----------------------------------------
+    def blocks(self):
+        layers = self.transformer.attn_layers.layers
+        return [(layers[2 * i], layers[2 * i + 1]) for i in range(len(layers) // 2)]
+
+    def embed_actions(self, actions):
+        if self.cfg.continuous:
+            return self.action_embeds(actions)
+        has = actions >= 0
+        emb = F.embedding(torch.where(has, actions, torch.zeros_like(actions)), self.action_embeds.embed.weight)
+        return emb * has[..., None].to(emb.dtype)
+
+    def hl_value(self, logits):
+        return (logits.softmax(dim=-1) * self.hl_centers).sum(-1)
+
+    # ---- learn-step forward (xtrl.py:479-559 with the mask path of x-transformers) --------------
+    def forward_train(self, state, actions, rewards, next_actions, latent_gene, lens, reward_keep=True,
+                      attn_seed=0, attn_offset=0):
+        c = self.cfg
+        b, n, _ = state.shape
+        tr = self.transformer
+        state_embed = self.to_state_embed(state)
+        sum_embeds = self.embed_actions(actions) + rewards[..., None] * self.reward_embed * float(reward_keep)
+        x = tr.project_in(state) + sum_embeds
+        H, dh = c.heads, c.dim_head
+        pos = torch.arange(n, device=state.device, dtype=torch.float32)
+        inv = tr.attn_layers.rotary_pos_emb.inv_freq
+        freqs = (pos[:, None] * inv[None, :]).repeat_interleave(2, dim=-1)
+        cos, sin = freqs.cos(), freqs.sin()
+        rot = freqs.shape[-1]
+        p_drop = c.dropout if self.training else 0.
+        first_v = None
+        for li, (attn_l, ff_l) in enumerate(self.blocks()):
+            (ln_a, _, _), blk, _ = attn_l
+            xn = ln_a(x)
+            split = lambda t: t.reshape(b, n, H, dh).permute(0, 2, 1, 3)
+            q, k, v = split(blk.to_q(xn)), split(blk.to_k(xn)), split(blk.to_v(xn))
+            orig_v = v
+            if c.value_residual and first_v is not None and blk.to_value_residual_mix is not None:
+                mix = torch.sigmoid(blk.to_value_residual_mix[0](xn)).permute(0, 2, 1)[..., None]
+                v = v.lerp(first_v, mix)
+            if first_v is None:
+                first_v = orig_v
+            q = torch.cat((q[..., :rot] * cos + _rotate_half(q[..., :rot]) * sin, q[..., rot:]), dim=-1)
+            k = torch.cat((k[..., :rot] * cos + _rotate_half(k[..., :rot]) * sin, k[..., rot:]), dim=-1)
+            o = ops.attention(q, k, v, lens, dh ** -0.5, p_drop, attn_seed, attn_offset + li * 65536)
+            o = o.permute(0, 2, 1, 3).reshape(b, n, H * dh)
+            if blk.to_v_gate is not None:
+                o = o * blk.to_v_gate(xn).sigmoid()
+            x = blk.to_out(o) + x
+            (ln_f, _, _), ffb, _ = ff_l
+            x = ffb.ff(ln_f(x)) + x
+        embed = tr.attn_layers.final_norm(x)
+        ewa = torch.cat((embed, self.embed_actions(next_actions)), dim=-1)
+        pred_raw = self.to_pred(ewa)
+        done_logit = self.to_pred_done(ewa)[..., 0]
+        f = c.frac_head_grad
+        embed = embed.detach() * (1. - f) + embed * f
+        ac_in = torch.cat((embed, state_embed), dim=-1)
+        if c.evolutionary:
+            lat = self.latent_to_embed(latent_gene)
+            ac_in = torch.cat((ac_in, lat[:, None, :].expand(-1, n, -1)), dim=-1)
+        return self.action_head(ac_in), self.critic_head(ac_in), pred_raw, done_logit

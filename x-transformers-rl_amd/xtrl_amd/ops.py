@@ -1,0 +1,199 @@
+"""Torch-facing wrappers of the HIP kernels (autograd Functions for the learn step).
+
+Every op checks shapes on the host before launching (the kernels assume them) and runs on the
+current torch stream.  No op has a CPU implementation."""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+
+
+def _f32c(t):
+    assert t.dtype == torch.float32 and t.is_cuda and t.is_contiguous(), (t.dtype, t.device, t.shape)
+    return t
+
+
+# --------------------------------------------------------------------------------------------
+# GEMM / LayerNorm
+# --------------------------------------------------------------------------------------------
+
+
+def gemm(x, w, bias=None, ln_gamma=None, residual=None, act=L.ACT_NONE, out=None):
+    """act(LN?(x) @ w.T + bias) (+ residual) on the f32 MFMA path.  x [M, K] (row stride may
+    exceed K), w [N, K] contiguous."""
+    lib = L.lib()
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and x.stride(1) == 1 and w.is_contiguous()
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    if bias is not None:
+        assert bias.shape == (N,) and bias.is_contiguous()
+    if ln_gamma is not None:
+        assert ln_gamma.shape == (K,)
+    if residual is not None:
+        assert residual.shape == (M, N) and residual.stride(1) == 1
+    L.check(lib.xtrl_gemm_f32(L.ptr(x), x.stride(0), L.ptr(w), K, L.ptr(bias), L.ptr(ln_gamma), L.ptr(residual),
+                              residual.stride(0) if residual is not None else 0, L.ptr(out), out.stride(0), None, 0,
+                              M, N, K, act, L.stream()), 'gemm')
+    return out
+
+
+def layernorm(x, gamma, out=None):
+    lib = L.lib()
+    M, D = x.shape
+    if out is None:
+        out = torch.empty(M, D, device=x.device, dtype=torch.float32)
+    L.check(lib.xtrl_layernorm_f32(L.ptr(x), x.stride(0), L.ptr(gamma), L.ptr(out), out.stride(0), M, D,
+                                   L.stream()), 'layernorm')
+    return out
+
+
+# --------------------------------------------------------------------------------------------
+# training attention
+# --------------------------------------------------------------------------------------------
+
+
+class AttentionFn(torch.autograd.Function):
+    """softmax(q k^T * scale + causal/key-padding mask) with post-softmax dropout, times v."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, lens, scale, dropout_p, seed, offset):
+        lib = L.lib()
+        b, H, n, dh = q.shape
+        for t in (q, k, v):
+            _f32c(t)
+            assert t.shape == (b, H, n, dh)
+        assert lens.dtype == torch.int32 and lens.shape == (b,)
+        o = torch.empty_like(q)
+        lse = torch.empty(b, H, n, device=q.device, dtype=torch.float32)
+        L.check(lib.xtrl_attn_fwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), b, H, n, dh,
+                                  float(scale), float(dropout_p), int(seed), int(offset), L.stream()), 'attn_fwd')
+        ctx.save_for_backward(q, k, v, lens, o, lse)
+        ctx.cfg = (float(scale), float(dropout_p), int(seed), int(offset))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        lib = L.lib()
+        q, k, v, lens, o, lse = ctx.saved_tensors
+        scale, p, seed, offset = ctx.cfg
+        b, H, n, dh = q.shape
+        do = do.contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty(b, H, n, device=q.device, dtype=torch.float32)
+        L.check(lib.xtrl_attn_bwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), L.ptr(do),
+                                  L.ptr(dq), L.ptr(dk), L.ptr(dv), L.ptr(delta), b, H, n, dh, scale, p, seed, offset,
+                                  L.stream()), 'attn_bwd')
+        return dq, dk, dv, None, None, None, None, None
+
+
+def attention(q, k, v, lens, scale, dropout_p=0., seed=0, offset=0):
+    return AttentionFn.apply(q.contiguous(), k.contiguous(), v.contiguous(), lens, scale, dropout_p, seed, offset)
+
+
+# --------------------------------------------------------------------------------------------
+# fused PPO / critic / world-model / done loss
+# --------------------------------------------------------------------------------------------
+
+
+class LossConsts:
+    """Per-minibatch constant tensors + hyper-parameters of the fused loss."""
+
+    def __init__(self, *, actions, old_logp, returns, old_values, dones, lens, real, support, centers, continuous,
+                 squash, hl_mean, eps_clip, value_clip, entropy_weight, w_actor, w_critic, w_autoreg, lo, hi, sigma):
+        self.__dict__.update(locals())
+        del self.__dict__['self']
+
+
+class LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, raw_actions, values, pred_raw, done_logit, K: LossConsts):
+        lib = L.lib()
+        b, n, B = values.shape
+        S1 = K.real.shape[-1]
+        A = K.old_logp.shape[-1] if K.continuous else raw_actions.shape[-1]
+        raw_actions, values, pred_raw, done_logit = (t.contiguous() for t in (raw_actions, values, pred_raw, done_logit))
+        assert pred_raw.shape == (b, n, 2 * S1) and done_logit.shape == (b, n)
+        assert raw_actions.shape == (b, n, 2 * A if K.continuous else A)
+        dev = values.device
+        tok = torch.empty(b, n, L.LOSS_TOK, device=dev, dtype=torch.float32)
+        stats = torch.zeros(L.LOSS_STATS, device=dev, dtype=torch.float32)
+        d = L.LossDesc(b=b, n=n, A=A, B=B, S1=S1, continuous=int(K.continuous), squash=int(K.squash),
+                       hl_reduction_mean=int(K.hl_mean), eps_clip=K.eps_clip, value_clip=K.value_clip,
+                       entropy_weight=K.entropy_weight, w_actor=K.w_actor, w_critic=K.w_critic,
+                       w_autoreg=K.w_autoreg, lo=K.lo, hi=K.hi, sigma=K.sigma)
+        keep = [raw_actions, values, pred_raw, done_logit, tok, stats]
+        fields = dict(raw_actions=raw_actions, values=values, pred_raw=pred_raw, done_logit=done_logit,
+                      actions=None if K.continuous else K.actions, actions_f=K.actions if K.continuous else None,
+                      old_logp=K.old_logp, returns=K.returns, old_values=K.old_values, dones=K.dones, lens=K.lens,
+                      real=K.real, support=K.support, centers=K.centers, tok=tok, stats=stats)
+        for name, t in fields.items():
+            if t is not None:
+                assert t.is_cuda and t.is_contiguous(), name
+                setattr(d, name, t.data_ptr())
+        L.check(lib.xtrl_loss_fwd(C.byref(d), L.stream()), 'loss_fwd')
+        ctx.desc = d
+        ctx.keep = keep + [K]
+        ctx.shapes = (raw_actions.shape, values.shape, pred_raw.shape, done_logit.shape)
+        ctx.mark_non_differentiable(stats)
+        return stats[L.LS['loss']].clone(), stats
+
+    @staticmethod
+    def backward(ctx, gloss, gstats):
+        lib = L.lib()
+        d = ctx.desc
+        sa, sv, sp, sd = ctx.shapes
+        dev = gloss.device
+        g_raw = torch.empty(sa, device=dev, dtype=torch.float32)
+        g_val = torch.empty(sv, device=dev, dtype=torch.float32)
+        g_pred = torch.empty(sp, device=dev, dtype=torch.float32)
+        g_done = torch.empty(sd, device=dev, dtype=torch.float32)
+        d.d_raw_actions, d.d_values, d.d_pred_raw, d.d_done_logit = (t.data_ptr() for t in (g_raw, g_val, g_pred, g_done))
+        # the upstream gradient is 1 for loss.backward(); a different scalar is folded in afterwards
+        L.check(lib.xtrl_loss_bwd(C.byref(d), 1.0, L.stream()), 'loss_bwd')
+        if not (isinstance(gloss, torch.Tensor) and gloss.numel() == 1):
+            raise RuntimeError('fused loss expects a scalar upstream gradient')
+        s = gloss.reshape(())
+        return g_raw * s, g_val * s, g_pred * s, g_done * s, None
+
+
+def fused_loss(raw_actions, values, pred_raw, done_logit, consts: LossConsts):
+    return LossFn.apply(raw_actions, values, pred_raw, done_logit, consts)
+
+
+# --------------------------------------------------------------------------------------------
+# HL-Gauss + GAE, optimiser
+# --------------------------------------------------------------------------------------------
+
+
+def hlgauss_gae(logits, rewards, bounds, centers, n, gamma, lam):
+    """logits [E, T, B] (uses [:, :n]), rewards / bounds [E, T] -> (values, returns) [E, n]."""
+    lib = L.lib()
+    E, T, B = logits.shape
+    assert rewards.shape == (E, T) and bounds.shape == (E, T) and bounds.dtype == torch.uint8 and n <= T
+    values = torch.empty(E, n, device=logits.device, dtype=torch.float32)
+    returns = torch.empty_like(values)
+    gl = float(torch.tensor(gamma * lam, dtype=torch.float32))
+    L.check(lib.xtrl_hlgauss_gae(L.ptr(logits), T * B, L.ptr(rewards), L.ptr(bounds), T, L.ptr(centers),
+                                 L.ptr(values), L.ptr(returns), E, n, B, float(gamma), gl, L.stream()), 'hlgauss_gae')
+    return values, returns
+
+
+def grad_norm(flat_grad, max_norm, ws, out):
+    L.check(L.lib().xtrl_grad_norm(L.ptr(flat_grad), flat_grad.numel(), L.ptr(ws), float(max_norm), L.ptr(out),
+                                   L.stream()), 'grad_norm')
+
+
+def adopt_atan2(p, g, m, v, p_init, seg, seg_ws, clip, *, lr, init_lr, betas, a, b, weight_decay, regen_rate,
+                cautious, first_step):
+    L.check(L.lib().xtrl_adopt_atan2(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_init), p.numel(), L.ptr(seg),
+                                     seg.numel() - 1, L.ptr(seg_ws), L.ptr(clip), lr, init_lr, betas[0], betas[1], a, b,
+                                     weight_decay, regen_rate, cautious, int(first_step), L.stream()), 'adopt_atan2')
+
+
+def ema_lerp(ema, p, weight):
+    L.check(L.lib().xtrl_ema_lerp(L.ptr(ema), L.ptr(p), p.numel(), float(weight), L.stream()), 'ema_lerp')

@@ -1,0 +1,219 @@
+"""Device-resident vectorised rollout (replaces Learner.forward's batch-1 loop, xtrl.py:1204-1356).
+
+One ``RolloutEngine`` owns, for a fixed (E envs x Tmax steps) shape:
+  * packed decode weights (refreshed from the EMA model once per learning update — the rollout
+    policy is constant for the whole update, xtrl.py:1194),
+  * per-layer KV caches [E][H][Tmax][dh], env state, trajectory buffers [E][Tmax][.],
+  * the ctypes ``XtrlDecodeDesc`` pointing at all of them.
+``run()`` drives ``xtrl_decode_step`` for t = 0..Tmax-1, either eagerly or by replaying a captured
+hipGraph of the whole rollout (the graph is reusable across updates because every buffer is
+persistent and the seed / update index live in device memory).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib as L
+from .model import WorldModelActorCritic
+
+SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
+
+
+class RolloutEngine:
+    def __init__(self, model: WorldModelActorCritic, E: int, Tmax: int, *, sim_mode=SIM_LANDER, hazard_log2=6,
+                 clamp=None, use_graph=False):
+        c = model.cfg
+        dev = next(model.parameters()).device
+        self.c, self.E, self.T, self.dev = c, E, Tmax, dev
+        self.sim_mode, self.use_graph = sim_mode, use_graph
+        d, H, dh, S, A, B = c.dim, c.heads, c.dim_head, c.state_dim, c.num_actions, c.num_bins
+        I = H * dh
+        self.n_qkv = 3 * I + (I if c.gate_values else 0) + (H if (c.value_residual and c.learned_mix) else 0)
+        ff = d * c.ff_mult
+        nA = 2 * A if c.continuous else A
+        f32, i32, u8 = torch.float32, torch.int32, torch.uint8
+        z = lambda *s, dt=f32: torch.zeros(*s, device=dev, dtype=dt)
+        # env / episode state
+        self.state, self.prev_action, self.prev_action_f = z(E, S), z(E, dt=i32), z(E, A)
+        self.prev_reward, self.alive, self.lens = z(E), z(E, dt=u8), z(E, dt=i32)
+        self.cum_reward = z(E, dt=torch.float64)
+        self.episode_of_slot = z(E, dt=i32)
+        self.rng = z(2, dt=torch.int64)
+        # trajectory
+        self.traj = dict(states=z(E, Tmax, S), actions=z(E, Tmax, dt=i32), actions_f=z(E, Tmax, A) if c.continuous else None,
+                         logp=z(E, Tmax, A) if c.continuous else z(E, Tmax), rewards=z(E, Tmax),
+                         bounds=z(E, Tmax, dt=u8), values=z(E, Tmax, B))
+        # scratch
+        self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
+        self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
+        self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
+        # packed weights
+        self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
+                      act_emb_b=z(d) if c.continuous else None, reward_embed=z(d), w_se=z(d, S), b_se=z(d),
+                      ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_a2=z(nA, 2 * d), b_a2=z(nA),
+                      w_c2=z(B, 2 * d), b_c2=z(B), inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
+        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), ln_ff=z(d),
+                        w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+        self.w_lat = None
+        self._build_desc(clamp, hazard_log2)
+        self.graph = None
+
+    # ------------------------------------------------------------------------------------------
+    def _build_desc(self, clamp, hazard_log2):
+        c, p = self.c, L.ptr
+        layers = (L.DecodeLayer * c.depth)()
+        for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
+            layers[i] = L.DecodeLayer(*(p(w[k]) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
+                                                          'b_ff1', 'w_ff2', 'b_ff2')), p(kc), p(vc))
+        self._layers = layers
+        D = L.DecodeDesc()
+        D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (self.E, c.state_dim, c.num_actions, c.num_bins, c.dim,
+                                                           c.depth, c.heads, c.dim_head, self.T)
+        D.G, D.ff, D.in_dim, D.n_qkv = c.dim_gene, c.dim * c.ff_mult, c.in_dim, self.n_qkv
+        D.continuous, D.squash, D.evolutionary = int(c.continuous), int(c.squash), int(c.evolutionary)
+        D.gate_values, D.value_residual, D.learned_mix = int(c.gate_values), int(c.value_residual), int(c.learned_mix)
+        D.rotary_abs, D.rot_dim = int(c.rotary_abs_rollout), c.dim_head // 2
+        D.sim_mode, D.hazard_log2, D.rs_eps = self.sim_mode, hazard_log2, 1e-5
+        if clamp is not None:
+            D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
+        w = self.w
+        for k in ('w_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1', 'w_a2',
+                  'b_a2', 'w_c2', 'b_c2', 'inv_freq', 'rs_mean', 'rs_var'):
+            setattr(D, k, w[k].data_ptr() if w[k] is not None else None)
+        D.b_pin = None
+        D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
+        for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
+                  'episode_of_slot'):
+            setattr(D, k, getattr(self, k).data_ptr())
+        D.rng = self.rng.data_ptr()
+        for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
+            t = self.traj[k]
+            setattr(D, 'traj_' + k, t.data_ptr() if t is not None else None)
+        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1'):
+            setattr(D, k, getattr(self, k).data_ptr())
+        self.desc = D
+
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def pack(self, model: WorldModelActorCritic, rs_mean, rs_var):
+        """Copy (EMA) model weights into the decode layout (xtrl.py:721-734, 304-369 names)."""
+        c, w = self.c, self.w
+        w['w_pin'].copy_(model.transformer.project_in.weight)
+        if c.continuous:
+            w['act_emb'].copy_(model.action_embeds.weight)
+            w['act_emb_b'].copy_(model.action_embeds.bias)
+        else:
+            w['act_emb'].copy_(model.action_embeds.embed.weight)
+        w['reward_embed'].copy_(model.reward_embed)
+        w['w_se'].copy_(model.to_state_embed.weight)
+        w['b_se'].copy_(model.to_state_embed.bias)
+        w['ln_final'].copy_(model.transformer.attn_layers.final_norm.gamma)
+        torch.cat((model.action_head[0].weight, model.critic_head[0].weight), out=w['w_h1'])
+        torch.cat((model.action_head[0].bias, model.critic_head[0].bias), out=w['b_h1'])
+        w['w_a2'].copy_(model.action_head[2].weight)
+        w['b_a2'].copy_(model.action_head[2].bias)
+        w['w_c2'].copy_(model.critic_head[2].weight)
+        w['b_c2'].copy_(model.critic_head[2].bias)
+        inv = model.transformer.attn_layers.rotary_pos_emb.inv_freq
+        w['inv_freq'][:inv.numel()].copy_(inv)
+        w['rs_mean'].copy_(rs_mean)
+        w['rs_var'].copy_(rs_var)
+        I = c.inner
+        for wl, (attn_l, ff_l) in zip(self.wl, model.blocks()):
+            (ln_a, _, _), blk, _ = attn_l
+            (ln_f, _, _), ffb, _ = ff_l
+            wl['ln_attn'].copy_(ln_a.gamma)
+            rows = [blk.to_q.weight, blk.to_k.weight, blk.to_v.weight]
+            bias = [torch.zeros(3 * I, device=self.dev)]
+            if blk.to_v_gate is not None:
+                rows.append(blk.to_v_gate.weight)
+                bias.append(blk.to_v_gate.bias)
+            elif c.gate_values:
+                raise RuntimeError('gate_values set but layer has no to_v_gate')
+            if c.value_residual and c.learned_mix:
+                if blk.to_value_residual_mix is not None:
+                    rows.append(blk.to_value_residual_mix[0].weight)
+                    bias.append(blk.to_value_residual_mix[0].bias)
+                else:   # first layer: columns present but unused
+                    rows.append(torch.zeros(c.heads, c.dim, device=self.dev))
+                    bias.append(torch.zeros(c.heads, device=self.dev))
+            torch.cat(rows, out=wl['w_qkv'])
+            torch.cat(bias, out=wl['b_qkv'])
+            wl['w_out'].copy_(blk.to_out.weight)
+            wl['ln_ff'].copy_(ln_f.gamma)
+            wl['w_ff1'].copy_(ffb.ff[0][0].weight)
+            wl['b_ff1'].copy_(ffb.ff[0][0].bias)
+            wl['w_ff2'].copy_(ffb.ff[2].weight)
+            wl['b_ff2'].copy_(ffb.ff[2].bias)
+        if c.evolutionary:
+            self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
+
+    # ------------------------------------------------------------------------------------------
+    def _begin(self, seed, update, slot_offset, episode_of_slot, latent):
+        for t in self.traj.values():
+            if t is not None:
+                t.zero_()
+        self.rng.copy_(torch.tensor([seed & 0x7FFFFFFFFFFFFFFF, (int(update) & 0xFFFFFFFF) | (int(slot_offset) << 32)],
+                                    dtype=torch.int64))
+        self.episode_of_slot.copy_(episode_of_slot.to(torch.int32))
+        if self.c.evolutionary:
+            d = self.c.dim
+            self.ac_in[:, 2 * d:].copy_(F.linear(latent, *self.w_lat))
+        L.check(L.lib().xtrl_rollout_begin(C.byref(self.desc), L.stream()), 'rollout_begin')
+
+    def step(self, t):
+        L.check(L.lib().xtrl_decode_step(C.byref(self.desc), int(t), L.stream()), f'decode_step(t={t})')
+
+    def _steps(self):
+        lib, s = L.lib(), L.stream()
+        for t in range(self.T):
+            L.check(lib.xtrl_decode_step(C.byref(self.desc), t, s), f'decode_step(t={t})')
+
+    @torch.no_grad()
+    def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0):
+        """Roll out Tmax steps of the device Sim for all E slots; returns the trajectory dict."""
+        assert self.sim_mode != SIM_HOST
+        self._begin(seed, update, slot_offset, episode_of_slot, latent)
+        if not self.use_graph:
+            self._steps()
+        else:
+            if self.graph is None:
+                self._steps()   # warm-up launch outside capture (code objects loaded)
+                self._begin(seed, update, slot_offset, episode_of_slot, latent)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._steps()
+                self.graph = g
+            self.graph.replay()
+        return self.traj
+
+    @torch.no_grad()
+    def run_host_env(self, env_reset, env_step, seed, update, latent=None, slot_offset=0, max_steps=None):
+        """E == 1 rollout against a host (numpy) env: the reference's scalar Sim contract."""
+        assert self.sim_mode == SIM_HOST and self.E == 1
+        state0 = env_reset()
+        self.state.copy_(torch.as_tensor(state0, dtype=torch.float32).reshape(1, -1))
+        self._begin(seed, update, slot_offset, torch.zeros(1, dtype=torch.int32), latent)
+        lib = L.lib()
+        T = min(self.T, max_steps or self.T)
+        total = 0.
+        t = 0
+        for t in range(T):
+            self.step(t)
+            if self.c.continuous:
+                action = self.prev_action_f[0].cpu().numpy()
+            else:
+                action = int(self.prev_action[0].item())
+            next_state, reward, terminated = env_step(action)
+            total += float(reward)
+            ns = torch.as_tensor(next_state, dtype=torch.float32, device=self.dev).reshape(1, -1)
+            rw = torch.tensor([float(reward)], dtype=torch.float32, device=self.dev)
+            tm = torch.tensor([1 if terminated else 0], dtype=torch.uint8, device=self.dev)
+            L.check(lib.xtrl_rollout_env_feedback(C.byref(self.desc), t, L.ptr(ns), L.ptr(rw), L.ptr(tm), L.stream()),
+                    'env_feedback')
+            if terminated:
+                break
+        return self.traj, t + 1, total
