@@ -1,0 +1,282 @@
+#!/usr/bin/env python
+"""Benchmark: env-steps/s of the Learner hot path (rollout + learn) on N MI355X, weak scaling.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One "step" = one learning update of the reference Learner loop (xtrl.py:1204-1373): a rollout of
+every (episode, gene) pair of this rank on the device Sim, then Agent.learn (GAE + epochs x
+minibatches of PPO/world-model updates with clip + AdoptAtan2 + EMA).  Inputs are synthetic
+(Philox LunarLander-shaped VecSim) and weights random-init; the timed region contains whole
+updates only (no checkpoint writes).
+
+Printed (rank 0, one JSON line): BASELINE metric + roofline of the decode-attention kernel
+(HIP events around every launch in the timed region) + the CPU baseline (the oracle's batch-1
+restatement of the reference Learner timed on this host) + the PPO loss delta vs that CPU
+reference on identical weights and minibatch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
+
+import numpy as np   # noqa: E402
+import torch         # noqa: E402
+import torch.distributed as dist   # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3    # dense fp32 MFMA / vector peak
+
+CONFIGS = {
+    # configs[2] of BASELINE.json — the north-star workload, per GPU
+    'c3': dict(workload='C3: LunarLander-shaped VecSim (S=8, A=4, hazard 1/64), 1024 episodes x 128 steps per '
+                        'update per GPU, depth-4 d=256 4x16-head gated value-residual world-model policy, '
+                        'batch 128 episodes, 4 epochs, dropout 0.25',
+               S=8, A=4, episodes=1024, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=False,
+               batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
+    # configs[1] — train_lander defaults (evolutionary, 3 genes), 256 episodes, depth-2 d=128
+    'c2': dict(workload='C2: LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 steps, depth-2 d=128 EPO',
+               S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,
+               batch=32, hazard_log2=6, dropout=0.25, mode='lander'),
+    # configs[0] — README Sim plumbing case
+    'c1': dict(workload='C1: README Sim (S=5, A=2, T=10), depth 1, d=48, 64 episodes, batch 8',
+               S=5, A=2, episodes=64, T=10, depth=1, dim=48, heads=4, dim_head=16, gates=False, evo=False,
+               batch=8, hazard_log2=0, dropout=0.25, mode='readme'),
+}
+
+
+def build_learner(cfg, seed, use_graph=True):
+    from xtrl_amd import Learner, SynthVecSim
+    wm = dict(attn_dim_head=cfg['dim_head'], heads=cfg['heads'], depth=cfg['depth'])
+    if cfg['gates']:
+        wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
+    learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
+                      max_timesteps=cfg['T'], batch_size=cfg['batch'], num_episodes_per_update=cfg['episodes'],
+                      evolutionary=cfg['evo'], evolve_every=5, evolve_after_step=10,
+                      latent_gene_pool=dict(dim=32, num_genes_per_island=3, num_selected=2, tournament_size=2),
+                      agent_kwargs=dict(hidden_dim=cfg['dim'], dropout=cfg['dropout'], seed=seed,
+                                        save_path='/tmp/xtrl_bench_ppo.pt'),
+                      use_graph=use_graph)
+    env = SynthVecSim(cfg['S'], cfg['A'], cfg['mode'], cfg['hazard_log2'])
+    return learner, env
+
+
+def one_update(learner, env, T, probe=None):
+    agent = learner.agent
+    u = agent.step
+    traj, lens, genes, cum = learner.rollout_device(env, u, T)
+    fit = learner.fitness(cum, genes)
+    steps = lens.sum()
+    agent.learn(traj, lens, genes, fit, update=u, probe=probe)
+    agent.logs = []
+    return steps, lens
+
+
+class DecodeAttnTimer:
+    """HIP events around every attention-decode launch of the timed region (XtrlDecodeDesc.prof_events)."""
+
+    def __init__(self, learner, env, T):
+        import ctypes as C
+        eng = learner._engine_for(env, T)
+        self.eng, self.L, self.T = eng, eng.c.depth, T
+        self.events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * T * self.L)]
+        self.arr = (C.c_void_p * len(self.events))(*[e.cuda_event for e in self.events])
+        eng.desc.prof_events = C.cast(self.arr, C.POINTER(C.c_void_p))
+        eng.graph = None          # re-capture with the event records inside
+        self.ms, self.launches, self.bytes = 0.0, 0, 0.0
+
+    def collect(self, lens):
+        """After an update: add kernel time and algorithmic bytes of its T*L launches."""
+        torch.cuda.synchronize()
+        for i in range(self.T * self.L):
+            self.ms += self.events[2 * i].elapsed_time(self.events[2 * i + 1])
+        self.launches += self.T * self.L
+        c = self.eng.c
+        H, dh = c.heads, c.dim_head
+        lens = lens.cpu().numpy()
+        t = np.arange(self.T)
+        alive = (lens[None, :] > t[:, None]).sum(1)                  # live episodes at step t
+        # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + q|k|v|gate|mix row (4 dh + 1)
+        # + value-residual row (dh) ; write K,V at t (2 dh) + output (dh)
+        per_head = 4.0 * (2 * t * dh + (4 * dh + 1) + dh + 2 * dh + dh)
+        self.bytes += float(self.L * (alive * H * per_head).sum())
+
+    def detach(self):
+        self.eng.desc.prof_events = None
+        self.eng.graph = None
+
+
+def cpu_baseline(cfg, seed, budget_s):
+    """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn), one
+    update on a bounded number of episodes of the same workload."""
+    from oracle import ref_port as R
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    episodes = 16 if cfg['T'] >= 100 else 64
+    batch = min(8, episodes)
+    c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
+                        dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],
+                        learned_mix=cfg['gates'], evolutionary=False, max_timesteps=cfg['T'], batch_size=batch,
+                        num_episodes_per_update=episodes, sim_mode=cfg['mode'], hazard_log2=cfg['hazard_log2'],
+                        seed=seed, dropout=cfg['dropout'])
+    oracle = R.OracleLearner(c)
+    t0 = time.perf_counter()
+    eps, fit = oracle.rollout(0)
+    t1 = time.perf_counter()
+    oracle.learn(eps, fit, 0)
+    t2 = time.perf_counter()
+    steps = sum(ep['len'] for ep in eps)
+    return dict(value=steps / (t2 - t0), unit='env-steps/s', cores=threads, kind='port',
+                sample=f'1 update, {episodes} episodes ({steps} env-steps), batch {batch}, same model/config, '
+                       f'rollout {t1 - t0:.1f}s + learn {t2 - t1:.1f}s (oracle/ref_port.OracleLearner, batch-1 '
+                       f'KV-cached decode like xtrl.py:1250-1341)')
+
+
+def ppo_loss_delta(learner, env, cfg):
+    """|L_gpu - L_cpu| / |L_cpu| on the first minibatch of one more update, identical weights /
+    RSNorm / minibatch tensors; the CPU side is the oracle's restatement."""
+    from oracle import ref_port as R
+    agent = learner.agent
+    c = agent.cfg
+    out = {}
+    saved_p = c.dropout
+    c.dropout = 0.          # dropout masks are not shared with the CPU side
+    u = agent.step
+    traj, lens, genes, cum = learner.rollout_device(env, u, cfg['T'])
+    mc = R.ModelConfig(c.state_dim, c.num_actions, c.dim, c.depth, c.heads, c.dim_head, cfg['T'], c.reward_range,
+                       c.num_bins, c.continuous, c.squash, c.evolutionary, c.dim_gene, c.frac_head_grad,
+                       c.entropy_weight, c.eps_clip, c.value_clip, 0., c.reward_dropout, True, c.gate_values,
+                       c.value_residual, c.learned_mix)
+    model = R.OracleWMAC(mc)
+
+    def probe(epoch, mbi, idx, loss, stats):
+        if out:
+            return
+        idx_c = idx.cpu()
+        n = int(lens.max())
+        sel = lambda t: t[idx_c][:, :n].cpu()
+        states, actions = sel(traj['states']), sel(traj['actions']).long()
+        rewards, old_lp, bounds = sel(traj['rewards']), sel(traj['logp']), sel(traj['bounds']).bool()
+        values = sel(traj['values'])
+        mb_lens = lens.cpu()[idx_c].long()
+        hl = model.hl
+        full_v = traj['values'][:, :n].cpu()
+        returns = R.calc_gae(traj['rewards'][:, :n].cpu(), hl(full_v), (~traj['bounds'][:, :n].cpu().bool()).float(),
+                             agent.gamma, agent.lam)[idx_c]
+        model.load_state_dict({k: v.detach().cpu() for k, v in agent.model.state_dict().items()})
+        model.train()
+        rs = R.RSNormState(c.state_dim + 1)
+        rs.mean, rs.var = agent.rs_mean.cpu().clone(), agent.rs_var.cpu().clone()
+        mb = R.Minibatch(states, actions, rewards, old_lp, returns, values, bounds, genes.cpu()[idx_c], mb_lens)
+        from xtrl_amd.learner import reward_coin
+        keep = reward_coin(agent.seed, u, epoch, mbi, c.reward_dropout)
+        ref, _, _, _ = R.minibatch_loss(model, rs, mb, None, R.LossWeights(agent.actor_loss_weight,
+                                                                            agent.critic_loss_weight,
+                                                                            agent.autoregressive_loss_weight), keep)
+        out.update(gpu=float(loss), cpu=float(ref))
+
+    agent.learn(traj, lens, genes, learner.fitness(cum, genes), update=u, probe=probe)
+    agent.logs = []
+    c.dropout = saved_p
+    out['rel_delta'] = abs(out['gpu'] - out['cpu']) / max(abs(out['cpu']), 1e-12)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
+    ap.add_argument('--seed', type=int, default=0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    cfg = CONFIGS[args.config]
+    torch.manual_seed(args.seed)
+    learner, env = build_learner(cfg, args.seed, use_graph=not args.no_graph)
+    T = cfg['T']
+
+    for _ in range(args.warmup):
+        one_update(learner, env, T)
+    timer = None if args.no_roofline else DecodeAttnTimer(learner, env, T)
+    if timer is not None:
+        one_update(learner, env, T)        # capture the graph with the event records inside (untimed)
+        timer.ms, timer.launches, timer.bytes = 0.0, 0, 0.0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    total = torch.zeros((), device='cuda', dtype=torch.int64)
+    lens_log = []
+    for _ in range(args.steps):
+        steps, lens = one_update(learner, env, T)
+        total += steps
+        if timer is not None:
+            lens_log.append(lens.clone())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if timer is not None and lens_log:
+        timer.collect(lens_log[-1])   # the event pairs hold the last update's T*L launches
+    el = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(total)
+    elapsed = float(el)
+    env_steps = int(total)
+    value = env_steps / elapsed
+
+    roofline = None
+    if timer is not None and timer.launches:
+        avg_s = timer.ms / timer.launches / 1e3
+        achieved = timer.bytes / timer.launches / avg_s / 1e9
+        roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache)', bound='hbm',
+                        achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s', frac=round(achieved / HBM_PEAK_GBS, 4),
+                        traffic=None, avg_launch_us=round(avg_s * 1e6, 2),
+                        bytes_per_launch=round(timer.bytes / timer.launches))
+        timer.detach()
+
+    loss_delta = None
+    cpu = None
+    if rank == 0:
+        try:
+            loss_delta = ppo_loss_delta(learner, env, cfg)
+        except Exception as e:   # reported, never hidden
+            loss_delta = dict(error=repr(e))
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(cfg, args.seed, 20.)
+    if rank == 0:
+        line = dict(metric='env-steps/s (rollout+update)', value=round(value, 1), unit='env-steps/s', n_gpus=world,
+                    steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
+                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
+                    data='synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)',
+                    config=dict(workload=cfg['workload'], global_batch=cfg['episodes'] * (3 if cfg['evo'] else 1) * world,
+                                seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
+                    roofline=roofline, cpu_baseline=cpu, ppo_loss=loss_delta)
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

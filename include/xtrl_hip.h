@@ -127,6 +127,10 @@ typedef struct XtrlDecodeDesc {
   float* ac_in;  /* [E][in_dim]  (final-normed embed | state embed | latent embed) */
   float* logits; /* [E][A or 2A] */
   float* v1;     /* [E][I] first layer's values (value residual) */
+  float* vals;   /* [E][B] critic logits of the current step (copied to traj_values for live episodes) */
+  /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
+   * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
+  void** prof_events;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and

@@ -289,7 +289,7 @@ def autoregressive_loss(state_pred, real):
 
 def done_loss(done_pred, dones):
     """xtrl.py:406-411."""
-    return F.binary_cross_entropy(done_pred, dones.float(), reduction='none')
+    return F.binary_cross_entropy(done_pred, dones.to(done_pred.dtype), reduction='none')
 
 
 def actor_loss(cfg, hl, raw, actions, old_log_probs, returns, old_values, mask):

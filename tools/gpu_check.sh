@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: parity tests, then (only if they did not crash the process) bench + profile.
+# Usage: tools/gpu_check.sh [tests|bench|prof|all] [bench args...]
+set -u
+mkdir -p gpurun_out
+what=${1:-all}; shift || true
+run_tests() {
+  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  rc=$?; tail -15 gpurun_out/gpu_tests.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+}
+run_bench() {
+  timeout -k 10 900 python bench.py "$@" > gpurun_out/bench.log 2>&1
+  rc=$?; tail -5 gpurun_out/bench.log
+  if [ $rc -ne 0 ]; then echo "bench rc=$rc: stopping"; exit $rc; fi
+}
+run_prof() {
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
+  rc=$?; cd $GRAFT_REPO_ROOT; tail -3 gpurun_out/prof.log
+  if [ $rc -ne 0 ]; then echo "prof rc=$rc"; exit $rc; fi
+}
+case $what in
+  tests) run_tests ;;
+  bench) run_bench "$@" ;;
+  prof) run_prof "$@" ;;
+  all) run_tests; run_bench "$@"; run_prof "$@" ;;
+esac

@@ -186,6 +186,8 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
   const XtrlRngState R = *D.rng;
   const uint32_t slot = R.slot_offset + e;
   const int A = D.A;
+  // Memory.value (xtrl.py:1315): critic logits of live episodes only; padding stays zero
+  for (int k = 0; k < D.B; ++k) D.traj_values[((int64_t)e * D.Tmax + t) * D.B + k] = D.vals[(int64_t)e * D.B + k];
   const float* lg = D.logits + (int64_t)e * (D.continuous ? 2 * A : A);
   if (!D.continuous) {
     float p[64];
@@ -333,7 +335,9 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
     int rc = gemm_f32(D->x, d, Ly.w_qkv, d, Ly.b_qkv, Ly.ln_attn, nullptr, 0, D->qkv, D->n_qkv, nullptr, 0, E,
                       D->n_qkv, d, XTRL_ACT_NONE, s);
     if (rc) return rc;
+    if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
+    if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
     if ((rc = gemm_f32(D->att, I, Ly.w_out, I, nullptr, nullptr, D->x, d, D->x, d, nullptr, 0, E, d, I,
                        XTRL_ACT_NONE, s)))
       return rc;
@@ -354,9 +358,8 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   if ((rc = gemm_f32(D->hff, 4 * d, D->w_a2, 2 * d, D->b_a2, nullptr, nullptr, 0, D->logits, n_act, nullptr, 0, E,
                      n_act, 2 * d, XTRL_ACT_NONE, s)))
     return rc;
-  if ((rc = gemm_f32(D->hff + 2 * d, 4 * d, D->w_c2, 2 * d, D->b_c2, nullptr, nullptr, 0,
-                     D->traj_values + (int64_t)t * D->B, D->Tmax * D->B, nullptr, 0, E, D->B, 2 * d, XTRL_ACT_NONE,
-                     s)))
+  if ((rc = gemm_f32(D->hff + 2 * d, 4 * d, D->w_c2, 2 * d, D->b_c2, nullptr, nullptr, 0, D->vals, D->B, nullptr, 0,
+                     E, D->B, 2 * d, XTRL_ACT_NONE, s)))
     return rc;
   hipLaunchKernelGGL(k_sample, dim3((E + 255) / 256), dim3(256), 0, s, *D, t);
   XTRL_LAUNCHED("sample");

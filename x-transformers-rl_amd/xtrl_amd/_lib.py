@@ -46,7 +46,8 @@ class DecodeDesc(C.Structure):
                 + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
                                     'alive', 'lens', 'cum_reward', 'episode_of_slot', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
-                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1')])
+                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals')]
+                + [('prof_events', C.POINTER(C.c_void_p))])
 
 
 class LossDesc(C.Structure):

@@ -201,8 +201,9 @@ class Agent(nn.Module):
         self._ema_update()
 
     # ---- learn (xtrl.py:808-1023) -----------------------------------------------------------------
-    def learn(self, traj, episode_lens, gene_ids, fitnesses=None, update=None):
-        """traj: dict of device tensors [N][Tmax][.] (rollout buffers, padded with zeros)."""
+    def learn(self, traj, episode_lens, gene_ids, fitnesses=None, update=None, probe=None):
+        """traj: dict of device tensors [N][Tmax][.] (rollout buffers, padded with zeros).
+        ``probe(epoch, minibatch, idx, loss, stats)`` (tests) runs after backward, before the step."""
         c, dev = self.cfg, self.device
         update = self.step if update is None else update
         lens = episode_lens.to(dev, torch.int32)
@@ -256,6 +257,8 @@ class Agent(nn.Module):
                 self.flat.zero_grad()
                 loss.backward()
                 dist_.mean_(self.flat.grad)
+                if probe is not None:
+                    probe(epoch, mbi, idx, loss, stats)
                 self.optimizer_step()
                 # RSNorm copy update with the normalised masked rows (xtrl.py:1005, 598-610)
                 with torch.no_grad():
