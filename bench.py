@@ -87,6 +87,8 @@ class DecodeAttnTimer:
         eng = learner._engine_for(env, T)
         self.eng, self.L, self.T = eng, eng.c.depth, T
         self.events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * T * self.L)]
+        for e in self.events:     # torch creates the HIP event lazily, on first record
+            e.record()
         self.arr = (C.c_void_p * len(self.events))(*[e.cuda_event for e in self.events])
         eng.desc.prof_events = C.cast(self.arr, C.POINTER(C.c_void_p))
         eng.graph = None          # re-capture with the event records inside
@@ -119,7 +121,7 @@ def cpu_baseline(cfg, seed, budget_s):
     from oracle import ref_port as R
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    episodes = 16 if cfg['T'] >= 100 else 64
+    episodes = 96 if cfg['T'] >= 100 else 512
     batch = min(8, episodes)
     c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
                         dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],

@@ -48,6 +48,13 @@ int xtrl_gemm_f32(const float* X, int ldx, const float* W, int ldw, const float*
                   const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M,
                   int N, int K, int act, void* stream);
 
+/* General C = A . B (+ bias) with either operand transposed; C = beta * C + result.
+ *   trans_a = 0: A[m][k] at A[m * lda + k]   trans_a = 1: A[m][k] at A[k * lda + m]
+ *   trans_b = 0: B[k][n] at B[n * ldb + k]   trans_b = 1: B[k][n] at B[k * ldb + n]
+ * (nn.Linear backward: dgrad = (0, 1), wgrad = (1, 1) with beta = 1 to accumulate) */
+int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
+                 float* C, int ldc, int M, int N, int K, float beta, void* stream);
+
 /* Y[m, :] = layer_norm(X[m, :]) * gamma  (x-transformers LayerNorm, final norm of the Decoder) */
 int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, void* stream);
 
@@ -227,12 +234,14 @@ int xtrl_loss_bwd(const XtrlLossDesc* desc, float grad_scale, void* stream);
  * out[1] = min(max_norm / (norm + 1e-6), 1) */
 int xtrl_grad_norm(const float* g, int64_t n, double* ws, float max_norm, float* out, void* stream);
 /* AdoptAtan2 step (xtrl.py:749, 991) on n parameters split into n_seg tensors
- * (seg_start[n_seg + 1] device offsets); g is scaled in place by clip[1] (clip may be NULL);
+ * (seg_start[n_seg + 1] device offsets) and processed as n_chunks contiguous pieces
+ * (chunks[n_chunks][3] = start, end, tensor index; one workgroup each, so the per-tensor cautious
+ * mean needs one atomic per workgroup); g is scaled in place by clip[1] (clip may be NULL);
  * seg_ws = n_seg ints of scratch; first_step != 0 initialises m = 0, v = g^2, p_init = p. */
-int xtrl_adopt_atan2(float* p, float* g, float* m, float* v, float* p_init, int64_t n, const int64_t* seg_start,
-                     int n_seg, int* seg_ws, const float* clip, float lr, float init_lr, float beta1, float beta2,
-                     float a, float b, float weight_decay, float regen_rate, float cautious, int first_step,
-                     void* stream);
+int xtrl_adopt_atan2(float* p, float* g, float* m, float* v, float* p_init, int64_t n, const int64_t* chunks,
+                     int n_chunks, const int64_t* seg_start, int n_seg, int* seg_ws, const float* clip, float lr,
+                     float init_lr, float beta1, float beta2, float a, float b, float weight_decay, float regen_rate,
+                     float cautious, int first_step, void* stream);
 /* ema = lerp(ema, p, 1 - decay) */
 int xtrl_ema_lerp(float* ema, const float* p, int64_t n, float weight, void* stream);
 

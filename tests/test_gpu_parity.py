@@ -323,7 +323,7 @@ def test_adopt_atan2_and_clip_match_oracle():
         opt.step()
         gflat = torch.cat([gr.reshape(-1) for gr in grads]).to(DEV)
         ops.grad_norm(gflat, 0.5, ws, clip)
-        ops.adopt_atan2(flat, gflat, m, v, pinit, seg, seg_ws, clip, lr=8e-4, init_lr=8e-4, betas=(0.9, 0.99),
+        ops.adopt_atan2(flat, gflat, m, v, pinit, seg, ops.adopt_chunks(seg, chunk=8), seg_ws, clip, lr=8e-4, init_lr=8e-4, betas=(0.9, 0.99),
                         a=1.27, b=1., weight_decay=0., regen_rate=1e-4, cautious=0.1, first_step=step == 0)
         torch.cuda.synchronize()
         tol(flat, torch.cat([p.detach().reshape(-1) for p in ref_params]), 1e-5, 1e-6)

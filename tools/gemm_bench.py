@@ -1,0 +1,35 @@
+"""Microbenchmark: libxtrl_hip fp32 MFMA GEMM vs torch (hipBLASLt) on the shapes of the hot path."""
+import sys, time
+sys.path[:0] = ['.', 'x-transformers-rl_amd']
+import torch
+from xtrl_amd import ops, _lib as L
+
+def timeit(fn, iters=20):
+    fn(); torch.cuda.synchronize()
+    s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+    s.record()
+    for _ in range(iters): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3   # us
+
+shapes = [  # (tag, M, N, K, ta, tb)
+    ('dec qkv', 1024, 260, 256, 0, 0), ('dec out', 1024, 256, 64, 0, 0), ('dec ff1', 1024, 1024, 256, 0, 0),
+    ('dec ff2', 1024, 256, 1024, 0, 0), ('dec head1', 1024, 1024, 512, 0, 0), ('dec vals', 1024, 100, 512, 0, 0),
+    ('fwd qkv', 16384, 192, 256, 0, 0), ('fwd ff1', 16384, 1024, 256, 0, 0), ('fwd ff2', 16384, 256, 1024, 0, 0),
+    ('fwd head1', 16384, 512, 512, 0, 0), ('fwd vals', 16384, 100, 512, 0, 0),
+    ('dgrad ff1', 16384, 256, 1024, 0, 1), ('dgrad ff2', 16384, 1024, 256, 0, 1),
+    ('wgrad ff1', 1024, 256, 16384, 1, 1), ('wgrad ff2', 256, 1024, 16384, 1, 1), ('wgrad qkv', 192, 256, 16384, 1, 1),
+]
+for tag, M, N, K, ta, tb in shapes:
+    A = torch.randn(K, M, device='cuda') if ta else torch.randn(M, K, device='cuda')
+    B = torch.randn(K, N, device='cuda') if tb else torch.randn(N, K, device='cuda')
+    C = torch.empty(M, N, device='cuda')
+    At = A.t() if ta else A
+    Bt = B if tb else B.t()
+    ref = At.double() @ Bt.double()
+    ops.gemm_ex(A, B, ta, tb, M, N, K, C)
+    err = float((C.double() - ref).abs().max() / ref.abs().max())
+    us = timeit(lambda: ops.gemm_ex(A, B, ta, tb, M, N, K, C))
+    ut = timeit(lambda: torch.matmul(At, Bt, out=C))
+    tf = 2 * M * N * K / us / 1e6
+    print(f'{tag:10s} M={M:6d} N={N:5d} K={K:6d}  xtrl {us:8.1f} us {tf:6.1f} TF | torch {ut:8.1f} us {2*M*N*K/ut/1e6:6.1f} TF | err {err:.1e}')

@@ -18,6 +18,7 @@ run_prof() {
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1
   rc=$?; cd $GRAFT_REPO_ROOT; tail -3 gpurun_out/prof.log
+  find gpurun_out/prof -type f ! -name '*stats*' -delete
   if [ $rc -ne 0 ]; then echo "prof rc=$rc"; exit $rc; fi
 }
 case $what in

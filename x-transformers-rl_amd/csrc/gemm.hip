@@ -1,56 +1,66 @@
-// Fused fp32 GEMM on the CDNA4 f32 matrix cores (v_mfma_f32_32x32x2_f32, exact f32 products).
+// Fused fp32 GEMM on the CDNA4 f32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32 products,
+// 64 cycles / instruction / SIMD, dependent-accumulator latency 64 -> one accumulator chain per
+// wave runs at the issue rate).
 //
-//   Y[m, n] = act( LN?(X)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])
+//   C[m, n] = act( LN?(A)[m, :] . B[:, n] + bias[n] ) (+ R[m, n])          (fp32 in, fp32 out)
 //
-// Tile: 64 x 64 output per 256-thread workgroup, 2 x 2 waves of 32 x 32, BK = 16.  Operands are
-// staged k-major in LDS ([BK][64 + 4]) so that an MFMA fragment read (lane l -> row l & 31,
-// k = l >> 5) is 32 consecutive dwords per half-wave: conflict-free ds_read_b32.  Staging is
-// register double-buffered: the next K-slab's global loads are issued before the current slab's
-// MFMAs and written to the other LDS buffer after them (one barrier per K-step).
+// Operand layouts (so one kernel serves forward, dgrad and wgrad of nn.Linear):
+//   A "N": A[m][k] at a[m * lda + k]       A "T": A[m][k] at a[k * lda + m]
+//   B "N": B[k][n] at b[n * ldb + k]  (nn.Linear weight [out][in])
+//   B "T": B[k][n] at b[k * ldb + n]
 //
-// The optional LayerNorm prologue (x-transformers LayerNorm: no affine, eps 1e-5, times gamma)
-// computes per-row mean / rstd for the block's 64 rows (two-pass, in registers) and normalises
-// the A operand while staging it, so pre-norm blocks need no separate normalisation pass.
-#include <stdarg.h>
-#include <stdio.h>
-
+// Geometry: WM x WN x WK waves; each wave owns a 32 x 32 output tile and a 32-deep share of every
+// K-slab (so WK > 1 splits K inside the workgroup; partial tiles are summed through LDS in fixed
+// order — deterministic).  Block tile (32 WM) x (32 WN), K-slab 32 WK.  Slabs are staged
+// global -> registers (float4, coalesced along the contiguous dimension) -> LDS in k-major images
+// [k][m + 1] / [k][n + 1] (the +1 pad keeps the MFMA fragment reads — 32 consecutive dwords per
+// half-wave — conflict-free); the next slab's global loads are issued before the current slab's
+// MFMAs (register double buffering, one barrier per slab).
+//
+// The optional LayerNorm prologue (x-transformers LayerNorm: no affine, eps 1e-5, times gamma;
+// A "N" only) computes per-row mean / rstd for the block's rows (two-pass) and normalises A while
+// staging it.
 #include "common.h"
 
 namespace xtrl {
 
 namespace {
-constexpr int BM = 64, BN = 64, BK = 16, LDSW = BM + 4;
 
 struct GemmArgs {
-  const float* X;
-  const float* W;
+  const float* A;
+  const float* B;
   const float* bias;
   const float* gamma;
   const float* R;
-  float* Y;
+  float* C;
   const int32_t* t_dev;
-  int64_t y_t_stride;
-  int ldx, ldw, ldr, ldy, M, N, K;
+  int64_t c_t_stride;
+  int lda, ldb, ldr, ldc, M, N, K;
+  float beta;   // C = beta * C + result (accumulate into C, used by weight gradients)
 };
 
-template <int ACT, bool LN, bool RES>
-__global__ __launch_bounds__(256) void k_gemm_f32(const GemmArgs a) {
-  __shared__ float As[2][BK][LDSW];
-  __shared__ float Bs[2][BK][LDSW];
-  __shared__ float row_mean[BM], row_rstd[BM];
+template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+__global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
+  constexpr int BM = 32 * WM, BN = 32 * WN, BK = 32 * WK, NT = 64 * WM * WN * WK;
+  constexpr int AST = BM + 1, BST = BN + 1;
+  constexpr int A_F4 = BM * BK / 4 / NT, B_F4 = BN * BK / 4 / NT;   // float4 loads per thread per slab
+  static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small for the thread count");
+  __shared__ float As[2][BK][AST];
+  __shared__ float Bs[2][BK][BST];
+  __shared__ float row_mean[LN ? BM : 1], row_rstd[LN ? BM : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int M = a.M, N = a.N, K = a.K;
 
   if constexpr (LN) {
-    // 16 rows per wave, two-pass mean / variance like F.layer_norm
-    for (int rr = 0; rr < 16; ++rr) {
-      const int r = wave * 16 + rr, m = m0 + r;
+    constexpr int NW = WM * WN * WK;
+    for (int r = wave; r < BM; r += NW) {
+      const int m = m0 + r;
       float mean = 0.f, rstd = 0.f;
       if (m < M) {
-        const float* xr = a.X + (int64_t)m * a.ldx;
+        const float* xr = a.A + (int64_t)m * a.lda;
         float s = 0.f;
         for (int k = lane; k < K; k += 64) s += xr[k];
         mean = wave_sum(s) / (float)K;
@@ -59,8 +69,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmArgs a) {
           const float dlt = xr[k] - mean;
           q += dlt * dlt;
         }
-        const float var = wave_sum(q) / (float)K;
-        rstd = 1.0f / sqrtf(var + 1e-5f);
+        rstd = 1.0f / sqrtf(wave_sum(q) / (float)K + 1e-5f);
       }
       if (lane == 0) {
         row_mean[r] = mean;
@@ -70,48 +79,93 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmArgs a) {
     __syncthreads();
   }
 
-  // staging: wave w loads k-columns [4w, 4w + 4) of the slab for all 64 rows (lane = row)
-  const int sr = lane, sk = wave * 4;
-  float4 ra, rb;
-  auto load_slab = [&](int k0) {
-    const int k = k0 + sk;
-    {
-      const int m = m0 + sr;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m < M) {
-        const float* p = a.X + (int64_t)m * a.ldx + k;
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (k + c < K) v[c] = p[c];
-        if constexpr (LN) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (k + c < K) v[c] = ((v[c] - row_mean[sr]) * row_rstd[sr]) * a.gamma[k + c];
-        }
+  // ---- staging: element (row, k-quad) assignments --------------------------------------------
+  // "N" operand (contiguous along k): thread covers k-quad q of row r; "T" operand (contiguous
+  // along m / n): thread covers an m-quad of k-row r.
+  float4 ra[A_F4], rb[B_F4];
+  auto load4 = [&](const float* base, int64_t ld, int outer, int inner, int outer_lim, int inner_lim) -> float4 {
+    // element (outer, inner .. inner+3) of a row-major [outer][inner] array
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (outer < outer_lim) {
+      const float* p = base + (int64_t)outer * ld + inner;
+      if (VEC && inner + 3 < inner_lim) {
+        const float4 f = *reinterpret_cast<const float4*>(p);
+        return f;
       }
-      ra = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (inner + c < inner_lim) v[c] = p[c];
     }
-    {
-      const int n = n0 + sr;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (n < N) {
-        const float* p = a.W + (int64_t)n * a.ldw + k;
+    return make_float4(v[0], v[1], v[2], v[3]);
+  };
+  auto load_slab = [&](int k0) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (k + c < K) v[c] = p[c];
+    for (int i = 0; i < A_F4; ++i) {
+      const int e = tid + i * NT;
+      if constexpr (!TA) {   // [BM rows][BK/4 quads]
+        const int r = e / (BK / 4), q = e % (BK / 4);
+        float4 f = load4(a.A, a.lda, m0 + r, k0 + 4 * q, M, K);
+        if constexpr (LN) {
+          const float mu = row_mean[r], rs = row_rstd[r];
+          const int k = k0 + 4 * q;
+          f.x = k + 0 < K ? ((f.x - mu) * rs) * a.gamma[k + 0] : 0.f;
+          f.y = k + 1 < K ? ((f.y - mu) * rs) * a.gamma[k + 1] : 0.f;
+          f.z = k + 2 < K ? ((f.z - mu) * rs) * a.gamma[k + 2] : 0.f;
+          f.w = k + 3 < K ? ((f.w - mu) * rs) * a.gamma[k + 3] : 0.f;
+        }
+        ra[i] = f;
+      } else {               // [BK rows][BM/4 quads]
+        const int r = e / (BM / 4), q = e % (BM / 4);
+        ra[i] = load4(a.A, a.lda, k0 + r, m0 + 4 * q, K, M);
       }
-      rb = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      const int e = tid + i * NT;
+      if constexpr (!TB) {
+        const int r = e / (BK / 4), q = e % (BK / 4);
+        rb[i] = load4(a.B, a.ldb, n0 + r, k0 + 4 * q, N, K);
+      } else {
+        const int r = e / (BN / 4), q = e % (BN / 4);
+        rb[i] = load4(a.B, a.ldb, k0 + r, n0 + 4 * q, K, N);
+      }
     }
   };
   auto store_slab = [&](int buf) {
-    As[buf][sk + 0][sr] = ra.x;
-    As[buf][sk + 1][sr] = ra.y;
-    As[buf][sk + 2][sr] = ra.z;
-    As[buf][sk + 3][sr] = ra.w;
-    Bs[buf][sk + 0][sr] = rb.x;
-    Bs[buf][sk + 1][sr] = rb.y;
-    Bs[buf][sk + 2][sr] = rb.z;
-    Bs[buf][sk + 3][sr] = rb.w;
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      const int e = tid + i * NT;
+      if constexpr (!TA) {
+        const int r = e / (BK / 4), q = e % (BK / 4);
+        As[buf][4 * q + 0][r] = ra[i].x;
+        As[buf][4 * q + 1][r] = ra[i].y;
+        As[buf][4 * q + 2][r] = ra[i].z;
+        As[buf][4 * q + 3][r] = ra[i].w;
+      } else {
+        const int r = e / (BM / 4), q = e % (BM / 4);
+        As[buf][r][4 * q + 0] = ra[i].x;
+        As[buf][r][4 * q + 1] = ra[i].y;
+        As[buf][r][4 * q + 2] = ra[i].z;
+        As[buf][r][4 * q + 3] = ra[i].w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      const int e = tid + i * NT;
+      if constexpr (!TB) {
+        const int r = e / (BK / 4), q = e % (BK / 4);
+        Bs[buf][4 * q + 0][r] = rb[i].x;
+        Bs[buf][4 * q + 1][r] = rb[i].y;
+        Bs[buf][4 * q + 2][r] = rb[i].z;
+        Bs[buf][4 * q + 3][r] = rb[i].w;
+      } else {
+        const int r = e / (BN / 4), q = e % (BN / 4);
+        Bs[buf][r][4 * q + 0] = rb[i].x;
+        Bs[buf][r][4 * q + 1] = rb[i].y;
+        Bs[buf][r][4 * q + 2] = rb[i].z;
+        Bs[buf][r][4 * q + 3] = rb[i].w;
+      }
+    }
   };
 
   f32x16 acc;
@@ -122,23 +176,42 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmArgs a) {
   load_slab(0);
   store_slab(0);
   __syncthreads();
-  const int fi = wm * 32 + (lane & 31), fj = wn * 32 + (lane & 31), fk = lane >> 5;
+  const int fi = wm * 32 + (lane & 31), fj = wn * 32 + (lane & 31), fk = wk * 32 + (lane >> 5);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_slab((kt + 1) * BK);
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float av = As[cur][kk + fk][fi];
-      const float bv = Bs[cur][kk + fk][fj];
+    for (int kk = 0; kk < 32; kk += 2) {
+      const float av = As[cur][fk + kk][fi];
+      const float bv = Bs[cur][fk + kk][fj];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
     if (kt + 1 < nk) store_slab(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31
-  float* Y = a.Y;
-  if (a.t_dev) Y += (int64_t)(*a.t_dev) * a.y_t_stride;
+  // ---- intra-workgroup split-K: waves wk > 0 hand their tiles to wk == 0 through LDS ----------
+  if constexpr (WK > 1) {
+    float* red = &As[0][0][0];   // reuse the staging LDS: (WK-1) * WM*WN * 16 * 64 floats
+    static_assert((WK - 1) * WM * WN * 16 * 64 <= 2 * BK * AST + 2 * BK * BST, "reduction scratch too small");
+    float* mine = red + ((wk - 1) * WM * WN + wmn) * 16 * 64;
+    if (wk > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mine[r * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll
+    for (int j = 1; j < WK; ++j) {
+      const float* src = red + ((j - 1) * WM * WN + wmn) * 16 * 64;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += src[r * 64 + lane];
+    }
+  }
+
+  // ---- epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 -------------
+  float* C = a.C;
+  if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
   const int n = n0 + wn * 32 + (lane & 31);
   if (n >= N) return;
   const float bn = a.bias ? a.bias[n] : 0.f;
@@ -150,7 +223,9 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmArgs a) {
       if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
       if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
       if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
-      Y[(int64_t)m * a.ldy + n] = v;
+      float* dst = C + (int64_t)m * a.ldc + n;
+      if (a.beta != 0.f) v = a.beta * (*dst) + v;
+      *dst = v;
     }
   }
 }
@@ -173,37 +248,69 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
   for (int k = lane; k < D; k += 64) Y[(int64_t)m * ldy + k] = ((xr[k] - mean) * rstd) * gamma[k];
 }
 
-template <int ACT, bool LN, bool RES>
+template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
 void launch(const GemmArgs& a, hipStream_t s) {
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((k_gemm_f32<ACT, LN, RES>), grid, dim3(256), 0, s, a);
+  dim3 grid((a.N + 32 * WN - 1) / (32 * WN), (a.M + 32 * WM - 1) / (32 * WM));
+  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TA, TB, ACT, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
 }
 
+// geometry choice: 64 x 64 tiles when they fill the chip, else 32 x 32 tiles with a 4-way split
+// of K inside the workgroup (decode-sized M) — both keep one 32 x 32 accumulator per wave
+template <bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+void dispatch_geom(const GemmArgs& a, hipStream_t s) {
+  const int64_t tiles64 = (int64_t)((a.M + 63) / 64) * ((a.N + 63) / 64);
+  if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
+  else launch<1, 1, 4, TA, TB, ACT, LN, RES, VEC>(a, s);
+}
+
+template <bool TA, bool TB, int ACT, bool LN, bool RES>
+void dispatch_vec(const GemmArgs& a, bool vec, hipStream_t s) {
+  if (vec) dispatch_geom<TA, TB, ACT, LN, RES, true>(a, s);
+  else dispatch_geom<TA, TB, ACT, LN, RES, false>(a, s);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
 }  // namespace
+
+int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
+            const float* ln_gamma, const float* R, int ldr, float* C, int ldc, const int32_t* t_dev,
+            int64_t c_t_stride, int M, int N, int K, int act, float beta, hipStream_t s) {
+  XTRL_REQUIRE(A && B && C, "gemm: null operand");
+  XTRL_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  XTRL_REQUIRE(lda >= (trans_a ? M : K) && ldb >= (trans_b ? N : K) && ldc >= N, "gemm: leading dims too small");
+  XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
+  XTRL_REQUIRE(!(ln_gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
+  if (M == 0 || N == 0) return XTRL_OK;
+  GemmArgs a{A, B, bias, ln_gamma, R, C, t_dev, c_t_stride, lda, ldb, ldr, ldc, M, N, K, beta};
+  const bool vec = aligned16(A) && aligned16(B) && (lda % 4 == 0) && (ldb % 4 == 0);
+  const bool ln = ln_gamma != nullptr, res = R != nullptr;
+#define XG(TA_, TB_, A_, L_, R_)                                                                   \
+  if (trans_a == TA_ && trans_b == TB_ && act == A_ && ln == L_ && res == R_) {                    \
+    dispatch_vec<TA_, TB_, A_, L_, R_>(a, vec, s);                                                 \
+    XTRL_LAUNCHED("gemm_f32");                                                                     \
+    return XTRL_OK;                                                                                \
+  }
+  // forward / decode (A row-major, B = nn.Linear weight)
+  XG(0, 0, XTRL_ACT_NONE, false, false)
+  XG(0, 0, XTRL_ACT_NONE, false, true)
+  XG(0, 0, XTRL_ACT_NONE, true, false)
+  XG(0, 0, XTRL_ACT_GELU, true, false)
+  XG(0, 0, XTRL_ACT_GELU, false, false)
+  XG(0, 0, XTRL_ACT_SILU, false, false)
+  // dgrad (B = weight used as [k][n]) and wgrad (A = dY^T)
+  XG(0, 1, XTRL_ACT_NONE, false, false)
+  XG(1, 1, XTRL_ACT_NONE, false, false)
+#undef XG
+  set_error("gemm: unsupported combination ta=%d tb=%d act=%d ln=%d residual=%d", trans_a, trans_b, act, (int)ln,
+            (int)res);
+  return XTRL_E_ARG;
+}
 
 int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
              const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
              int K, int act, hipStream_t s) {
-  XTRL_REQUIRE(X && W && Y, "gemm: null operand");
-  XTRL_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
-  XTRL_REQUIRE(ldx >= K && ldw >= K && ldy >= N, "gemm: leading dims too small");
-  XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
-  if (M == 0 || N == 0) return XTRL_OK;
-  GemmArgs a{X, W, bias, ln_gamma, R, Y, t_dev, y_t_stride, ldx, ldw, ldr, ldy, M, N, K};
-  const bool ln = ln_gamma != nullptr, res = R != nullptr;
-#define XTRL_GEMM_CASE(A_, L_, R_) \
-  if (act == A_ && ln == L_ && res == R_) { launch<A_, L_, R_>(a, s); XTRL_LAUNCHED("gemm_f32"); return XTRL_OK; }
-  XTRL_GEMM_CASE(XTRL_ACT_NONE, false, false)
-  XTRL_GEMM_CASE(XTRL_ACT_NONE, false, true)
-  XTRL_GEMM_CASE(XTRL_ACT_NONE, true, false)
-  XTRL_GEMM_CASE(XTRL_ACT_NONE, true, true)
-  XTRL_GEMM_CASE(XTRL_ACT_GELU, false, false)
-  XTRL_GEMM_CASE(XTRL_ACT_GELU, true, false)
-  XTRL_GEMM_CASE(XTRL_ACT_SILU, false, false)
-  XTRL_GEMM_CASE(XTRL_ACT_SILU, true, false)
-#undef XTRL_GEMM_CASE
-  set_error("gemm: unsupported combination act=%d ln=%d residual=%d", act, (int)ln, (int)res);
-  return XTRL_E_ARG;
+  return gemm_ex(0, 0, X, ldx, W, ldw, bias, ln_gamma, R, ldr, Y, ldy, t_dev, y_t_stride, M, N, K, act, 0.f, s);
 }
 
 int layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, hipStream_t s) {
@@ -221,6 +328,12 @@ extern "C" int xtrl_gemm_f32(const float* X, int ldx, const float* W, int ldw, c
                              const int32_t* t_dev, int64_t y_t_stride, int M, int N, int K, int act, void* stream) {
   return xtrl::gemm_f32(X, ldx, W, ldw, bias, ln_gamma, R, ldr, Y, ldy, t_dev, y_t_stride, M, N, K, act,
                         xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb,
+                            const float* bias, float* C, int ldc, int M, int N, int K, float beta, void* stream) {
+  return xtrl::gemm_ex(trans_a, trans_b, A, lda, B, ldb, bias, nullptr, nullptr, 0, C, ldc, nullptr, 0, M, N, K,
+                       XTRL_ACT_NONE, beta, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D,

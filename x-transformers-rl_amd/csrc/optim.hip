@@ -40,7 +40,9 @@ __global__ void k_norm_final(const double* ws, int nb, float max_norm, float* ou
 struct AdoptArgs {
   float *p, *g, *m, *v, *p_init;
   int64_t n;
-  const int64_t* seg;
+  const int64_t* chunks;   // [n_chunks][3]: start, end, segment
+  int n_chunks;
+  const int64_t* seg;      // [n_seg + 1] segment offsets
   int n_seg;
   int* cnt;
   const float* clip;
@@ -48,20 +50,14 @@ struct AdoptArgs {
   int first;
 };
 
-__device__ __forceinline__ int find_seg(const int64_t* seg, int n_seg, int64_t i) {
-  int lo = 0, hi = n_seg - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (seg[mid] <= i) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// pass A: regen / weight decay, first-step init, m update, cautious alignment counts
+// pass A (one workgroup per chunk of one parameter tensor): regen / weight decay, first-step
+// init, m update, and the cautious alignment count of the chunk -> ONE atomic per workgroup
 __global__ __launch_bounds__(256) void k_adopt_a(const AdoptArgs A) {
+  const int64_t c0 = A.chunks[3 * blockIdx.x], c1 = A.chunks[3 * blockIdx.x + 1];
+  const int sg = (int)A.chunks[3 * blockIdx.x + 2];
   const float coef = A.clip ? A.clip[1] : 1.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * 256) {
+  int aligned = 0;
+  for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
     const float g = A.g[i] * coef;
     A.g[i] = g;
     float p = A.p[i];
@@ -77,24 +73,34 @@ __global__ __launch_bounds__(256) void k_adopt_a(const AdoptArgs A) {
     const float u = atan2f(g, A.b * sqrtf(A.v[i]));
     const float m = lerpf_(A.m[i], u, 1.f - A.beta1);
     A.m[i] = m;
-    if (A.cautious < 1.f && m * g > 0.f) atomicAdd(&A.cnt[find_seg(A.seg, A.n_seg, i)], 1);
+    aligned += (m * g > 0.f) ? 1 : 0;
   }
+  if (A.first || A.cautious >= 1.f) return;
+  __shared__ int sh[4];
+  int w = aligned;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&A.cnt[sg], sh[0] + sh[1] + sh[2] + sh[3]);
 }
 
 // pass B: p -= lr * a * m * scale; v = lerp(v, g^2, 1 - beta2)
 __global__ __launch_bounds__(256) void k_adopt_b(const AdoptArgs A) {
   if (A.first) return;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.n; i += (int64_t)gridDim.x * 256) {
+  const int64_t c0 = A.chunks[3 * blockIdx.x], c1 = A.chunks[3 * blockIdx.x + 1];
+  const int sg = (int)A.chunks[3 * blockIdx.x + 2];
+  float mean = 1.f;
+  if (A.cautious < 1.f) {
+    const double len = (double)(A.seg[sg + 1] - A.seg[sg]);
+    const double k = (double)A.cnt[sg];
+    mean = (float)((k + (double)A.cautious * (len - k)) / len);
+  }
+  const float inv = 1.f / fmaxf(mean, 1e-5f);
+  for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
     const float g = A.g[i], m = A.m[i];
     float upd = m;
-    if (A.cautious < 1.f) {
-      const int s = find_seg(A.seg, A.n_seg, i);
-      const double len = (double)(A.seg[s + 1] - A.seg[s]);
-      const double k = (double)A.cnt[s];
-      const float mean = (float)((k + (double)A.cautious * (len - k)) / len);
-      const float sc = (m * g > 0.f) ? 1.f : A.cautious;
-      upd = m * (sc / fmaxf(mean, 1e-5f));
-    }
+    if (A.cautious < 1.f) upd = m * (((m * g > 0.f) ? 1.f : A.cautious) * inv);
     A.p[i] = A.p[i] + (-A.lr) * (upd * A.a);
     A.v[i] = lerpf_(A.v[i], g * g, 1.f - A.beta2);
   }
@@ -118,11 +124,12 @@ int grad_norm(const float* g, int64_t n, double* ws, float max_norm, float* out,
 }
 
 int adopt_atan2(const AdoptArgs& A, hipStream_t s) {
-  XTRL_REQUIRE(A.p && A.g && A.m && A.v && A.n > 0 && A.seg && A.n_seg > 0 && A.cnt, "adopt_atan2: bad arguments");
+  XTRL_REQUIRE(A.p && A.g && A.m && A.v && A.n > 0 && A.seg && A.n_seg > 0 && A.cnt && A.chunks && A.n_chunks > 0,
+               "adopt_atan2: bad arguments");
   XTRL_REQUIRE(A.regen <= 0.f || A.p_init, "adopt_atan2: regen needs p_init");
   if (hipMemsetAsync(A.cnt, 0, sizeof(int) * A.n_seg, s) != hipSuccess) return check_launch("adopt_atan2 memset");
-  hipLaunchKernelGGL(k_adopt_a, dim3(grid_for(A.n)), dim3(256), 0, s, A);
-  hipLaunchKernelGGL(k_adopt_b, dim3(grid_for(A.n)), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(k_adopt_a, dim3(A.n_chunks), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(k_adopt_b, dim3(A.n_chunks), dim3(256), 0, s, A);
   XTRL_LAUNCHED("adopt_atan2");
   return XTRL_OK;
 }
@@ -141,11 +148,12 @@ extern "C" int xtrl_grad_norm(const float* g, int64_t n, double* ws, float max_n
 }
 
 extern "C" int xtrl_adopt_atan2(float* p, float* g, float* m, float* v, float* p_init, int64_t n,
-                                const int64_t* seg_start, int n_seg, int* seg_ws, const float* clip, float lr,
-                                float init_lr, float beta1, float beta2, float a, float b, float weight_decay,
-                                float regen_rate, float cautious, int first_step, void* stream) {
-  xtrl::AdoptArgs A{p,   g,       m,     v,     p_init, n, seg_start, n_seg, seg_ws, clip, lr, init_lr, beta1,
-                    beta2, a, b, weight_decay, regen_rate, cautious, first_step};
+                                const int64_t* chunks, int n_chunks, const int64_t* seg_start, int n_seg,
+                                int* seg_ws, const float* clip, float lr, float init_lr, float beta1, float beta2,
+                                float a, float b, float weight_decay, float regen_rate, float cautious, int first_step,
+                                void* stream) {
+  xtrl::AdoptArgs A{p,     g,      m,       v,    p_init, n, chunks, n_chunks, seg_start, n_seg, seg_ws, clip, lr,
+                    init_lr, beta1, beta2, a, b, weight_decay, regen_rate, cautious, first_step};
   return xtrl::adopt_atan2(A, xtrl::as_stream(stream));
 }
 

@@ -63,6 +63,7 @@ SIGNATURES = {
     'xtrl_abi_version': (I32, []),
     'xtrl_last_error': (C.c_char_p, []),
     'xtrl_gemm_f32': (I32, [P, I32, P, I32, P, P, P, I32, P, I32, P, I64, I32, I32, I32, I32, P]),
+    'xtrl_gemm_ex': (I32, [I32, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, F32, P]),
     'xtrl_layernorm_f32': (I32, [P, I32, P, P, I32, I32, I32, P]),
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
@@ -74,8 +75,8 @@ SIGNATURES = {
     'xtrl_loss_fwd': (I32, [C.POINTER(LossDesc), P]),
     'xtrl_loss_bwd': (I32, [C.POINTER(LossDesc), F32, P]),
     'xtrl_grad_norm': (I32, [P, I64, P, F32, P, P]),
-    'xtrl_adopt_atan2': (I32, [P, P, P, P, P, I64, P, I32, P, P, F32, F32, F32, F32, F32, F32, F32, F32, F32, I32,
-                               P]),
+    'xtrl_adopt_atan2': (I32, [P, P, P, P, P, I64, P, I32, P, I32, P, P, F32, F32, F32, F32, F32, F32, F32, F32, F32,
+                               I32, P]),
     'xtrl_ema_lerp': (I32, [P, P, I64, F32, P]),
     'xtrl_sim_reset': (I32, [P, I32, I32, U64, U32, P, P]),
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),

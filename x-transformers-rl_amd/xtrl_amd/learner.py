@@ -126,6 +126,7 @@ class Agent(nn.Module):
         self.opt_cfg = dict(lr=lr, init_lr=lr, betas=tuple(betas), a=1.27, b=1.0, weight_decay=0.,
                             regen_rate=regen_reg_rate, cautious=cautious_factor)
         self.seg_ws = torch.zeros(len(self.flat.params), device=dev, dtype=torch.int32)
+        self.opt_chunks = ops.adopt_chunks(self.flat.seg)
         self.norm_ws = torch.zeros(512, device=dev, dtype=torch.float64)
         self.clip_out = torch.zeros(2, device=dev)
         self.max_grad_norm = max_grad_norm
@@ -194,7 +195,7 @@ class Agent(nn.Module):
         ops.grad_norm(self.flat.grad, self.max_grad_norm, self.norm_ws, self.clip_out)
         o = self.opt_cfg
         ops.adopt_atan2(self.flat.flat, self.flat.grad, self.opt_m, self.opt_v, self.opt_p_init, self.flat.seg,
-                        self.seg_ws, self.clip_out, lr=o['lr'], init_lr=o['init_lr'], betas=o['betas'], a=o['a'],
+                        self.opt_chunks, self.seg_ws, self.clip_out, lr=o['lr'], init_lr=o['init_lr'], betas=o['betas'], a=o['a'],
                         b=o['b'], weight_decay=o['weight_decay'], regen_rate=o['regen_rate'], cautious=o['cautious'],
                         first_step=self.opt_first)
         self.opt_first = False

@@ -42,6 +42,13 @@ def gemm(x, w, bias=None, ln_gamma=None, residual=None, act=L.ACT_NONE, out=None
     return out
 
 
+def gemm_ex(a, b, trans_a, trans_b, M, N, K, out, bias=None, beta=0.):
+    """C[M, N] = beta C + A . B (+ bias); operand layouts as in include/xtrl_hip.h (xtrl_gemm_ex)."""
+    L.check(L.lib().xtrl_gemm_ex(int(trans_a), int(trans_b), L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), L.ptr(bias),
+                                 L.ptr(out), out.stride(0), M, N, K, float(beta), L.stream()), 'gemm_ex')
+    return out
+
+
 def layernorm(x, gamma, out=None):
     lib = L.lib()
     M, D = x.shape
@@ -188,11 +195,22 @@ def grad_norm(flat_grad, max_norm, ws, out):
                                    L.stream()), 'grad_norm')
 
 
-def adopt_atan2(p, g, m, v, p_init, seg, seg_ws, clip, *, lr, init_lr, betas, a, b, weight_decay, regen_rate,
+def adopt_chunks(seg, chunk=8192):
+    """[n_chunks][3] (start, end, tensor) pieces of the flat buffer, one workgroup each."""
+    offs = seg.tolist()
+    rows = []
+    for s_, (a, b) in enumerate(zip(offs[:-1], offs[1:])):
+        for st in range(a, b, chunk):
+            rows.append((st, min(st + chunk, b), s_))
+    return torch.tensor(rows, dtype=torch.int64, device=seg.device)
+
+
+def adopt_atan2(p, g, m, v, p_init, seg, chunks, seg_ws, clip, *, lr, init_lr, betas, a, b, weight_decay, regen_rate,
                 cautious, first_step):
-    L.check(L.lib().xtrl_adopt_atan2(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_init), p.numel(), L.ptr(seg),
-                                     seg.numel() - 1, L.ptr(seg_ws), L.ptr(clip), lr, init_lr, betas[0], betas[1], a, b,
-                                     weight_decay, regen_rate, cautious, int(first_step), L.stream()), 'adopt_atan2')
+    L.check(L.lib().xtrl_adopt_atan2(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), L.ptr(p_init), p.numel(), L.ptr(chunks),
+                                     chunks.shape[0], L.ptr(seg), seg.numel() - 1, L.ptr(seg_ws), L.ptr(clip), lr,
+                                     init_lr, betas[0], betas[1], a, b, weight_decay, regen_rate, cautious,
+                                     int(first_step), L.stream()), 'adopt_atan2')
 
 
 def ema_lerp(ema, p, weight):
