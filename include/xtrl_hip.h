@@ -55,6 +55,12 @@ int xtrl_gemm_f32(const float* X, int ldx, const float* W, int ldw, const float*
 int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
                  float* C, int ldc, int M, int N, int K, float beta, void* stream);
 
+/* nn.Linear weight gradient: dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] over M tokens.  The token
+ * range is split over workgroups (partial tiles in ws, ws_floats >= splits * N * K, up to
+ * 512 / tiles splits) and summed in fixed order — deterministic. */
+int xtrl_gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K,
+                    float beta, float* ws, int64_t ws_floats, void* stream);
+
 /* Y[m, :] = layer_norm(X[m, :]) * gamma  (x-transformers LayerNorm, final norm of the Decoder) */
 int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, void* stream);
 
@@ -135,6 +141,7 @@ typedef struct XtrlDecodeDesc {
   float* logits; /* [E][A or 2A] */
   float* v1;     /* [E][I] first layer's values (value residual) */
   float* vals;   /* [E][B] critic logits of the current step (copied to traj_values for live episodes) */
+  float* xn;     /* [E][d] layer-normalised residual stream (input of the q|k|v and FF1 projections) */
   /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
    * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
   void** prof_events;

@@ -332,16 +332,20 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   XTRL_LAUNCHED("embed");
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
-    int rc = gemm_f32(D->x, d, Ly.w_qkv, d, Ly.b_qkv, Ly.ln_attn, nullptr, 0, D->qkv, D->n_qkv, nullptr, 0, E,
-                      D->n_qkv, d, XTRL_ACT_NONE, s);
+    // pre-norm once per row (a LN prologue inside the GEMM would be recomputed by every column tile)
+    int rc = layernorm_f32(D->x, d, Ly.ln_attn, D->xn, d, E, d, s);
     if (rc) return rc;
+    if ((rc = gemm_f32(D->xn, d, Ly.w_qkv, d, Ly.b_qkv, nullptr, nullptr, 0, D->qkv, D->n_qkv, nullptr, 0, E,
+                       D->n_qkv, d, XTRL_ACT_NONE, s)))
+      return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
     if ((rc = gemm_f32(D->att, I, Ly.w_out, I, nullptr, nullptr, D->x, d, D->x, d, nullptr, 0, E, d, I,
                        XTRL_ACT_NONE, s)))
       return rc;
-    if ((rc = gemm_f32(D->x, d, Ly.w_ff1, d, Ly.b_ff1, Ly.ln_ff, nullptr, 0, D->hff, D->ff, nullptr, 0, E, D->ff, d,
+    if ((rc = layernorm_f32(D->x, d, Ly.ln_ff, D->xn, d, E, d, s))) return rc;
+    if ((rc = gemm_f32(D->xn, d, Ly.w_ff1, d, Ly.b_ff1, nullptr, nullptr, 0, D->hff, D->ff, nullptr, 0, E, D->ff, d,
                        XTRL_ACT_GELU, s)))
       return rc;
     if ((rc = gemm_f32(D->hff, D->ff, Ly.w_ff2, D->ff, Ly.b_ff2, nullptr, D->x, d, D->x, d, nullptr, 0, E, d, D->ff,

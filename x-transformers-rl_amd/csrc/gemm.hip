@@ -36,7 +36,9 @@ struct GemmArgs {
   const int32_t* t_dev;
   int64_t c_t_stride;
   int lda, ldb, ldr, ldc, M, N, K;
-  float beta;   // C = beta * C + result (accumulate into C, used by weight gradients)
+  float beta;          // C = beta * C + result (accumulate into C, used by weight gradients)
+  int kspan;           // > 0: split-K across blockIdx.z, each split covers kspan of K ...
+  int64_t c_split;     // ... and writes its partial tile at C + z * c_split (phase 2 sums them)
 };
 
 template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
@@ -52,7 +54,16 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = a.M, N = a.N, K = a.K;
+  const int M = a.M, N = a.N;
+  int K = a.K;
+  const float* __restrict__ Ab = a.A;
+  const float* __restrict__ Bb = a.B;
+  if (a.kspan > 0) {   // cross-workgroup split of K: shift the operands to this split's K range
+    const int kb = blockIdx.z * a.kspan;
+    K = min(a.kspan, a.K - kb);
+    Ab += TA ? (int64_t)kb * a.lda : kb;
+    Bb += TB ? (int64_t)kb * a.ldb : kb;
+  }
 
   if constexpr (LN) {
     constexpr int NW = WM * WN * WK;
@@ -104,7 +115,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TA) {   // [BM rows][BK/4 quads]
         const int r = e / (BK / 4), q = e % (BK / 4);
-        float4 f = load4(a.A, a.lda, m0 + r, k0 + 4 * q, M, K);
+        float4 f = load4(Ab, a.lda, m0 + r, k0 + 4 * q, M, K);
         if constexpr (LN) {
           const float mu = row_mean[r], rs = row_rstd[r];
           const int k = k0 + 4 * q;
@@ -116,7 +127,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
         ra[i] = f;
       } else {               // [BK rows][BM/4 quads]
         const int r = e / (BM / 4), q = e % (BM / 4);
-        ra[i] = load4(a.A, a.lda, k0 + r, m0 + 4 * q, K, M);
+        ra[i] = load4(Ab, a.lda, k0 + r, m0 + 4 * q, K, M);
       }
     }
 #pragma unroll
@@ -124,10 +135,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TB) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        rb[i] = load4(a.B, a.ldb, n0 + r, k0 + 4 * q, N, K);
+        rb[i] = load4(Bb, a.ldb, n0 + r, k0 + 4 * q, N, K);
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        rb[i] = load4(a.B, a.ldb, k0 + r, n0 + 4 * q, K, N);
+        rb[i] = load4(Bb, a.ldb, k0 + r, n0 + 4 * q, K, N);
       }
     }
   };
@@ -212,6 +223,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   // ---- epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 -------------
   float* C = a.C;
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
+  if (a.kspan > 0) C += blockIdx.z * a.c_split;
   const int n = n0 + wn * 32 + (lane & 31);
   if (n >= N) return;
   const float bn = a.bias ? a.bias[n] : 0.f;
@@ -248,9 +260,23 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
   for (int k = lane; k < D; k += 64) Y[(int64_t)m * ldy + k] = ((xr[k] - mean) * rstd) * gamma[k];
 }
 
+// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] (fixed order: deterministic)
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, int M, int N, float* C, int ldc,
+                                                       float beta) {
+  const int64_t MN = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
+    float acc = ws[i];
+    for (int z = 1; z < S; ++z) acc += ws[z * MN + i];
+    const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+    float* dst = C + (int64_t)m * ldc + n;
+    *dst = (beta != 0.f) ? beta * (*dst) + acc : acc;
+  }
+}
+
 template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
 void launch(const GemmArgs& a, hipStream_t s) {
-  dim3 grid((a.N + 32 * WN - 1) / (32 * WN), (a.M + 32 * WM - 1) / (32 * WM));
+  const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
+  dim3 grid((a.N + 32 * WN - 1) / (32 * WN), (a.M + 32 * WM - 1) / (32 * WM), splits);
   hipLaunchKernelGGL((k_gemm<WM, WN, WK, TA, TB, ACT, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
 }
 
@@ -282,7 +308,7 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
   XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
   XTRL_REQUIRE(!(ln_gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
   if (M == 0 || N == 0) return XTRL_OK;
-  GemmArgs a{A, B, bias, ln_gamma, R, C, t_dev, c_t_stride, lda, ldb, ldr, ldc, M, N, K, beta};
+  GemmArgs a{A, B, bias, ln_gamma, R, C, t_dev, c_t_stride, lda, ldb, ldr, ldc, M, N, K, beta, 0, 0};
   const bool vec = aligned16(A) && aligned16(B) && (lda % 4 == 0) && (ldb % 4 == 0);
   const bool ln = ln_gamma != nullptr, res = R != nullptr;
 #define XG(TA_, TB_, A_, L_, R_)                                                                   \
@@ -305,6 +331,41 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
   set_error("gemm: unsupported combination ta=%d tb=%d act=%d ln=%d residual=%d", trans_a, trans_b, act, (int)ln,
             (int)res);
   return XTRL_E_ARG;
+}
+
+// weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
+// split the token range over workgroups (partial 64x64 tiles in ws), then a fixed-order sum
+int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
+               float* ws, int64_t ws_floats, hipStream_t s) {
+  XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
+  XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
+  // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
+  const int64_t tiles = (int64_t)((N + 63) / 64) * ((K + 63) / 64);
+  int splits = (int)std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, (M + 255) / 256));
+  int kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
+  splits = (M + kspan - 1) / kspan;
+  while (splits > 1 && (int64_t)splits * N * K > ws_floats) {   // fit the partial slabs in ws
+    splits = std::max(1, splits / 2);
+    kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
+    splits = (M + kspan - 1) / kspan;
+  }
+  const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0);
+  if (splits <= 1) {
+    GemmArgs a{dY, X, nullptr, nullptr, nullptr, dW, nullptr, 0, ldy, ldx, 0, ldw, N, K, M, beta, 0, 0};
+    if (vec) launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
+    else launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
+    XTRL_LAUNCHED("gemm_wgrad");
+    return XTRL_OK;
+  }
+  XTRL_REQUIRE(ws && (int64_t)splits * N * K <= ws_floats, "gemm_wgrad: workspace too small");
+  GemmArgs a{dY, X, nullptr, nullptr, nullptr, ws, nullptr, 0, ldy, ldx, 0, K, N, K, M, 0.f, kspan, (int64_t)N * K};
+  if (vec) launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
+  else launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
+  const int64_t MN = (int64_t)N * K;
+  hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((MN + 255) / 256, 2048)), dim3(256), 0, s, ws,
+                     splits, N, K, dW, ldw, beta);
+  XTRL_LAUNCHED("gemm_wgrad");
+  return XTRL_OK;
 }
 
 int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
@@ -334,6 +395,11 @@ extern "C" int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, c
                             const float* bias, float* C, int ldc, int M, int N, int K, float beta, void* stream) {
   return xtrl::gemm_ex(trans_a, trans_b, A, lda, B, ldb, bias, nullptr, nullptr, 0, C, ldc, nullptr, 0, M, N, K,
                        XTRL_ACT_NONE, beta, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N,
+                               int K, float beta, float* ws, int64_t ws_floats, void* stream) {
+  return xtrl::gemm_wgrad(dY, ldy, X, ldx, dW, ldw, M, N, K, beta, ws, ws_floats, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D,

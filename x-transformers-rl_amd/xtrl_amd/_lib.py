@@ -46,7 +46,7 @@ class DecodeDesc(C.Structure):
                 + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
                                     'alive', 'lens', 'cum_reward', 'episode_of_slot', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
-                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals')]
+                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals', 'xn')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
 
 
@@ -64,6 +64,7 @@ SIGNATURES = {
     'xtrl_last_error': (C.c_char_p, []),
     'xtrl_gemm_f32': (I32, [P, I32, P, I32, P, P, P, I32, P, I32, P, I64, I32, I32, I32, I32, P]),
     'xtrl_gemm_ex': (I32, [I32, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, F32, P]),
+    'xtrl_gemm_wgrad': (I32, [P, I32, P, I32, P, I32, I32, I32, I32, F32, P, I64, P]),
     'xtrl_layernorm_f32': (I32, [P, I32, P, P, I32, I32, I32, P]),
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),

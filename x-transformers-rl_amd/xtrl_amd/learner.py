@@ -106,13 +106,16 @@ class Agent(nn.Module):
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
         self.model = WorldModelActorCritic(c).to(dev)
-        self.flat = FlatParams(self.model, dev)
+        self.flat = FlatParams(self.model, dev, order=self.model.flat_order())
+
         # EMA copy (ema-pytorch semantics restated: update_after_step 100, update_every 10, power 2/3)
         self.ema_model = copy.deepcopy(self.model)
         for p in self.ema_model.parameters():
             p.grad = None
         self.ema_flat = self.flat.flat.clone()
         self.flat.rebind(self.ema_model, self.ema_flat)
+        self.gemm_ws = torch.empty(4 << 20, device=dev)     # split-K weight-gradient partial tiles
+        self.model.bind_flat(self.flat, self.gemm_ws)
         self.ema_beta = ema_decay
         self.ema_update_every, self.ema_update_after = 10, 100
         self.ema_model_every = (ema_kwargs or {}).get('update_model_with_ema_every', None)

@@ -164,12 +164,66 @@ class WorldModelActorCritic(nn.Module):
     def embed_actions(self, actions):
         if self.cfg.continuous:
             return self.action_embeds(actions)
-        has = actions >= 0
-        emb = F.embedding(torch.where(has, actions, torch.zeros_like(actions)), self.action_embeds.embed.weight)
-        return emb * has[..., None].to(emb.dtype)
+        # SafeEmbedding (xtrl.py:181-195) as a one-hot product: its backward is a small GEMM
+        # instead of a scatter-add of 16K rows into A rows
+        onehot = F.one_hot(actions.clamp(min=0), self.cfg.num_actions).to(torch.float32)
+        onehot = onehot * (actions >= 0)[..., None].to(torch.float32)
+        return onehot @ self.action_embeds.embed.weight
+
+    def _zero_bias(self, n, like):
+        z = getattr(self, '_zb', None)
+        if z is None or z.shape[0] < n or z.device != like.device:
+            z = torch.zeros(max(n, 1024), device=like.device)
+            self._zb = z
+        return z[:n]
 
     def hl_value(self, logits):
         return (logits.softmax(dim=-1) * self.hl_centers).sum(-1)
+
+    # ---- flat-buffer layout / binding ---------------------------------------------------------------
+    def flat_order(self):
+        """Parameter order of the flat buffer: the q|k|v|gate|mix weights of each attention block and
+        the first actor / critic head layers are adjacent so their concatenations are views."""
+        c = self.cfg
+        names = [n for n, _ in self.named_parameters()]
+        pri = []
+        for li, (_, _) in enumerate(self.blocks()):
+            pre = f'transformer.attn_layers.layers.{2 * li}.1.'
+            mix = c.value_residual and c.learned_mix and li > 0
+            pri += [pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
+            pri += [pre + 'to_v_gate.weight'] if c.gate_values else []
+            pri += [pre + 'to_value_residual_mix.0.weight'] if mix else []
+            pri += [pre + 'to_v_gate.bias'] if c.gate_values else []
+            pri += [pre + 'to_value_residual_mix.0.bias'] if mix else []
+        pri += ['action_head.0.weight', 'critic_head.0.weight', 'action_head.0.bias', 'critic_head.0.bias']
+        taken = set(pri)
+        return pri + [n for n in names if n not in taken]
+
+    def bind_flat(self, flat, ws):
+        """Record the concatenated weight / gradient views used by forward_train."""
+        c = self.cfg
+        d, I = c.dim, c.inner
+        self._flat, self._ws = flat, ws
+        self._proj = []
+        for li, (_, _) in enumerate(self.blocks()):
+            pre = f'transformer.attn_layers.layers.{2 * li}.1.'
+            mix = c.value_residual and c.learned_mix and li > 0
+            wn = [pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
+            wn += [pre + 'to_v_gate.weight'] if c.gate_values else []
+            wn += [pre + 'to_value_residual_mix.0.weight'] if mix else []
+            bn = ([pre + 'to_v_gate.bias'] if c.gate_values else []) + ([pre + 'to_value_residual_mix.0.bias'] if mix else [])
+            n_out = 3 * I + (I if c.gate_values else 0) + (c.heads if mix else 0)
+            entry = dict(w=flat.span(wn).view(n_out, d), wg=flat.span(wn, flat.grad).view(n_out, d), mix=mix,
+                         b=flat.span(bn) if bn else None, bg=flat.span(bn, flat.grad) if bn else None)
+            self._proj.append(entry)
+        hn = ['action_head.0.weight', 'critic_head.0.weight']
+        bn = ['action_head.0.bias', 'critic_head.0.bias']
+        self._head1 = dict(w=flat.span(hn).view(4 * d, c.in_dim), wg=flat.span(hn, flat.grad).view(4 * d, c.in_dim),
+                           b=flat.span(bn), bg=flat.span(bn, flat.grad))
+
+    def _lin(self, x, mod):
+        b = mod.bias
+        return ops.xlinear(x, mod.weight, b, mod.weight.grad, b.grad if b is not None else None, self._ws)
 
     # ---- learn-step forward (xtrl.py:479-559 with the mask path of x-transformers) --------------
     def forward_train(self, state, actions, rewards, next_actions, latent_gene, lens, reward_keep=True,
@@ -177,10 +231,10 @@ class WorldModelActorCritic(nn.Module):
         c = self.cfg
         b, n, _ = state.shape
         tr = self.transformer
-        state_embed = self.to_state_embed(state)
+        state_embed = self._lin(state, self.to_state_embed)
         sum_embeds = self.embed_actions(actions) + rewards[..., None] * self.reward_embed * float(reward_keep)
-        x = tr.project_in(state) + sum_embeds
-        H, dh = c.heads, c.dim_head
+        x = self._lin(state, tr.project_in) + sum_embeds
+        H, dh, I = c.heads, c.dim_head, c.inner
         pos = torch.arange(n, device=state.device, dtype=torch.float32)
         inv = tr.attn_layers.rotary_pos_emb.inv_freq
         freqs = (pos[:, None] * inv[None, :]).repeat_interleave(2, dim=-1)
@@ -188,34 +242,48 @@ class WorldModelActorCritic(nn.Module):
         rot = freqs.shape[-1]
         p_drop = c.dropout if self.training else 0.
         first_v = None
+        split = lambda t: t.reshape(b, n, H, dh).permute(0, 2, 1, 3)
         for li, (attn_l, ff_l) in enumerate(self.blocks()):
             (ln_a, _, _), blk, _ = attn_l
             xn = ln_a(x)
-            split = lambda t: t.reshape(b, n, H, dh).permute(0, 2, 1, 3)
-            q, k, v = split(blk.to_q(xn)), split(blk.to_k(xn)), split(blk.to_v(xn))
+            P = self._proj[li]
+            # one projection for q | k | v | gate | mix: one well-shaped GEMM, gradient into the flat buffer
+            bias = None
+            if P['b'] is not None:
+                bias = torch.cat((self._zero_bias(3 * I, x), P['b']))
+            proj = ops.xlinear(xn, P['w'], bias, P['wg'], P['bg'], self._ws, bg_off=3 * I)
+            q, k, v = split(proj[..., :I]), split(proj[..., I:2 * I]), split(proj[..., 2 * I:3 * I])
+            gate_pre = proj[..., 3 * I:4 * I] if c.gate_values else None
             orig_v = v
-            if c.value_residual and first_v is not None and blk.to_value_residual_mix is not None:
-                mix = torch.sigmoid(blk.to_value_residual_mix[0](xn)).permute(0, 2, 1)[..., None]
+            if P['mix'] and first_v is not None:
+                mix = torch.sigmoid(proj[..., -H:]).permute(0, 2, 1)[..., None]
                 v = v.lerp(first_v, mix)
             if first_v is None:
                 first_v = orig_v
             q = torch.cat((q[..., :rot] * cos + _rotate_half(q[..., :rot]) * sin, q[..., rot:]), dim=-1)
             k = torch.cat((k[..., :rot] * cos + _rotate_half(k[..., :rot]) * sin, k[..., rot:]), dim=-1)
             o = ops.attention(q, k, v, lens, dh ** -0.5, p_drop, attn_seed, attn_offset + li * 65536)
-            o = o.permute(0, 2, 1, 3).reshape(b, n, H * dh)
-            if blk.to_v_gate is not None:
-                o = o * blk.to_v_gate(xn).sigmoid()
-            x = blk.to_out(o) + x
+            o = o.permute(0, 2, 1, 3).reshape(b, n, I)
+            if gate_pre is not None:
+                o = o * gate_pre.sigmoid()
+            x = self._lin(o, blk.to_out) + x
             (ln_f, _, _), ffb, _ = ff_l
-            x = ffb.ff(ln_f(x)) + x
+            h = F.gelu(self._lin(ln_f(x), ffb.ff[0][0]))
+            h = F.dropout(h, p_drop, self.training) if p_drop > 0 else h
+            x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)
         ewa = torch.cat((embed, self.embed_actions(next_actions)), dim=-1)
-        pred_raw = self.to_pred(ewa)
-        done_logit = self.to_pred_done(ewa)[..., 0]
+        pred_raw = self._lin(F.silu(self._lin(ewa, self.to_pred[0])), self.to_pred[2])
+        done_logit = self._lin(ewa, self.to_pred_done[0])[..., 0]
         f = c.frac_head_grad
         embed = embed.detach() * (1. - f) + embed * f
         ac_in = torch.cat((embed, state_embed), dim=-1)
         if c.evolutionary:
-            lat = self.latent_to_embed(latent_gene)
+            lat = self._lin(latent_gene, self.latent_to_embed)
             ac_in = torch.cat((ac_in, lat[:, None, :].expand(-1, n, -1)), dim=-1)
-        return self.action_head(ac_in), self.critic_head(ac_in), pred_raw, done_logit
+        hd = self._head1
+        hid = F.silu(ops.xlinear(ac_in, hd['w'], hd['b'], hd['wg'], hd['bg'], self._ws))
+        d2 = 2 * c.dim
+        raw_actions = self._lin(hid[..., :d2], self.action_head[2])
+        values = self._lin(hid[..., d2:], self.critic_head[2])
+        return raw_actions, values, pred_raw, done_logit

@@ -49,6 +49,50 @@ def gemm_ex(a, b, trans_a, trans_b, M, N, K, out, bias=None, beta=0.):
     return out
 
 
+def wgrad(dy, x, dw, ws, beta=1.):
+    """dw[N, K] = beta dw + dy[M, N]^T x[M, K]  (split over the M tokens, deterministic)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert dw.shape == (N, K) and dw.is_contiguous() and x.stride(1) == 1 and dy.stride(1) == 1
+    L.check(L.lib().xtrl_gemm_wgrad(L.ptr(dy), dy.stride(0), L.ptr(x), x.stride(0), L.ptr(dw), K, M, N, K,
+                                    float(beta), L.ptr(ws), ws.numel(), L.stream()), 'gemm_wgrad')
+
+
+class XLinearFn(torch.autograd.Function):
+    """nn.Linear whose parameter gradients are accumulated straight into the flat gradient
+    buffer (the weight gradient by the split-K HIP GEMM, so no per-parameter accumulation pass);
+    forward and input-gradient GEMMs stay on hipBLASLt."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wg, bg, bg_off, ws):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.extra = (wg, bg, bg_off, ws, x.shape)
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        wg, bg, bg_off, ws, xshape = ctx.extra
+        dy2 = dy.reshape(-1, w.shape[0])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = torch.mm(dy2, w).view(xshape) if ctx.needs_input_grad[0] else None
+        if wg is not None:
+            wgrad(dy2, x2, wg, ws, beta=1.)
+        if bg is not None:
+            bg.add_(dy2[:, bg_off:].sum(0))
+        return dx, None, None, None, None, None, None
+
+
+def xlinear(x, w, b, wg, bg, ws, bg_off=0):
+    return XLinearFn.apply(x, w, b, wg, bg, bg_off, ws)
+
+
 def layernorm(x, gamma, out=None):
     lib = L.lib()
     M, D = x.shape

@@ -49,7 +49,7 @@ class RolloutEngine:
         # scratch
         self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
         self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
-        self.vals = z(E, B)
+        self.vals, self.xn = z(E, B), z(E, d)
         self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
         # packed weights
         self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
@@ -93,7 +93,7 @@ class RolloutEngine:
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             t = self.traj[k]
             setattr(D, 'traj_' + k, t.data_ptr() if t is not None else None)
-        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals'):
+        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals', 'xn'):
             setattr(D, k, getattr(self, k).data_ptr())
         self.desc = D
 
