@@ -19,6 +19,7 @@ shapes = [  # (tag, M, N, K, ta, tb)
     ('fwd head1', 16384, 512, 512, 0, 0), ('fwd vals', 16384, 100, 512, 0, 0),
     ('dgrad ff1', 16384, 256, 1024, 0, 1), ('dgrad ff2', 16384, 1024, 256, 0, 1),
     ('wgrad ff1', 1024, 256, 16384, 1, 1), ('wgrad ff2', 256, 1024, 16384, 1, 1), ('wgrad qkv', 192, 256, 16384, 1, 1),
+    ('wgrad out', 256, 64, 16384, 1, 1), ('wgrad head2', 100, 512, 16384, 1, 1),
 ]
 for tag, M, N, K, ta, tb in shapes:
     A = torch.randn(K, M, device='cuda') if ta else torch.randn(M, K, device='cuda')
@@ -33,3 +34,16 @@ for tag, M, N, K, ta, tb in shapes:
     ut = timeit(lambda: torch.matmul(At, Bt, out=C))
     tf = 2 * M * N * K / us / 1e6
     print(f'{tag:10s} M={M:6d} N={N:5d} K={K:6d}  xtrl {us:8.1f} us {tf:6.1f} TF | torch {ut:8.1f} us {2*M*N*K/ut/1e6:6.1f} TF | err {err:.1e}')
+
+print('--- weight gradients through xtrl_gemm_wgrad (split over tokens) vs torch')
+ws = torch.empty(32 << 20, device='cuda')
+for tag, N, K, M in [('ff1', 1024, 256, 16384), ('ff2', 256, 1024, 16384), ('proj', 260, 256, 16384),
+                     ('out', 256, 64, 16384), ('head1', 1024, 768, 16384), ('head2', 100, 512, 16384),
+                     ('done', 1, 512, 16384), ('pin', 256, 8, 16384)]:
+    dy = torch.randn(M, N, device='cuda'); x = torch.randn(M, K, device='cuda'); dw = torch.zeros(N, K, device='cuda')
+    ops.wgrad(dy, x, dw, ws, beta=0.)
+    ref = dy.double().t() @ x.double()
+    err = float((dw.double() - ref).abs().max() / ref.abs().max())
+    us = timeit(lambda: ops.wgrad(dy, x, dw, ws, beta=0.))
+    ut = timeit(lambda: torch.mm(dy.t(), x, out=dw))
+    print(f'wgrad {tag:6s} N={N:5d} K={K:5d} M={M}  xtrl {us:8.1f} us {2*M*N*K/us/1e6:6.1f} TF | torch {ut:8.1f} us | err {err:.1e}')

@@ -41,14 +41,16 @@ struct GemmArgs {
   int64_t c_split;     // ... and writes its partial tile at C + z * c_split (phase 2 sums them)
 };
 
-template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
-  constexpr int BM = 32 * WM, BN = 32 * WN, BK = 32 * WK, NT = 64 * WM * WN * WK;
-  constexpr int AST = BM + 1, BST = BN + 1;
+  constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN, BK = 32 * WK, NT = 64 * WM * WN * WK;
+  // k-major LDS images; row stride +1 for transposed staging writes ("N" operand), +4 (16-byte rows,
+  // ds_write_b128) when the global rows are already k-major ("T" operand)
+  constexpr int AST = TA ? BM + 4 : BM + 1, BST = TB ? BN + 4 : BN + 1;
   constexpr int A_F4 = BM * BK / 4 / NT, B_F4 = BN * BK / 4 / NT;   // float4 loads per thread per slab
   static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small for the thread count");
-  __shared__ float As[2][BK][AST];
-  __shared__ float Bs[2][BK][BST];
+  __shared__ __attribute__((aligned(16))) float As[2][BK][AST];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BST];
   __shared__ float row_mean[LN ? BM : 1], row_rstd[LN ? BM : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -90,44 +92,63 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     __syncthreads();
   }
 
-  // ---- staging: element (row, k-quad) assignments --------------------------------------------
-  // "N" operand (contiguous along k): thread covers k-quad q of row r; "T" operand (contiguous
-  // along m / n): thread covers an m-quad of k-row r.
   float4 ra[A_F4], rb[B_F4];
-  auto load4 = [&](const float* base, int64_t ld, int outer, int inner, int outer_lim, int inner_lim) -> float4 {
-    // element (outer, inner .. inner+3) of a row-major [outer][inner] array
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (outer < outer_lim) {
-      const float* p = base + (int64_t)outer * ld + inner;
-      if (VEC && inner + 3 < inner_lim) {
-        const float4 f = *reinterpret_cast<const float4*>(p);
-        return f;
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (inner + c < inner_lim) v[c] = p[c];
+  // Branch-free staging loads.  Indices are clamped into the operand, so every load is in bounds;
+  // rows / columns past M or N then hold duplicates that only feed output rows / columns the
+  // epilogue discards, and only the reduction index k needs zeroing past K — which can only happen
+  // in the last slab (TAIL, a workgroup-uniform branch).  Keeping selects out of the interior slabs
+  // lets the next slab's loads stay in flight across the current slab's MFMAs.  VEC requires the
+  // contiguous extent to be a multiple of 4, so a quad is all-in or all-out.
+  auto load4 = [&](const float* base, int64_t ld, int outer, int inner, int outer_lim, int inner_lim,
+                   bool outer_is_k, bool tail) -> float4 {
+    const float* row = base + (int64_t)min(outer, outer_lim - 1) * ld;
+    float4 f;
+    if constexpr (VEC) {
+      f = *reinterpret_cast<const float4*>(row + min(inner, inner_lim - 4));
+    } else {
+      f.x = row[min(inner + 0, inner_lim - 1)];
+      f.y = row[min(inner + 1, inner_lim - 1)];
+      f.z = row[min(inner + 2, inner_lim - 1)];
+      f.w = row[min(inner + 3, inner_lim - 1)];
     }
-    return make_float4(v[0], v[1], v[2], v[3]);
+    if (tail) {
+      if (outer_is_k) {
+        const bool ok = outer < outer_lim;
+        f = make_float4(ok ? f.x : 0.f, ok ? f.y : 0.f, ok ? f.z : 0.f, ok ? f.w : 0.f);
+      } else {
+        f.x = inner + 0 < inner_lim ? f.x : 0.f;
+        f.y = inner + 1 < inner_lim ? f.y : 0.f;
+        f.z = inner + 2 < inner_lim ? f.z : 0.f;
+        f.w = inner + 3 < inner_lim ? f.w : 0.f;
+      }
+    }
+    return f;
   };
-  auto load_slab = [&](int k0) {
+  auto load_slab = [&](int k0, bool tail) {
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int e = tid + i * NT;
       if constexpr (!TA) {   // [BM rows][BK/4 quads]
         const int r = e / (BK / 4), q = e % (BK / 4);
-        float4 f = load4(Ab, a.lda, m0 + r, k0 + 4 * q, M, K);
+        float4 f = load4(Ab, a.lda, m0 + r, k0 + 4 * q, M, K, false, tail);
         if constexpr (LN) {
           const float mu = row_mean[r], rs = row_rstd[r];
           const int k = k0 + 4 * q;
-          f.x = k + 0 < K ? ((f.x - mu) * rs) * a.gamma[k + 0] : 0.f;
-          f.y = k + 1 < K ? ((f.y - mu) * rs) * a.gamma[k + 1] : 0.f;
-          f.z = k + 2 < K ? ((f.z - mu) * rs) * a.gamma[k + 2] : 0.f;
-          f.w = k + 3 < K ? ((f.w - mu) * rs) * a.gamma[k + 3] : 0.f;
+          f.x = ((f.x - mu) * rs) * a.gamma[min(k + 0, K - 1)];
+          f.y = ((f.y - mu) * rs) * a.gamma[min(k + 1, K - 1)];
+          f.z = ((f.z - mu) * rs) * a.gamma[min(k + 2, K - 1)];
+          f.w = ((f.w - mu) * rs) * a.gamma[min(k + 3, K - 1)];
+          if (tail) {
+            f.x = k + 0 < K ? f.x : 0.f;
+            f.y = k + 1 < K ? f.y : 0.f;
+            f.z = k + 2 < K ? f.z : 0.f;
+            f.w = k + 3 < K ? f.w : 0.f;
+          }
         }
         ra[i] = f;
       } else {               // [BK rows][BM/4 quads]
         const int r = e / (BM / 4), q = e % (BM / 4);
-        ra[i] = load4(Ab, a.lda, k0 + r, m0 + 4 * q, K, M);
+        ra[i] = load4(Ab, a.lda, k0 + r, m0 + 4 * q, K, M, true, tail);
       }
     }
 #pragma unroll
@@ -135,10 +156,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TB) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        rb[i] = load4(Bb, a.ldb, n0 + r, k0 + 4 * q, N, K);
+        rb[i] = load4(Bb, a.ldb, n0 + r, k0 + 4 * q, N, K, false, tail);
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        rb[i] = load4(Bb, a.ldb, k0 + r, n0 + 4 * q, K, N);
+        rb[i] = load4(Bb, a.ldb, k0 + r, n0 + 4 * q, K, N, true, tail);
       }
     }
   };
@@ -154,10 +175,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
         As[buf][4 * q + 3][r] = ra[i].w;
       } else {
         const int r = e / (BM / 4), q = e % (BM / 4);
-        As[buf][r][4 * q + 0] = ra[i].x;
-        As[buf][r][4 * q + 1] = ra[i].y;
-        As[buf][r][4 * q + 2] = ra[i].z;
-        As[buf][r][4 * q + 3] = ra[i].w;
+        *reinterpret_cast<float4*>(&As[buf][r][4 * q]) = ra[i];
       }
     }
 #pragma unroll
@@ -171,44 +189,83 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
         Bs[buf][4 * q + 3][r] = rb[i].w;
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        Bs[buf][r][4 * q + 0] = rb[i].x;
-        Bs[buf][r][4 * q + 1] = rb[i].y;
-        Bs[buf][r][4 * q + 2] = rb[i].z;
-        Bs[buf][r][4 * q + 3] = rb[i].w;
+        *reinterpret_cast<float4*>(&Bs[buf][r][4 * q]) = rb[i];
       }
     }
   };
 
-  f32x16 acc;
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nk = (K + BK - 1) / BK;
-  load_slab(0);
+  const int fi = wm * 32 * TM + (lane & 31), fj = wn * 32 * TN + (lane & 31), fk = wk * 32 + (lane >> 5);
+  // MFMA fragments double-buffered in registers: the LDS reads of step s + 1 are issued (and pinned
+  // by a scheduling barrier) ahead of step s's MFMAs, so their latency hides behind them
+  auto compute = [&](int cur) {
+    float av[2][TM], bv[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[0][i] = As[cur][fk][fi + 32 * i];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[0][j] = Bs[cur][fk][fj + 32 * j];
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int pb = st & 1;
+      if (st + 1 < 16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) av[pb ^ 1][i] = As[cur][fk + 2 * st + 2][fi + 32 * i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bv[pb ^ 1][j] = Bs[cur][fk + 2 * st + 2][fj + 32 * j];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[pb][i], bv[pb][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Software pipeline with the only possibly-partial slab (the last) peeled off: the steady-state
+  // body is one basic block (loads of slab kt + 1, MFMAs of slab kt, LDS stores of slab kt + 1), so
+  // the loads' wait lands at the stores, after the MFMAs.
+  load_slab(0, true);
   store_slab(0);
   __syncthreads();
-  const int fi = wm * 32 + (lane & 31), fj = wn * 32 + (lane & 31), fk = wk * 32 + (lane >> 5);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_slab((kt + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < 32; kk += 2) {
-      const float av = As[cur][fk + kk][fi];
-      const float bv = Bs[cur][fk + kk][fj];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-    }
-    if (kt + 1 < nk) store_slab(cur ^ 1);
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) {
+    load_slab((kt + 1) * BK, false);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMAs (the scheduler sinks them)
+    compute(kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_slab((kt & 1) ^ 1);
     __syncthreads();
   }
+  if (kt + 1 < nk) {
+    load_slab((kt + 1) * BK, true);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_slab((kt & 1) ^ 1);
+    __syncthreads();
+    ++kt;
+  }
+  compute(kt & 1);
 
   // ---- intra-workgroup split-K: waves wk > 0 hand their tiles to wk == 0 through LDS ----------
   if constexpr (WK > 1) {
-    float* red = &As[0][0][0];   // reuse the staging LDS: (WK-1) * WM*WN * 16 * 64 floats
+    static_assert(TM == 1 && TN == 1, "intra-workgroup split-K uses one tile per wave");
+    float* red = &As[0][0][0];   // reuse the staging LDS
     static_assert((WK - 1) * WM * WN * 16 * 64 <= 2 * BK * AST + 2 * BK * BST, "reduction scratch too small");
     float* mine = red + ((wk - 1) * WM * WN + wmn) * 16 * 64;
+    __syncthreads();   // every wave is done reading the last slab
     if (wk > 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mine[r * 64 + lane] = acc[r];
+      for (int r = 0; r < 16; ++r) mine[r * 64 + lane] = acc[0][0][r];
     }
     __syncthreads();
     if (wk > 0) return;
@@ -216,7 +273,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     for (int j = 1; j < WK; ++j) {
       const float* src = red + ((j - 1) * WM * WN + wmn) * 16 * 64;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += src[r * 64 + lane];
+      for (int r = 0; r < 16; ++r) acc[0][0][r] += src[r * 64 + lane];
     }
   }
 
@@ -224,20 +281,42 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   float* C = a.C;
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
   if (a.kspan > 0) C += blockIdx.z * a.c_split;
-  const int n = n0 + wn * 32 + (lane & 31);
-  if (n >= N) return;
-  const float bn = a.bias ? a.bias[n] : 0.f;
+  const bool acc_c = a.beta != 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (m < M) {
-      float v = acc[r] + bn;
-      if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
-      if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
-      if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
-      float* dst = C + (int64_t)m * a.ldc + n;
-      if (a.beta != 0.f) v = a.beta * (*dst) + v;
-      *dst = v;
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);
+    if (n >= N) continue;
+    const float bn = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
+      if (mb + 27 < M) {   // all 16 rows of this lane in range: unpredicated stores
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb + (r & 3) + 8 * (r >> 2);
+          float v = acc[i][j][r] + bn;
+          if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
+          if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
+          if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
+          float* dst = C + (int64_t)m * a.ldc + n;
+          if (acc_c) v = a.beta * (*dst) + v;
+          *dst = v;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb + (r & 3) + 8 * (r >> 2);
+          if (m < M) {
+            float v = acc[i][j][r] + bn;
+            if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
+            if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
+            if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
+            float* dst = C + (int64_t)m * a.ldc + n;
+            if (acc_c) v = a.beta * (*dst) + v;
+            *dst = v;
+          }
+        }
+      }
     }
   }
 }
@@ -260,10 +339,29 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
   for (int k = lane; k < D; k += 64) Y[(int64_t)m * ldy + k] = ((xr[k] - mean) * rstd) * gamma[k];
 }
 
-// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] (fixed order: deterministic)
+// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] (fixed order: deterministic).
+// Partials are dense [S][M][N]; each thread sums one float4 column of the S slices.
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, int M, int N, float* C, int ldc,
                                                        float beta) {
   const int64_t MN = (int64_t)M * N;
+  if ((N & 3) == 0) {
+    const int64_t Q = MN >> 2;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < Q; q += (int64_t)gridDim.x * 256) {
+      float4 acc = reinterpret_cast<const float4*>(ws)[q];
+      for (int z = 1; z < S; ++z) {
+        const float4 p = reinterpret_cast<const float4*>(ws + z * MN)[q];
+        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+      }
+      const int64_t i = q << 2;
+      const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+      float* dst = C + (int64_t)m * ldc + n;
+      if (beta != 0.f) {
+        acc.x += beta * dst[0]; acc.y += beta * dst[1]; acc.z += beta * dst[2]; acc.w += beta * dst[3];
+      }
+      dst[0] = acc.x; dst[1] = acc.y; dst[2] = acc.z; dst[3] = acc.w;
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
     float acc = ws[i];
     for (int z = 1; z < S; ++z) acc += ws[z * MN + i];
@@ -273,20 +371,24 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
   }
 }
 
-template <int WM, int WN, int WK, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
 void launch(const GemmArgs& a, hipStream_t s) {
+  constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
   const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
-  dim3 grid((a.N + 32 * WN - 1) / (32 * WN), (a.M + 32 * WM - 1) / (32 * WM), splits);
-  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TA, TB, ACT, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, ACT, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
 }
 
-// geometry choice: 64 x 64 tiles when they fill the chip, else 32 x 32 tiles with a 4-way split
-// of K inside the workgroup (decode-sized M) — both keep one 32 x 32 accumulator per wave
+// geometry: 128 x 128 tiles (2 x 2 waves of 64 x 64, four accumulator chains each) when they fill
+// the chip, else 64 x 64 tiles, else 32 x 32 tiles with a 4-way split of K inside the workgroup
+// (decode-sized M)
 template <bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
 void dispatch_geom(const GemmArgs& a, hipStream_t s) {
+  const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * ((a.N + 127) / 128);
   const int64_t tiles64 = (int64_t)((a.M + 63) / 64) * ((a.N + 63) / 64);
-  if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
-  else launch<1, 1, 4, TA, TB, ACT, LN, RES, VEC>(a, s);
+  if (tiles128 >= 192) launch<2, 2, 1, 2, 2, TA, TB, ACT, LN, RES, VEC>(a, s);
+  else if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, 1, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
+  else launch<1, 1, 4, 1, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
 }
 
 template <bool TA, bool TB, int ACT, bool LN, bool RES>
@@ -309,7 +411,8 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
   XTRL_REQUIRE(!(ln_gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
   if (M == 0 || N == 0) return XTRL_OK;
   GemmArgs a{A, B, bias, ln_gamma, R, C, t_dev, c_t_stride, lda, ldb, ldr, ldc, M, N, K, beta, 0, 0};
-  const bool vec = aligned16(A) && aligned16(B) && (lda % 4 == 0) && (ldb % 4 == 0);
+  const bool vec = aligned16(A) && aligned16(B) && (lda % 4 == 0) && (ldb % 4 == 0) &&
+                   ((trans_a ? M : K) % 4 == 0) && ((trans_b ? N : K) % 4 == 0);
   const bool ln = ln_gamma != nullptr, res = R != nullptr;
 #define XG(TA_, TB_, A_, L_, R_)                                                                   \
   if (trans_a == TA_ && trans_b == TB_ && act == A_ && ln == L_ && res == R_) {                    \
@@ -340,8 +443,15 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
   XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
   // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
-  const int64_t tiles = (int64_t)((N + 63) / 64) * ((K + 63) / 64);
-  int splits = (int)std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, (M + 255) / 256));
+  // 128 x 128 tiles (2 workgroups / CU by registers) when the weight is large, else 64 x 64 (4 / CU);
+  // split the tokens until one resident round of workgroups covers the chip, keeping at least 8
+  // K-slabs (256 tokens) per split so the pipeline reaches steady state (more splits would cost
+  // more partial-tile traffic in phase 2 than they save)
+  const bool big = (int64_t)N * K >= 256 * 256;
+  const int tm = big ? 128 : 64;
+  const int64_t tiles = (int64_t)((N + tm - 1) / tm) * ((K + tm - 1) / tm);
+  const int64_t target = big ? 512 : 1024;
+  int splits = (int)std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (M + 255) / 256));
   int kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
   splits = (M + kspan - 1) / kspan;
   while (splits > 1 && (int64_t)splits * N * K > ws_floats) {   // fit the partial slabs in ws
@@ -349,21 +459,28 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
     kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
     splits = (M + kspan - 1) / kspan;
   }
-  const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0);
-  if (splits <= 1) {
-    GemmArgs a{dY, X, nullptr, nullptr, nullptr, dW, nullptr, 0, ldy, ldx, 0, ldw, N, K, M, beta, 0, 0};
-    if (vec) launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
-    else launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
-    XTRL_LAUNCHED("gemm_wgrad");
-    return XTRL_OK;
+  const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0) && (N % 4 == 0) && (K % 4 == 0);
+  GemmArgs a{dY, X, nullptr, nullptr, nullptr, dW, nullptr, 0, ldy, ldx, 0, ldw, N, K, M, beta, 0, 0};
+  if (splits > 1) {
+    XTRL_REQUIRE(ws && (int64_t)splits * N * K <= ws_floats, "gemm_wgrad: workspace too small");
+    a.C = ws;
+    a.ldc = K;
+    a.beta = 0.f;
+    a.kspan = kspan;
+    a.c_split = (int64_t)N * K;
   }
-  XTRL_REQUIRE(ws && (int64_t)splits * N * K <= ws_floats, "gemm_wgrad: workspace too small");
-  GemmArgs a{dY, X, nullptr, nullptr, nullptr, ws, nullptr, 0, ldy, ldx, 0, K, N, K, M, 0.f, kspan, (int64_t)N * K};
-  if (vec) launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
-  else launch<2, 2, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
-  const int64_t MN = (int64_t)N * K;
-  hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((MN + 255) / 256, 2048)), dim3(256), 0, s, ws,
-                     splits, N, K, dW, ldw, beta);
+  if (big) {
+    if (vec) launch<2, 2, 1, 2, 2, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
+    else launch<2, 2, 1, 2, 2, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
+  } else {
+    if (vec) launch<2, 2, 1, 1, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
+    else launch<2, 2, 1, 1, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
+  }
+  if (splits > 1) {
+    const int64_t MN = (int64_t)N * K;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((MN + 255) / 256, 2048)), dim3(256), 0, s,
+                       ws, splits, N, K, dW, ldw, beta);
+  }
   XTRL_LAUNCHED("gemm_wgrad");
   return XTRL_OK;
 }

@@ -114,7 +114,7 @@ class Agent(nn.Module):
             p.grad = None
         self.ema_flat = self.flat.flat.clone()
         self.flat.rebind(self.ema_model, self.ema_flat)
-        self.gemm_ws = torch.empty(4 << 20, device=dev)     # split-K weight-gradient partial tiles
+        self.gemm_ws = torch.empty(32 << 20, device=dev)    # split-K weight-gradient partial tiles (128 MiB)
         self.model.bind_flat(self.flat, self.gemm_ws)
         self.ema_beta = ema_decay
         self.ema_update_every, self.ema_update_after = 10, 100
