@@ -115,6 +115,19 @@ class DecodeAttnTimer:
         self.eng.graph = None
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, written by tools/gpu_check.sh pmc from two rocprofv3 --pmc
+    passes of this bench: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of the MI355X guide)."""
+    import glob
+    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_pmc_traffic.json')))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    hits = [v for k, v in data.items() if kernel in k]
+    return round(hits[0]['traffic']) if hits else None
+
+
 def cpu_baseline(cfg, seed, budget_s):
     """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn), one
     update on a bounded number of episodes of the same workload."""
@@ -254,7 +267,7 @@ def main():
         achieved = timer.bytes / timer.launches / avg_s / 1e9
         roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache)', bound='hbm',
                         achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s', frac=round(achieved / HBM_PEAK_GBS, 4),
-                        traffic=None, avg_launch_us=round(avg_s * 1e6, 2),
+                        traffic=pmc_traffic('k_attn_decode'), avg_launch_us=round(avg_s * 1e6, 2),
                         bytes_per_launch=round(timer.bytes / timer.launches))
         timer.detach()
 

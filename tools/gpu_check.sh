@@ -21,7 +21,18 @@ run_prof() {
   find gpurun_out/prof -type f ! -name '*stats*' -delete
   if [ $rc -ne 0 ]; then echo "prof rc=$rc"; exit $rc; fi
 }
+run_pmc() {
+  # HBM traffic counters, one counter group per pass (FETCH_SIZE and WRITE_SIZE do not fit together)
+  cd /tmp && export TMPDIR=/tmp
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 900 rocprofv3 --pmc $c --kernel-include-regex "k_attn_decode|k_gemm" -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$c -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log 2>&1
+    rc=$?; tail -2 $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log
+    if [ $rc -ne 0 ]; then echo "pmc $c rc=$rc"; exit $rc; fi
+  done
+  cd $GRAFT_REPO_ROOT && python3 tools/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.txt; cat gpurun_out/pmc_summary.txt
+}
 case $what in
+  pmc) run_pmc "$@" ;;
   tests) run_tests ;;
   bench) run_bench "$@" ;;
   prof) run_prof "$@" ;;
