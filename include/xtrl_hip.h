@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 1
+#define XTRL_ABI_VERSION 2
 
 int xtrl_abi_version(void);
 const char* xtrl_last_error(void);
@@ -183,6 +183,101 @@ int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t*
 int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
                   const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b,
                   int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Learn-step forward / backward of WorldModelActorCritic on one minibatch, hand-scheduled (no
+ * autograd): replaces `model(..., mask=mask)` + `loss.backward()` of Agent.learn
+ * (xtrl.py:928-935, 982) with the x-transformers Decoder inside.
+ *   T = b * n tokens (token t = episode * n + step), activations token-major [T][features].
+ *   Parameters live in ONE fp32 buffer `flat`; gradients at the same offsets of `grad`
+ *   (accumulated: the caller zeroes `grad`).  Offsets are in floats, -1 = absent.
+ * Forward writes raw / values / pred / done (the inputs of xtrl_loss_fwd) and saves what the
+ * backward needs; backward consumes d_raw / d_values / d_pred / d_done (xtrl_loss_bwd).
+ * Feed-forward dropout keep(m, n) = philox(seed; n, m >> 2, ff_offset + layer, (7 << 24)) word
+ * (m & 3) >= p * 2^32; attention dropout as xtrl_attn_fwd with offset attn_offset + layer * 65536.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct XtrlTrainLayer {
+  int64_t ln_attn, w_proj, b_proj, w_out, ln_ff, w_ff1, b_ff1, w_ff2, b_ff2;
+  int n_qkv;            /* 3I (+ I value gates) (+ H value-residual mix, layers >= 2) */
+  int mix;              /* learned value-residual mix in this layer */
+  float* x_attn;        /* [T][d] residual stream entering the attention block */
+  float* x_ff;          /* [T][d] entering the feed-forward block */
+  float* xn_attn;       /* [T][d] LayerNorm outputs */
+  float* xn_ff;
+  float* st_attn;       /* [T][2] LayerNorm (mean, rstd) */
+  float* st_ff;
+  float* proj;          /* [T][n_qkv] q | k | v | gate | mix pre-activations */
+  float* qkv;           /* [T][3I] rotary q, k and (mixed) v */
+  float* o;             /* [T][I] attention output */
+  float* og;            /* [T][I] gated output (== o when there are no value gates) */
+  float* lse;           /* [b][H][n] */
+  float* u;             /* [T][ff] FF1 pre-activation */
+  float* hd;            /* [T][ff] GELU + dropout output */
+} XtrlTrainLayer;
+
+typedef struct XtrlTrainDesc {
+  int b, n, S, A, d, L, H, dh, ff, B, in_dim, n_out, G;
+  int continuous, evolutionary, gate_values, rot_dim;
+  float dropout, frac_head_grad, reward_keep, attn_scale;
+  uint64_t seed;
+  uint32_t attn_offset, ff_offset;
+  float* flat;
+  float* grad;
+  int64_t w_pin, act_emb, act_emb_b, reward_embed, w_se, b_se, ln_final;
+  int64_t w_pd, b_pd;   /* to_pred.0 | to_pred_done: weights [d + 1][2d], biases [d + 1], adjacent */
+  int64_t w_pred2, b_pred2, w_lat, b_lat, w_h1, b_h1, w_a2, b_a2, w_c2, b_c2;
+  const float* inv_freq;         /* [rot_dim / 2] */
+  /* minibatch */
+  const float* swr;              /* [T][S + 1] normalised states | normalised previous reward */
+  const int32_t* prev_action;    /* [T] discrete, -1 = none */
+  const int32_t* next_action;    /* [T] */
+  const float* prev_action_f;    /* [T][A] continuous */
+  const float* next_action_f;
+  const float* latent;           /* [b][G] (evolutionary) */
+  const int32_t* lens;           /* [b] */
+  /* forward outputs */
+  float* raw;                    /* [T][n_out] */
+  float* values;                 /* [T][B] */
+  float* pred;                   /* [T][2 (S + 1)] */
+  float* done;                   /* [T] */
+  /* head activations */
+  float* x_final;                /* [T][d] residual stream after the last block */
+  float* st_final;               /* [T][2] */
+  float* ac_in;                  /* [T][in_dim] embed | state_embed | latent_embed */
+  float* ewa;                    /* [T][2d] embed | next-action embed */
+  float* zp;                     /* [T][d + 4] pre-activation of to_pred.0 | to_pred_done */
+  float* hp;                     /* [T][d + 4] SiLU(to_pred.0) | done logit */
+  float* z1;                     /* [T][4d] pre-activation of action_head.0 | critic_head.0 */
+  float* h1;                     /* [T][4d] SiLU */
+  float* lat_e;                  /* [b][d] */
+  /* loss gradients */
+  const float* d_raw;
+  const float* d_values;
+  const float* d_pred;
+  const float* d_done;
+  /* backward scratch */
+  float* dx;                     /* [T][d] */
+  float* dxn;                    /* [T][d] */
+  float* dff;                    /* [T][ff] */
+  float* dproj;                  /* [T][max n_qkv] */
+  float* dog;                    /* [T][I] */
+  float* dvfirst;                /* [T][I] */
+  float* dz1;                    /* [T][4d] */
+  float* dac;                    /* [T][in_dim] */
+  float* dzp;                    /* [T][d + 4] */
+  float* dewa;                   /* [T][2d] */
+  float* delta;                  /* [b][H][n] */
+  float* part;                   /* deterministic partial sums */
+  int64_t part_floats;
+  float* ws;                     /* split-K weight-gradient partial tiles */
+  int64_t ws_floats;
+  const XtrlTrainLayer* layers;  /* host array [L] */
+} XtrlTrainDesc;
+
+int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
+int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream);
+/* the feed-forward dropout keep mask of layer `layer` as uint8 [M][N] (tests / reference mode) */
+int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused PPO / critic / world-model / done loss   (xtrl.py:398-477 losses, :939-978 combination)

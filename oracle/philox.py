@@ -32,6 +32,7 @@ FIELD_TERM = 3
 FIELD_SAMPLE = 4
 FIELD_COIN = 5
 FIELD_DROPOUT = 6
+FIELD_FF_DROPOUT = 7
 
 SQRT3 = np.float32(1.7320508075688772)
 

@@ -30,7 +30,8 @@ def test_struct_layouts_match_header():
     from xtrl_amd import _lib
     header = (REPO / 'include' / 'xtrl_hip.h').read_text()
     for cname, py in (('XtrlDecodeLayer', _lib.DecodeLayer), ('XtrlDecodeDesc', _lib.DecodeDesc),
-                      ('XtrlLossDesc', _lib.LossDesc), ('XtrlRngState', _lib.RngState)):
+                      ('XtrlLossDesc', _lib.LossDesc), ('XtrlRngState', _lib.RngState),
+                      ('XtrlTrainLayer', _lib.TrainLayer), ('XtrlTrainDesc', _lib.TrainDesc)):
         body = re.search(r'typedef struct %s \{(.*?)\} %s;' % (cname, cname), header, re.S).group(1)
         body = re.sub(r'/\*.*?\*/', '', body, flags=re.S)
         names = []
@@ -41,7 +42,7 @@ def test_struct_layouts_match_header():
             decl = re.sub(r'^(const\s+)?\w+\s*\**', '', decl)   # drop the type of the first declarator
             for part in decl.split(','):
                 part = part.strip().lstrip('*').strip()
-                part = re.sub(r'^(const\s+)?(int|float|uint8_t|int32_t|uint32_t|uint64_t|double|XtrlDecodeLayer|XtrlRngState)\s*\**\s*', '', part)
+                part = re.sub(r'^(const\s+)?(int|float|uint8_t|int32_t|int64_t|uint32_t|uint64_t|double|XtrlDecodeLayer|XtrlRngState|XtrlTrainLayer)\s*\**\s*', '', part)
                 if part:
                     names.append(part)
         assert names == [f[0] for f in py._fields_], (cname, names, [f[0] for f in py._fields_])

@@ -9,7 +9,7 @@
 // row pad; the probability tile crosses LDS once per wave to turn the MFMA C layout (rows on
 // lane groups) into the A layout (rows on lanes), in a 66-float-stride image (conflict-free read).
 // Dropout keep bits: philox(seed; c0 = i >> 2, c1 = j, c2 = offset + b*H + h) word (i & 3).
-#include "common.h"
+#include "kernels.h"
 #include "philox.h"
 
 namespace xtrl {
@@ -30,10 +30,11 @@ __device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, int i
 }
 
 struct AttnArgs {
-  const float *Q, *K, *V, *O, *LSE, *dO, *Dl;
-  float *Oout, *LSEout, *dQ, *dK, *dV, *Dout;
+  const float *Q, *K, *V, *O, *LSE, *dO, *Dl, *G;
+  float *Oout, *LSEout, *dQ, *dK, *dV, *Dout, *OGout;
   const int32_t* lens;
   int H, n;
+  AttnLayout in, out, grad, gate;   // q/k/v; o/do/og; dq/dk/dv; gate
   float scale, inv_keep;
   uint32_t thresh;    // keep iff word >= thresh (thresh = 0: no dropout)
   uint64_t seed;
@@ -50,7 +51,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
   const int q0 = blockIdx.x * TQ;
   const int len = a.lens[b];
-  const int64_t base = (int64_t)bh * n * DH;
+  const int h = bh - b * a.H;
+  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh;
+  const int isi = a.in.si, osi = a.out.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
 
@@ -58,7 +61,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
   {
     const int i = q0 + 16 * w + lr;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) qa[s] = (i < n) ? a.Q[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
+    for (int s = 0; s < KS; ++s) qa[s] = (i < n) ? a.Q[ib + (int64_t)i * isi + 4 * s + lg] : 0.f;
   }
   float m[4], l[4];
   f32x4v o[ND];
@@ -75,8 +78,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     __syncthreads();
     for (int x = tid; x < TK * DH; x += 256) {
       const int j = x / DH, c = x - j * DH, jj = kt * TK + j;
-      Ks[j][c] = jj < n ? a.K[base + (int64_t)jj * DH + c] : 0.f;
-      Vs[j][c] = jj < n ? a.V[base + (int64_t)jj * DH + c] : 0.f;
+      Ks[j][c] = jj < n ? a.K[ib + (int64_t)jj * isi + c] : 0.f;
+      Vs[j][c] = jj < n ? a.V[ib + (int64_t)jj * isi + c] : 0.f;
     }
     __syncthreads();
     f32x4v sacc[4];
@@ -133,7 +136,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     const int i = q0 + 16 * w + 4 * lg + r;
     if (i < n) {
 #pragma unroll
-      for (int d = 0; d < ND; ++d) a.Oout[base + (int64_t)i * DH + 16 * d + lr] = o[d][r] / l[r];
+      for (int d = 0; d < ND; ++d) {
+        const int64_t at = ob + (int64_t)i * osi + 16 * d + lr;
+        const float ov = o[d][r] / l[r];
+        a.Oout[at] = ov;
+        if (a.OGout)   // gated values (x-transformers attn_gate_values)
+          a.OGout[at] = ov * sigmoidf_(a.G[b * a.gate.sb + h * a.gate.sh + (int64_t)i * a.gate.si + 16 * d + lr]);
+      }
       if (lr == 0) a.LSEout[(int64_t)bh * n + i] = m[r] + logf(l[r]);
     }
   }
@@ -143,8 +152,10 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 __global__ void k_attn_delta(const AttnArgs a, int rows, int DH) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= rows) return;
+  const int bh = r / a.n, i = r - bh * a.n, b = bh / a.H, h = bh - b * a.H;
+  const int64_t at = b * a.out.sb + h * a.out.sh + (int64_t)i * a.out.si;
   float s = 0.f;
-  for (int c = 0; c < DH; ++c) s += a.dO[(int64_t)r * DH + c] * a.O[(int64_t)r * DH + c];
+  for (int c = 0; c < DH; ++c) s += a.dO[at + c] * a.O[at + c];
   a.Dout[r] = s;
 }
 
@@ -159,7 +170,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
   const int j0 = blockIdx.x * TK;
   const int len = a.lens[b];
-  const int64_t base = (int64_t)bh * n * DH;
+  const int h = bh - b * a.H;
+  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
 
@@ -168,8 +181,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
     const int j = j0 + 16 * w + lr;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      ka[s] = (j < n) ? a.K[base + (int64_t)j * DH + 4 * s + lg] : 0.f;
-      va[s] = (j < n) ? a.V[base + (int64_t)j * DH + 4 * s + lg] : 0.f;
+      ka[s] = (j < n) ? a.K[ib + (int64_t)j * isi + 4 * s + lg] : 0.f;
+      va[s] = (j < n) ? a.V[ib + (int64_t)j * isi + 4 * s + lg] : 0.f;
     }
   }
   f32x4v dk[ND], dv[ND];
@@ -183,8 +196,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
       __syncthreads();
       for (int x = tid; x < TQ * DH; x += 256) {
         const int i = x / DH, c = x - i * DH, ii = qt * TQ + i;
-        Qs[i][c] = ii < n ? a.Q[base + (int64_t)ii * DH + c] : 0.f;
-        dOs[i][c] = ii < n ? a.dO[base + (int64_t)ii * DH + c] : 0.f;
+        Qs[i][c] = ii < n ? a.Q[ib + (int64_t)ii * isi + c] : 0.f;
+        dOs[i][c] = ii < n ? a.dO[ob + (int64_t)ii * osi + c] : 0.f;
       }
       if (tid < TQ) {
         const int ii = qt * TQ + tid;
@@ -229,8 +242,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
     if (j < n) {
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        a.dK[base + (int64_t)j * DH + 16 * d + lr] = dk[d][r] * a.scale;
-        a.dV[base + (int64_t)j * DH + 16 * d + lr] = dv[d][r];
+        a.dK[gb + (int64_t)j * gsi + 16 * d + lr] = dk[d][r] * a.scale;
+        a.dV[gb + (int64_t)j * gsi + 16 * d + lr] = dv[d][r];
       }
     }
   }
@@ -246,7 +259,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
   const int q0 = blockIdx.x * TQ;
   const int len = a.lens[b];
-  const int64_t base = (int64_t)bh * n * DH;
+  const int h = bh - b * a.H;
+  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
 
@@ -255,8 +270,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
     const int i = q0 + 16 * w + lr;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      qa[s] = (i < n) ? a.Q[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
-      da[s] = (i < n) ? a.dO[base + (int64_t)i * DH + 4 * s + lg] : 0.f;
+      qa[s] = (i < n) ? a.Q[ib + (int64_t)i * isi + 4 * s + lg] : 0.f;
+      da[s] = (i < n) ? a.dO[ob + (int64_t)i * osi + 4 * s + lg] : 0.f;
     }
   }
   float lse[4], dl[4];
@@ -274,8 +289,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
     __syncthreads();
     for (int x = tid; x < TK * DH; x += 256) {
       const int j = x / DH, c = x - j * DH, jj = kt * TK + j;
-      Ks[j][c] = jj < n ? a.K[base + (int64_t)jj * DH + c] : 0.f;
-      Vs[j][c] = jj < n ? a.V[base + (int64_t)jj * DH + c] : 0.f;
+      Ks[j][c] = jj < n ? a.K[ib + (int64_t)jj * isi + c] : 0.f;
+      Vs[j][c] = jj < n ? a.V[ib + (int64_t)jj * isi + c] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -309,55 +324,59 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
     const int i = q0 + 16 * w + 4 * lg + r;
     if (i < n) {
 #pragma unroll
-      for (int d = 0; d < ND; ++d) a.dQ[base + (int64_t)i * DH + 16 * d + lr] = dq[d][r] * a.scale;
+      for (int d = 0; d < ND; ++d) a.dQ[gb + (int64_t)i * gsi + 16 * d + lr] = dq[d][r] * a.scale;
     }
   }
 }
 
-int fill_args(AttnArgs& a, const int32_t* lens, int H, int n, int dh, float scale, float p, uint64_t seed,
-              uint32_t offset) {
-  XTRL_REQUIRE(dh == 16 || dh == 32 || dh == 64, "attn: dim_head %d unsupported (16/32/64)", dh);
-  XTRL_REQUIRE(lens && H > 0 && n > 0, "attn: bad arguments");
-  XTRL_REQUIRE(p >= 0.f && p < 1.f, "attn: dropout %f outside [0, 1)", p);
-  a.lens = lens;
-  a.H = H;
-  a.n = n;
-  a.scale = scale;
-  a.inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const double th = (double)p * 4294967296.0;
-  a.thresh = p > 0.f ? (uint32_t)fmin(th, 4294967295.0) : 0u;
-  if (p > 0.f && a.thresh == 0) a.thresh = 1;
-  a.seed = seed;
-  a.offset = offset;
+int fill_args(AttnArgs& a, const AttnProblem& p) {
+  XTRL_REQUIRE(p.dh == 16 || p.dh == 32 || p.dh == 64, "attn: dim_head %d unsupported (16/32/64)", p.dh);
+  XTRL_REQUIRE(p.lens && p.H > 0 && p.n > 0 && p.b > 0, "attn: bad arguments");
+  XTRL_REQUIRE(p.dropout >= 0.f && p.dropout < 1.f, "attn: dropout %f outside [0, 1)", p.dropout);
+  a.lens = p.lens;
+  a.H = p.H;
+  a.n = p.n;
+  a.in = p.in;
+  a.out = p.out;
+  a.grad = p.grad;
+  a.gate = p.gate;
+  a.scale = p.scale;
+  a.inv_keep = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
+  a.thresh = dropout_thresh(p.dropout);
+  a.seed = p.seed;
+  a.offset = p.offset;
   return XTRL_OK;
 }
 
 }  // namespace
 
-int attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o, float* lse, int b, int H,
-             int n, int dh, float scale, float p, uint64_t seed, uint32_t offset, hipStream_t s) {
+int attn_fwd_ex(const AttnProblem& p, const float* q, const float* k, const float* v, float* o, float* lse,
+                const float* gate, float* og, hipStream_t s) {
   AttnArgs a{};
-  if (int rc = fill_args(a, lens, H, n, dh, scale, p, seed, offset)) return rc;
-  XTRL_REQUIRE(q && k && v && o && lse && b > 0, "attn_fwd: null operand");
+  if (int rc = fill_args(a, p)) return rc;
+  XTRL_REQUIRE(q && k && v && o && lse, "attn_fwd: null operand");
+  XTRL_REQUIRE(!gate == !og, "attn_fwd: gate and og go together");
   a.Q = q;
   a.K = k;
   a.V = v;
   a.Oout = o;
   a.LSEout = lse;
-  dim3 grid((n + TQ - 1) / TQ, b * H);
-  if (dh == 16) hipLaunchKernelGGL(k_attn_fwd<16>, grid, dim3(256), 0, s, a);
-  else if (dh == 32) hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, s, a);
+  a.G = gate;
+  a.OGout = og;
+  dim3 grid((p.n + TQ - 1) / TQ, p.b * p.H);
+  if (p.dh == 16) hipLaunchKernelGGL(k_attn_fwd<16>, grid, dim3(256), 0, s, a);
+  else if (p.dh == 32) hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, s, a);
   XTRL_LAUNCHED("attn_fwd");
   return XTRL_OK;
 }
 
-int attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o, const float* lse,
-             const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b, int H, int n, int dh,
-             float scale, float p, uint64_t seed, uint32_t offset, hipStream_t s) {
+int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const float* v, const float* o,
+                const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
+                hipStream_t s) {
   AttnArgs a{};
-  if (int rc = fill_args(a, lens, H, n, dh, scale, p, seed, offset)) return rc;
-  XTRL_REQUIRE(q && k && v && o && lse && dout && dq && dk && dv && delta_ws && b > 0, "attn_bwd: null operand");
+  if (int rc = fill_args(a, p)) return rc;
+  XTRL_REQUIRE(q && k && v && o && lse && dout && dq && dk && dv && delta_ws, "attn_bwd: null operand");
   a.Q = q;
   a.K = k;
   a.V = v;
@@ -369,14 +388,14 @@ int attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens
   a.dQ = dq;
   a.dK = dk;
   a.dV = dv;
-  const int rows = b * H * n;
-  hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, s, a, rows, dh);
+  const int rows = p.b * p.H * p.n;
+  hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, s, a, rows, p.dh);
   XTRL_LAUNCHED("attn_delta");
-  dim3 grid((n + TQ - 1) / TQ, b * H);
-  if (dh == 16) {
+  dim3 grid((p.n + TQ - 1) / TQ, p.b * p.H);
+  if (p.dh == 16) {
     hipLaunchKernelGGL(k_attn_bwd_dkdv<16>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_attn_bwd_dq<16>, grid, dim3(256), 0, s, a);
-  } else if (dh == 32) {
+  } else if (p.dh == 32) {
     hipLaunchKernelGGL(k_attn_bwd_dkdv<32>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_attn_bwd_dq<32>, grid, dim3(256), 0, s, a);
   } else {
@@ -387,18 +406,26 @@ int attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens
   return XTRL_OK;
 }
 
+AttnProblem contiguous_problem(const int32_t* lens, int b, int H, int n, int dh, float scale, float p, uint64_t seed,
+                               uint32_t offset) {
+  AttnProblem pr{b, H, n, dh, lens, scale, p, seed, offset, {}, {}, {}, {}};
+  pr.in = pr.out = pr.grad = attn_layout_bhnd(H, n, dh);
+  return pr;
+}
+
 }  // namespace xtrl
 
 extern "C" int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o,
                              float* lse, int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
                              uint32_t offset, void* stream) {
-  return xtrl::attn_fwd(q, k, v, lens, o, lse, b, H, n, dh, scale, dropout_p, seed, offset, xtrl::as_stream(stream));
+  return xtrl::attn_fwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset), q, k, v, o,
+                           lse, nullptr, nullptr, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
                              const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
                              int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
                              uint32_t offset, void* stream) {
-  return xtrl::attn_bwd(q, k, v, lens, o, lse, dout, dq, dk, dv, delta_ws, b, H, n, dh, scale, dropout_p, seed,
-                        offset, xtrl::as_stream(stream));
+  return xtrl::attn_bwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset), q, k, v, o,
+                           lse, dout, dq, dk, dv, delta_ws, xtrl::as_stream(stream));
 }

@@ -20,28 +20,24 @@
 // The optional LayerNorm prologue (x-transformers LayerNorm: no affine, eps 1e-5, times gamma;
 // A "N" only) computes per-row mean / rstd for the block's rows (two-pass) and normalises A while
 // staging it.
-#include "common.h"
+#include "kernels.h"
+#include "philox.h"
 
 namespace xtrl {
 
 namespace {
 
-struct GemmArgs {
-  const float* A;
-  const float* B;
-  const float* bias;
-  const float* gamma;
-  const float* R;
-  float* C;
-  const int32_t* t_dev;
-  int64_t c_t_stride;
-  int lda, ldb, ldr, ldc, M, N, K;
-  float beta;          // C = beta * C + result (accumulate into C, used by weight gradients)
-  int kspan;           // > 0: split-K across blockIdx.z, each split covers kspan of K ...
-  int64_t c_split;     // ... and writes its partial tile at C + z * c_split (phase 2 sums them)
-};
+__device__ __forceinline__ float gelu_grad_(float x) {   // torch GeluBackward (erf form)
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * expf(x * x * -0.5f);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float silu_grad_(float x) {   // torch silu_backward factor
+  const float sg = 1.0f / (1.0f + expf(-x));
+  return sg * (1.0f + x * (1.0f - sg));
+}
 
-template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN, BK = 32 * WK, NT = 64 * WM * WN * WK;
   // k-major LDS images; row stride +1 for transposed staging writes ("N" operand), +4 (16-byte rows,
@@ -282,39 +278,57 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
   if (a.kspan > 0) C += blockIdx.z * a.c_split;
   const bool acc_c = a.beta != 0.f;
+  constexpr bool DROP = (EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);
     if (n >= N) continue;
-    const float bn = a.bias ? a.bias[n] : 0.f;
+    const float bn = (a.bias && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
+    const bool act = n < a.act_cols;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
-      if (mb + 27 < M) {   // all 16 rows of this lane in range: unpredicated stores
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mb + (r & 3) + 8 * (r >> 2);
-          float v = acc[i][j][r] + bn;
-          if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
-          if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
+      for (int g = 0; g < 4; ++g) {
+        // rows mb + 8g + 0..3 (a 4-aligned group): one Philox block gives their four keep words
+        u32x4_t kw{0u, 0u, 0u, 0u};
+        if (DROP && a.drop_thresh)
+          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
+                             a.seed);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = mb + 8 * g + q;
+          if (m >= M) continue;
+          float v = acc[i][j][4 * g + q] + bn;
+          const uint32_t word = q == 0 ? kw.x : (q == 1 ? kw.y : (q == 2 ? kw.z : kw.w));
+          if constexpr (EPI == EPI_GELU) v = geluf_(v);
+          if constexpr (EPI == EPI_SILU) v = siluf_(v);
+          if constexpr (EPI == EPI_GELU_DROP) {
+            a.aux_out[(int64_t)m * a.ld_aux_out + n] = v;
+            v = geluf_(v);
+            if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
+          }
+          if constexpr (EPI == EPI_SILU_SAVE) {
+            a.aux_out[(int64_t)m * a.ld_aux_out + n] = v;
+            if (act) v = siluf_(v);
+          }
+          if constexpr (EPI == EPI_DGELU_DROP) {
+            if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
+            v = v * gelu_grad_(a.aux_in[(int64_t)m * a.ld_aux_in + n]);
+          }
+          if constexpr (EPI == EPI_DSILU) {
+            if (act) v = v * silu_grad_(a.aux_in[(int64_t)m * a.ld_aux_in + n]);
+          }
+          if constexpr (EPI == EPI_DGATE) {
+            const float sg = sigmoidf_(a.aux_in2[(int64_t)m * a.ld_aux_in2 + n]);
+            const float o = a.aux_in[(int64_t)m * a.ld_aux_in + n];
+            a.aux_out[(int64_t)m * a.ld_aux_out + n] = (v * o) * (1.0f - sg) * sg;
+            v = v * sg;
+          }
           if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
           float* dst = C + (int64_t)m * a.ldc + n;
           if (acc_c) v = a.beta * (*dst) + v;
           *dst = v;
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mb + (r & 3) + 8 * (r >> 2);
-          if (m < M) {
-            float v = acc[i][j][r] + bn;
-            if constexpr (ACT == XTRL_ACT_GELU) v = geluf_(v);
-            if constexpr (ACT == XTRL_ACT_SILU) v = siluf_(v);
-            if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
-            float* dst = C + (int64_t)m * a.ldc + n;
-            if (acc_c) v = a.beta * (*dst) + v;
-            *dst = v;
-          }
         }
       }
     }
@@ -371,69 +385,84 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
   }
 }
 
-template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
 void launch(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
   const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, ACT, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
+  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, EPI, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
 }
 
 // geometry: 128 x 128 tiles (2 x 2 waves of 64 x 64, four accumulator chains each) when they fill
 // the chip, else 64 x 64 tiles, else 32 x 32 tiles with a 4-way split of K inside the workgroup
-// (decode-sized M)
-template <bool TA, bool TB, int ACT, bool LN, bool RES, bool VEC>
-void dispatch_geom(const GemmArgs& a, hipStream_t s) {
+// (decode-sized M).  Operands whose contiguous extent is not a multiple of 4 (or unaligned) take
+// the scalar-load variant, instantiated for the 64 x 64 geometry only.
+template <bool TA, bool TB, int EPI, bool LN, bool RES>
+void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * ((a.N + 127) / 128);
   const int64_t tiles64 = (int64_t)((a.M + 63) / 64) * ((a.N + 63) / 64);
-  if (tiles128 >= 192) launch<2, 2, 1, 2, 2, TA, TB, ACT, LN, RES, VEC>(a, s);
-  else if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, 1, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
-  else launch<1, 1, 4, 1, 1, TA, TB, ACT, LN, RES, VEC>(a, s);
-}
-
-template <bool TA, bool TB, int ACT, bool LN, bool RES>
-void dispatch_vec(const GemmArgs& a, bool vec, hipStream_t s) {
-  if (vec) dispatch_geom<TA, TB, ACT, LN, RES, true>(a, s);
-  else dispatch_geom<TA, TB, ACT, LN, RES, false>(a, s);
+  if (!vec) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, false>(a, s);
+  else if (tiles128 >= 192) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  else launch<1, 1, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
-int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
-            const float* ln_gamma, const float* R, int ldr, float* C, int ldc, const int32_t* t_dev,
-            int64_t c_t_stride, int M, int N, int K, int act, float beta, hipStream_t s) {
-  XTRL_REQUIRE(A && B && C, "gemm: null operand");
-  XTRL_REQUIRE(M >= 0 && N >= 0 && K > 0, "gemm: bad shape M=%d N=%d K=%d", M, N, K);
-  XTRL_REQUIRE(lda >= (trans_a ? M : K) && ldb >= (trans_b ? N : K) && ldc >= N, "gemm: leading dims too small");
-  XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
-  XTRL_REQUIRE(!(ln_gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
-  if (M == 0 || N == 0) return XTRL_OK;
-  GemmArgs a{A, B, bias, ln_gamma, R, C, t_dev, c_t_stride, lda, ldb, ldr, ldc, M, N, K, beta, 0, 0};
-  const bool vec = aligned16(A) && aligned16(B) && (lda % 4 == 0) && (ldb % 4 == 0) &&
-                   ((trans_a ? M : K) % 4 == 0) && ((trans_b ? N : K) % 4 == 0);
-  const bool ln = ln_gamma != nullptr, res = R != nullptr;
-#define XG(TA_, TB_, A_, L_, R_)                                                                   \
-  if (trans_a == TA_ && trans_b == TB_ && act == A_ && ln == L_ && res == R_) {                    \
-    dispatch_vec<TA_, TB_, A_, L_, R_>(a, vec, s);                                                 \
+int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s) {
+  XTRL_REQUIRE(a.A && a.B && a.C, "gemm: null operand");
+  XTRL_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
+  XTRL_REQUIRE(a.lda >= (trans_a ? a.M : a.K) && a.ldb >= (trans_b ? a.N : a.K) && a.ldc >= a.N,
+               "gemm: leading dims too small");
+  XTRL_REQUIRE(!(a.gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
+  XTRL_REQUIRE(!((epi == EPI_GELU_DROP || epi == EPI_SILU_SAVE || epi == EPI_DGATE) && !a.aux_out),
+               "gemm: epilogue %d needs aux_out", epi);
+  XTRL_REQUIRE(!((epi == EPI_DGELU_DROP || epi == EPI_DSILU || epi == EPI_DGATE) && !a.aux_in),
+               "gemm: epilogue %d needs aux_in", epi);
+  XTRL_REQUIRE(!(epi == EPI_DGATE && !a.aux_in2), "gemm: gate epilogue needs aux_in2");
+  if (a.M == 0 || a.N == 0) return XTRL_OK;
+  const bool vec = aligned16(a.A) && aligned16(a.B) && (a.lda % 4 == 0) && (a.ldb % 4 == 0) &&
+                   ((trans_a ? a.M : a.K) % 4 == 0) && ((trans_b ? a.N : a.K) % 4 == 0);
+  const bool ln = a.gamma != nullptr, res = a.R != nullptr;
+#define XG(TA_, TB_, E_, L_, R_)                                                                   \
+  if (trans_a == TA_ && trans_b == TB_ && epi == E_ && ln == L_ && res == R_) {                    \
+    dispatch_geom<TA_, TB_, E_, L_, R_>(a, vec, s);                                                \
     XTRL_LAUNCHED("gemm_f32");                                                                     \
     return XTRL_OK;                                                                                \
   }
   // forward / decode (A row-major, B = nn.Linear weight)
-  XG(0, 0, XTRL_ACT_NONE, false, false)
-  XG(0, 0, XTRL_ACT_NONE, false, true)
-  XG(0, 0, XTRL_ACT_NONE, true, false)
-  XG(0, 0, XTRL_ACT_GELU, true, false)
-  XG(0, 0, XTRL_ACT_GELU, false, false)
-  XG(0, 0, XTRL_ACT_SILU, false, false)
-  // dgrad (B = weight used as [k][n]) and wgrad (A = dY^T)
-  XG(0, 1, XTRL_ACT_NONE, false, false)
-  XG(1, 1, XTRL_ACT_NONE, false, false)
+  XG(0, 0, EPI_NONE, false, false)
+  XG(0, 0, EPI_NONE, false, true)
+  XG(0, 0, EPI_NONE, true, false)
+  XG(0, 0, EPI_GELU, true, false)
+  XG(0, 0, EPI_GELU, false, false)
+  XG(0, 0, EPI_SILU, false, false)
+  XG(0, 0, EPI_GELU_DROP, false, false)
+  XG(0, 0, EPI_SILU_SAVE, false, false)
+  // dgrad (B = weight used as [k][n]) with fused activation / dropout / gate backward
+  XG(0, 1, EPI_NONE, false, false)
+  XG(0, 1, EPI_DGELU_DROP, false, false)
+  XG(0, 1, EPI_DSILU, false, false)
+  XG(0, 1, EPI_DGATE, false, false)
+  // wgrad (A = dY^T)
+  XG(1, 1, EPI_NONE, false, false)
 #undef XG
-  set_error("gemm: unsupported combination ta=%d tb=%d act=%d ln=%d residual=%d", trans_a, trans_b, act, (int)ln,
+  set_error("gemm: unsupported combination ta=%d tb=%d epi=%d ln=%d residual=%d", trans_a, trans_b, epi, (int)ln,
             (int)res);
   return XTRL_E_ARG;
+}
+
+int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
+            const float* ln_gamma, const float* R, int ldr, float* C, int ldc, const int32_t* t_dev,
+            int64_t c_t_stride, int M, int N, int K, int act, float beta, hipStream_t s) {
+  XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
+  GemmArgs a;
+  a.A = A; a.B = B; a.bias = bias; a.gamma = ln_gamma; a.R = R; a.C = C; a.t_dev = t_dev;
+  a.c_t_stride = c_t_stride; a.lda = lda; a.ldb = ldb; a.ldr = ldr; a.ldc = ldc; a.M = M; a.N = N; a.K = K;
+  a.beta = beta;
+  return gemm_run(a, trans_a, trans_b, act, s);
 }
 
 // weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
@@ -460,7 +489,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
     splits = (M + kspan - 1) / kspan;
   }
   const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0) && (N % 4 == 0) && (K % 4 == 0);
-  GemmArgs a{dY, X, nullptr, nullptr, nullptr, dW, nullptr, 0, ldy, ldx, 0, ldw, N, K, M, beta, 0, 0};
+  GemmArgs a;
+  a.A = dY; a.B = X; a.C = dW; a.lda = ldy; a.ldb = ldx; a.ldc = ldw; a.M = N; a.N = K; a.K = M; a.beta = beta;
   if (splits > 1) {
     XTRL_REQUIRE(ws && (int64_t)splits * N * K <= ws_floats, "gemm_wgrad: workspace too small");
     a.C = ws;
@@ -469,13 +499,9 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
     a.kspan = kspan;
     a.c_split = (int64_t)N * K;
   }
-  if (big) {
-    if (vec) launch<2, 2, 1, 2, 2, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
-    else launch<2, 2, 1, 2, 2, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
-  } else {
-    if (vec) launch<2, 2, 1, 1, 1, true, true, XTRL_ACT_NONE, false, false, true>(a, s);
-    else launch<2, 2, 1, 1, 1, true, true, XTRL_ACT_NONE, false, false, false>(a, s);
-  }
+  if (!vec) launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, false>(a, s);
+  else if (big) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
+  else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
   if (splits > 1) {
     const int64_t MN = (int64_t)N * K;
     hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((MN + 255) / 256, 2048)), dim3(256), 0, s,

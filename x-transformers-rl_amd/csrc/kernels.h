@@ -1,0 +1,99 @@
+// Internal (C++) interfaces shared between the translation units of libxtrl_hip.
+// Not part of the C-ABI: include/xtrl_hip.h is.
+#pragma once
+#include "common.h"
+
+namespace xtrl {
+
+// ---------------------------------------------------------------------------------------------
+// fp32 MFMA GEMM (gemm.hip)
+//   C[m, n] = epi( LN?(A)[m, :] . B[:, n] + bias ) (+ R[m, n]);   C = beta * C + result
+// Operand layouts:  A "N": A[m][k] at A[m * lda + k]    A "T": A[m][k] at A[k * lda + m]
+//                   B "N": B[k][n] at B[n * ldb + k]    B "T": B[k][n] at B[k * ldb + n]
+// ---------------------------------------------------------------------------------------------
+enum GemmEpi : int {
+  EPI_NONE = 0,        // (bias)
+  EPI_GELU = 1,        // gelu(v)
+  EPI_SILU = 2,        // silu(v)
+  EPI_GELU_DROP = 3,   // aux_out = v; C = dropout(gelu(v))                       (FF1 forward, train)
+  EPI_SILU_SAVE = 4,   // aux_out = v; C = n < act_cols ? silu(v) : v              (head hidden layers)
+  EPI_DGELU_DROP = 5,  // C = dropout_bwd(v) * gelu'(aux_in)                        (FF2 dgrad -> FF1 pre-act)
+  EPI_DSILU = 6,       // C = n < act_cols ? v * silu'(aux_in) : v
+  EPI_DGATE = 7,       // s = sigmoid(aux_in2): C = v * s; aux_out = v * aux_in * (1 - s) * s   (value gate)
+};
+
+struct GemmArgs {
+  const float* A = nullptr;
+  const float* B = nullptr;
+  const float* bias = nullptr;    // bias[n - bias_col0] for n >= bias_col0
+  const float* gamma = nullptr;   // LayerNorm prologue (A "N" only)
+  const float* R = nullptr;       // residual
+  float* C = nullptr;
+  const int32_t* t_dev = nullptr; // C += (*t_dev) * c_t_stride (decode writes into trajectory rows)
+  int64_t c_t_stride = 0;
+  int lda = 0, ldb = 0, ldr = 0, ldc = 0, M = 0, N = 0, K = 0;
+  float beta = 0.f;
+  int kspan = 0;                  // > 0: split K over blockIdx.z (partial tiles at C + z * c_split)
+  int64_t c_split = 0;
+  int bias_col0 = 0;
+  int act_cols = 1 << 30;
+  const float* aux_in = nullptr;  int ld_aux_in = 0;
+  const float* aux_in2 = nullptr; int ld_aux_in2 = 0;
+  float* aux_out = nullptr;       int ld_aux_out = 0;
+  uint64_t seed = 0;              // dropout (EPI_GELU_DROP / EPI_DGELU_DROP): keep(m, n) =
+  uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT) word (m & 3)
+  uint32_t drop_thresh = 0;       //   >= drop_thresh (0: no dropout)
+  float inv_keep = 1.f;
+};
+
+// launch C = op(A, B) for the combination (trans_a, trans_b, epi, LN = gamma != 0, RES = R != 0)
+int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s);
+// dW[N][K] (+)= dY^T X over M tokens, split-K over workgroups with a fixed-order reduction
+int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
+               float* ws, int64_t ws_floats, hipStream_t s);
+int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
+             const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
+             int K, int act, hipStream_t s);
+int layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, hipStream_t s);
+
+// dropout threshold of probability p on a uint32 word: keep iff word >= thresh
+inline uint32_t dropout_thresh(float p) {
+  if (!(p > 0.f)) return 0u;
+  const double th = (double)p * 4294967296.0;
+  const uint32_t t = (uint32_t)fmin(th, 4294967295.0);
+  return t ? t : 1u;
+}
+
+// ---------------------------------------------------------------------------------------------
+// training attention on strided operands (attn.hip)
+//   element (b, h, i, c) of a tensor with layout L is at P + b * L.sb + h * L.sh + i * L.si + c
+// ---------------------------------------------------------------------------------------------
+struct AttnLayout {
+  int64_t sb, sh;
+  int si;
+};
+inline AttnLayout attn_layout_bhnd(int H, int n, int dh) {
+  return AttnLayout{(int64_t)H * n * dh, (int64_t)n * dh, dh};
+}
+inline AttnLayout attn_layout_tokens(int n, int ld, int dh) {   // [b*n][ld], head h at column h*dh
+  return AttnLayout{(int64_t)n * ld, (int64_t)dh, ld};
+}
+
+struct AttnProblem {
+  int b, H, n, dh;
+  const int32_t* lens;
+  float scale, dropout;
+  uint64_t seed;
+  uint32_t offset;
+  AttnLayout in, out, grad;   // q/k/v; o/do (and og); dq/dk/dv
+  AttnLayout gate;            // gate pre-activations (x-transformers attn_gate_values)
+};
+
+// o (ungated) and lse; if gate != nullptr also og = o * sigmoid(gate) (og in the `out` layout)
+int attn_fwd_ex(const AttnProblem& p, const float* q, const float* k, const float* v, float* o, float* lse,
+                const float* gate, float* og, hipStream_t s);
+int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const float* v, const float* o,
+                const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
+                hipStream_t s);
+
+}  // namespace xtrl

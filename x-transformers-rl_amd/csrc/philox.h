@@ -17,7 +17,8 @@ enum RngField : uint32_t {
   FIELD_TERM = 3,
   FIELD_SAMPLE = 4,
   FIELD_COIN = 5,
-  FIELD_DROPOUT = 6,
+  FIELD_DROPOUT = 6,      // attention probabilities (learn)
+  FIELD_FF_DROPOUT = 7,   // feed-forward hidden units (learn)
 };
 
 struct u32x4_t {

@@ -1,0 +1,662 @@
+// Learn-step forward / backward of WorldModelActorCritic on one minibatch without autograd
+// (Agent.learn, x_transformers_rl.py:928-935 forward with mask, :982 backward; the x-transformers
+// Decoder restated in SURVEY Appendix A).  The dense layers run on the fused fp32 MFMA GEMM with
+// their elementwise neighbours folded into prologues / epilogues (LayerNorm, bias, GELU + dropout,
+// SiLU, residual, value gate, and their derivatives), the attention core on the strided flash
+// kernels, and everything else in the handful of small kernels below.  All reductions over tokens
+// (bias / LayerNorm-gain / embedding gradients) are two-phase with a fixed summation order, so the
+// step is deterministic run to run.
+#include "kernels.h"
+#include "philox.h"
+
+namespace xtrl {
+namespace {
+
+constexpr int kMaxDPerLane = 8;   // LayerNorm kernels: d <= 512
+
+__device__ __forceinline__ float ldg(const float* p) { return __builtin_nontemporal_load(p); }
+
+// ---- embeddings: x0 = project_in(state) + action_embed(prev) + reward * keep * reward_embed;
+//      ac_in[:, d:2d] = to_state_embed(state); ewa[:, d:2d] = action_embed(next);
+//      ac_in[:, 2d:3d] = latent_to_embed(gene)  (xtrl.py:494-503, 516-549)
+struct EmbedArgs {
+  const float *swr, *w_pin, *act_emb, *act_emb_b, *reward_embed, *w_se, *b_se, *lat_e, *prev_af, *next_af;
+  const int32_t *prev_a, *next_a;
+  float *x0, *ac_in, *ewa;
+  int T, n, S, A, d, in_dim, continuous, evolutionary;
+  float keep;
+};
+
+__global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)a.T * a.d) return;
+  const int t = (int)(i / a.d), c = (int)(i - (int64_t)t * a.d);
+  const float* st = a.swr + (int64_t)t * (a.S + 1);
+  float pin = 0.f, se = 0.f;
+  for (int s = 0; s < a.S; ++s) {
+    const float x = st[s];
+    pin += x * a.w_pin[(int64_t)c * a.S + s];
+    se += x * a.w_se[(int64_t)c * a.S + s];
+  }
+  se += a.b_se[c];
+  float ap, an;
+  if (a.continuous) {
+    const float* w = a.act_emb + (int64_t)c * a.A;
+    ap = 0.f;
+    an = 0.f;
+    for (int k = 0; k < a.A; ++k) {
+      ap += a.prev_af[(int64_t)t * a.A + k] * w[k];
+      an += a.next_af[(int64_t)t * a.A + k] * w[k];
+    }
+    ap += a.act_emb_b[c];
+    an += a.act_emb_b[c];
+  } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
+    const int p = a.prev_a[t], q = a.next_a[t];
+    ap = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
+    an = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
+  }
+  const float r = st[a.S];
+  a.x0[i] = pin + (ap + (r * a.reward_embed[c]) * a.keep);
+  a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se;
+  a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an;
+  if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = a.lat_e[(int64_t)(t / a.n) * a.d + c];
+}
+
+// lat_e[b][c] = latent[b] . w[c] + bias[c]
+__global__ void k_latent_embed(const float* latent, const float* w, const float* bias, float* out, int b, int G,
+                               int d) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b * d) return;
+  const int e = i / d, c = i - e * d;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += latent[(int64_t)e * G + g] * w[(int64_t)c * G + g];
+  out[i] = s + bias[c];
+}
+
+// ---- LayerNorm (x-transformers: layer_norm without affine, eps 1e-5, times gamma) ------------
+// one wave per row; y written to y1 (and y2 when given); stats = (mean, rstd)
+__global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gamma, float* y1, int ld1, float* y2,
+                                                int ld2, float* stats, int T, int d) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const float* xr = x + (int64_t)t * d;
+  float v[kMaxDPerLane];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) {
+    const int c = lane + 64 * k;
+    v[k] = c < d ? xr[c] : 0.f;
+    s += v[k];
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) {
+    const int c = lane + 64 * k;
+    const float dl = c < d ? v[k] - mean : 0.f;
+    q += dl * dl;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) {
+    const int c = lane + 64 * k;
+    if (c < d) {
+      const float y = ((v[k] - mean) * rstd) * gamma[c];
+      y1[(int64_t)t * ld1 + c] = y;
+      if (y2) y2[(int64_t)t * ld2 + c] = y;
+    }
+  }
+  if (lane == 0) {
+    stats[2 * t] = mean;
+    stats[2 * t + 1] = rstd;
+  }
+}
+
+// LayerNorm backward for ROWS rows per block (4 waves): upstream gradient g = s1 * g1 + g2 (g2
+// optional), dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)) (+ dres, in place
+// allowed: dx may alias dres); per-block partial d gamma = sum_rows g * xhat -> part[block][d]
+constexpr int LN_ROWS = 64;
+__global__ __launch_bounds__(256) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2, int ldg2,
+                                                const float* x, const float* stats, const float* gamma,
+                                                const float* dres, float* dx, float* part, int T, int d) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float dg[kMaxDPerLane];
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) dg[k] = 0.f;
+  const int r0 = blockIdx.x * LN_ROWS;
+  for (int r = w; r < LN_ROWS; r += 4) {
+    const int t = r0 + r;
+    if (t >= T) break;
+    const float mean = stats[2 * t], rstd = stats[2 * t + 1];
+    float gg[kMaxDPerLane], xh[kMaxDPerLane];
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxDPerLane; ++k) {
+      const int c = lane + 64 * k;
+      float g = 0.f, xhat = 0.f, gm = 0.f;
+      if (c < d) {
+        g = s1 * g1[(int64_t)t * ldg1 + c];
+        if (g2) g += g2[(int64_t)t * ldg2 + c];
+        xhat = (x[(int64_t)t * d + c] - mean) * rstd;
+        gm = g * gamma[c];
+        dg[k] += g * xhat;
+      }
+      gg[k] = gm;
+      xh[k] = xhat;
+      sa += gm;
+      sb += gm * xhat;
+    }
+    const float ma = wave_sum(sa) / (float)d, mb = wave_sum(sb) / (float)d;
+#pragma unroll
+    for (int k = 0; k < kMaxDPerLane; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d) {
+        float v = rstd * (gg[k] - ma - xh[k] * mb);
+        if (dres) v += dres[(int64_t)t * d + c];
+        dx[(int64_t)t * d + c] = v;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) {
+    const int c = lane + 64 * k;
+    if (c < d) red[w][c] = dg[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 256)
+    part[(int64_t)blockIdx.x * d + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+// ---- rotary + value-residual mix (x-transformers Attention) --------------
+// one thread per (token, head): q, k rotated on their first rot_dim channels (interleaved pairs,
+// position = step within the episode); v mixed towards the first layer's v
+struct PrepArgs {
+  const float* proj;    // [T][n_qkv]
+  const float* vfirst;  // layer-0 proj (v at column 2I)
+  float* qkv;           // [T][3I]
+  const float* inv_freq;
+  int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col;   // mix_col < 0: no mix
+};
+
+__global__ __launch_bounds__(256) void k_qkv_prep(const PrepArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.T * a.H) return;
+  const int t = i / a.H, h = i - t * a.H;
+  const float pos = (float)(t % a.n);
+  const float* pr = a.proj + (int64_t)t * a.n_qkv;
+  float* out = a.qkv + (int64_t)t * 3 * a.I;
+  for (int which = 0; which < 2; ++which) {
+    const float* src = pr + which * a.I + h * a.dh;
+    float* dst = out + which * a.I + h * a.dh;
+    for (int j = 0; j < a.dh; j += 2) {
+      const float x0 = src[j], x1 = src[j + 1];
+      if (j < a.rot_dim) {
+        const float f = pos * a.inv_freq[j >> 1];
+        const float cs = cosf(f), sn = sinf(f);
+        dst[j] = x0 * cs + (-x1) * sn;
+        dst[j + 1] = x1 * cs + x0 * sn;
+      } else {
+        dst[j] = x0;
+        dst[j + 1] = x1;
+      }
+    }
+  }
+  const float* v = pr + 2 * a.I + h * a.dh;
+  float* dv = out + 2 * a.I + h * a.dh;
+  if (a.mix_col >= 0) {
+    const float m = sigmoidf_(pr[a.mix_col + h]);
+    const float* vf = a.vfirst + (int64_t)t * a.ld_vfirst + 2 * a.I + h * a.dh;
+    for (int j = 0; j < a.dh; ++j) dv[j] = lerpf_(v[j], vf[j], m);
+  } else {
+    for (int j = 0; j < a.dh; ++j) dv[j] = v[j];
+  }
+}
+
+// backward of k_qkv_prep, in place on dproj ([T][n_qkv], dq | dk | dv written by the attention
+// backward): inverse rotation of dq, dk; lerp backward for v (dv -> (1 - m) dv, dvfirst += m dv,
+// d mix_pre = sum(dv * (vf - v)) * m (1 - m)); layer 0 adds the accumulated dvfirst to its dv
+struct PrepBwdArgs {
+  float* dproj;
+  const float* proj;
+  const float* vfirst;
+  float* dvfirst;       // [T][I]
+  const float* inv_freq;
+  int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col, first_layer, accumulate;
+};
+
+__global__ __launch_bounds__(256) void k_qkv_prep_bwd(const PrepBwdArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.T * a.H) return;
+  const int t = i / a.H, h = i - t * a.H;
+  const float pos = (float)(t % a.n);
+  float* dr = a.dproj + (int64_t)t * a.n_qkv;
+  for (int which = 0; which < 2; ++which) {
+    float* g = dr + which * a.I + h * a.dh;
+    for (int j = 0; j < a.rot_dim && j < a.dh; j += 2) {
+      const float f = pos * a.inv_freq[j >> 1];
+      const float cs = cosf(f), sn = sinf(f);
+      const float g0 = g[j], g1 = g[j + 1];
+      g[j] = g0 * cs + g1 * sn;
+      g[j + 1] = g1 * cs + (-g0) * sn;
+    }
+  }
+  float* gv = dr + 2 * a.I + h * a.dh;
+  float* dvf = a.dvfirst + (int64_t)t * a.I + h * a.dh;
+  if (a.mix_col >= 0) {
+    const float* pr = a.proj + (int64_t)t * a.n_qkv;
+    const float m = sigmoidf_(pr[a.mix_col + h]);
+    const float* v = pr + 2 * a.I + h * a.dh;
+    const float* vf = a.vfirst + (int64_t)t * a.ld_vfirst + 2 * a.I + h * a.dh;
+    float dm = 0.f;
+    for (int j = 0; j < a.dh; ++j) {
+      const float g = gv[j];
+      dm += g * (vf[j] - v[j]);
+      gv[j] = g * (1.0f - m);
+      dvf[j] = a.accumulate ? dvf[j] + g * m : g * m;
+    }
+    dr[a.mix_col + h] = dm * (1.0f - m) * m;
+  } else if (a.first_layer && a.accumulate) {
+    for (int j = 0; j < a.dh; ++j) gv[j] += dvf[j];
+  }
+}
+
+// ---- deterministic column sums: part[chunk][c] = sum over the chunk's rows of w_r * src[r][c] --
+__global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, int rows, int cols, int chunk_rows,
+                                                     const float* rw, int ld_rw, float rw_scale, float* part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
+  float s = 0.f;
+  if (rw) {
+    for (int r = r0; r < r1; ++r) s += src[(int64_t)r * ld + c] * (rw[(int64_t)r * ld_rw] * rw_scale);
+  } else {
+    for (int r = r0; r < r1; ++r) s += src[(int64_t)r * ld + c];
+  }
+  part[(int64_t)blockIdx.y * cols + c] = s;
+}
+
+// dst[c] += sum_k part[k][c]   (fixed order)
+__global__ __launch_bounds__(256) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * cols + c];
+  dst[c] += s;
+}
+
+// discrete action-embedding gradient: part[chunk][a][c] = sum over rows of the chunk with
+// prev[r] == a of g1[r][c]  +  rows with next[r] == a of g2[r][c]
+__global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld1, const int32_t* prev,
+                                                         const float* g2, int ld2, const int32_t* next, int rows,
+                                                         int d, int A, int chunk_rows, float* part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
+  float* out = part + (int64_t)blockIdx.y * A * d;
+  for (int a = 0; a < A; ++a) out[(int64_t)a * d + c] = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const int p = prev[r], q = next[r];
+    if (p >= 0) out[(int64_t)p * d + c] += g1[(int64_t)r * ld1 + c];
+    if (q >= 0) out[(int64_t)q * d + c] += g2[(int64_t)r * ld2 + c];
+  }
+}
+
+// latent gradient of the evolutionary conditioning: dlat[e][c] = sum_steps dac[e*n + s][2d + c]
+__global__ void k_latent_grad(const float* dac, int ld, int off, int b, int n, int d, float* dlat) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b * d) return;
+  const int e = i / d, c = i - e * d;
+  float s = 0.f;
+  for (int t = 0; t < n; ++t) s += dac[((int64_t)e * n + t) * ld + off + c];
+  dlat[i] = s;
+}
+
+// dW[c][g] += sum_e dlat[e][c] latent[e][g];  db[c] += sum_e dlat[e][c]
+__global__ void k_latent_wgrad(const float* dlat, const float* latent, int b, int d, int G, float* dw, float* db) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d * (G + 1)) return;
+  const int c = i / (G + 1), g = i - c * (G + 1);
+  float s = 0.f;
+  if (g < G) {
+    for (int e = 0; e < b; ++e) s += dlat[(int64_t)e * d + c] * latent[(int64_t)e * G + g];
+    dw[(int64_t)c * G + g] += s;
+  } else {
+    for (int e = 0; e < b; ++e) s += dlat[(int64_t)e * d + c];
+    db[c] += s;
+  }
+}
+
+__global__ void k_copy_col(const float* src, int ld, float* dst, int lddst, int rows) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < rows) dst[(int64_t)r * lddst] = src[(int64_t)r * ld];
+}
+
+__global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint64_t seed, uint32_t off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(m >> 2), off, rng_c3(FIELD_FF_DROPOUT, 0), seed);
+  const int q = m & 3;
+  const uint32_t w = q == 0 ? r.x : (q == 1 ? r.y : (q == 2 ? r.z : r.w));
+  mask[i] = (uint8_t)(thresh == 0 || w >= thresh);
+}
+
+// ---- host helpers -----------------------------------------------------------------------------
+inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+struct Ctx {
+  const XtrlTrainDesc* D;
+  hipStream_t s;
+  int T;
+  const float* P(int64_t off) const { return off >= 0 ? D->flat + off : nullptr; }
+  float* G(int64_t off) const { return off >= 0 ? D->grad + off : nullptr; }
+};
+
+// C[M][N] = A[M][K] . W[N][K]^T (+ bias) with an epilogue
+int linear_fwd(const Ctx& c, const float* A, int lda, const float* W, const float* bias, float* C, int ldc, int M,
+               int N, int K, int epi, const float* R = nullptr, float* aux_out = nullptr, int ld_aux = 0,
+               int act_cols = 1 << 30, int bias_col0 = 0, uint32_t drop_off = 0) {
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
+  g.R = R; g.ldr = ldc; g.aux_out = aux_out; g.ld_aux_out = ld_aux; g.act_cols = act_cols; g.bias_col0 = bias_col0;
+  if (epi == EPI_GELU_DROP) {
+    g.seed = c.D->seed;
+    g.drop_off = drop_off;
+    g.drop_thresh = dropout_thresh(c.D->dropout);
+    g.inv_keep = c.D->dropout > 0.f ? 1.f / (1.f - c.D->dropout) : 1.f;
+  }
+  return gemm_run(g, 0, 0, epi, c.s);
+}
+
+// dX[M][K] = dY[M][N] . W[N][K] with an epilogue
+int linear_dgrad(const Ctx& c, const float* dY, int ldy, const float* W, float* dX, int ldx, int M, int N, int K,
+                 int epi, const float* aux_in = nullptr, int ld_aux = 0, int act_cols = 1 << 30,
+                 uint32_t drop_off = 0, const float* aux_in2 = nullptr, int ld_aux2 = 0, float* aux_out = nullptr,
+                 int ld_aux_out = 0) {
+  GemmArgs g;
+  g.A = dY; g.lda = ldy; g.B = W; g.ldb = K; g.C = dX; g.ldc = ldx; g.M = M; g.N = K; g.K = N;
+  g.aux_in = aux_in; g.ld_aux_in = ld_aux; g.act_cols = act_cols;
+  g.aux_in2 = aux_in2; g.ld_aux_in2 = ld_aux2; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
+  if (epi == EPI_DGELU_DROP) {
+    g.seed = c.D->seed;
+    g.drop_off = drop_off;
+    g.drop_thresh = dropout_thresh(c.D->dropout);
+    g.inv_keep = c.D->dropout > 0.f ? 1.f / (1.f - c.D->dropout) : 1.f;
+  }
+  return gemm_run(g, 0, 1, epi, c.s);
+}
+
+int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float* dW, int M, int N, int K) {
+  return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s);
+}
+
+// dst[0:cols] += sum over rows of src (optionally weighted by rw[r * ld_rw] * rw_scale)
+int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* dst, const float* rw = nullptr,
+           int ld_rw = 0, float rw_scale = 1.f) {
+  if (!dst || cols <= 0) return XTRL_OK;
+  int chunks = std::min(256, std::max(1, rows / 32));
+  const int chunk_rows = (rows + chunks - 1) / chunks;
+  chunks = (rows + chunk_rows - 1) / chunk_rows;
+  XTRL_REQUIRE((int64_t)chunks * cols <= c.D->part_floats, "train: partial-sum workspace too small");
+  hipLaunchKernelGGL(k_colsum_part, dim3(blocks(cols, 256), chunks), dim3(256), 0, c.s, src, ld, rows, cols,
+                     chunk_rows, rw, ld_rw, rw_scale, c.D->part);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 256)), dim3(256), 0, c.s, c.D->part, chunks, cols, dst);
+  XTRL_LAUNCHED("train colsum");
+  return XTRL_OK;
+}
+
+int ln_fwd(const Ctx& c, const float* x, const float* gamma, float* y1, int ld1, float* y2, int ld2, float* st) {
+  hipLaunchKernelGGL(k_ln_fwd, dim3(blocks(c.T, 4)), dim3(256), 0, c.s, x, gamma, y1, ld1, y2, ld2, st, c.T,
+                     c.D->d);
+  XTRL_LAUNCHED("train ln_fwd");
+  return XTRL_OK;
+}
+
+int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, int ldg2, const float* x,
+           const float* st, const float* gamma, const float* dres, float* dx, float* dgamma) {
+  const int d = c.D->d, nb = (int)blocks(c.T, LN_ROWS);
+  XTRL_REQUIRE((int64_t)nb * d <= c.D->part_floats, "train: partial-sum workspace too small");
+  hipLaunchKernelGGL(k_ln_bwd, dim3(nb), dim3(256), 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx,
+                     c.D->part, c.T, d);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 256)), dim3(256), 0, c.s, c.D->part, nb, d, dgamma);
+  XTRL_LAUNCHED("train ln_bwd");
+  return XTRL_OK;
+}
+
+AttnProblem attn_problem(const Ctx& c, const XtrlTrainLayer& Ly, int li) {
+  const XtrlTrainDesc* D = c.D;
+  const int I = D->H * D->dh;
+  AttnProblem p{};
+  p.b = D->b;
+  p.H = D->H;
+  p.n = D->n;
+  p.dh = D->dh;
+  p.lens = D->lens;
+  p.scale = D->attn_scale;
+  p.dropout = D->dropout;
+  p.seed = D->seed;
+  p.offset = D->attn_offset + (uint32_t)li * 65536u;
+  p.in = attn_layout_tokens(D->n, 3 * I, D->dh);
+  p.out = attn_layout_tokens(D->n, I, D->dh);
+  p.grad = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
+  p.gate = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
+  return p;
+}
+
+int validate(const XtrlTrainDesc* D) {
+  XTRL_REQUIRE(D && D->layers && D->flat && D->grad, "train: null descriptor / layers / parameters");
+  XTRL_REQUIRE(D->b > 0 && D->n > 0 && D->d > 0 && D->L > 0 && D->H > 0 && D->dh > 0, "train: bad sizes");
+  XTRL_REQUIRE(D->d <= 64 * kMaxDPerLane, "train: d = %d > %d unsupported", D->d, 64 * kMaxDPerLane);
+  XTRL_REQUIRE(D->dh % 2 == 0 && D->rot_dim <= D->dh, "train: bad rotary dims");
+  XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "train: in_dim mismatch");
+  XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "train: evolutionary needs latent buffers");
+  XTRL_REQUIRE(D->continuous ? (D->prev_action_f && D->next_action_f) : (D->prev_action && D->next_action),
+               "train: missing action inputs");
+  return XTRL_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
+  if (int rc = validate(D)) return rc;
+  const Ctx c{D, s, D->b * D->n};
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4;
+  int rc;
+  // embeddings
+  if (D->evolutionary) {
+    hipLaunchKernelGGL(k_latent_embed, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->latent, c.P(D->w_lat),
+                       c.P(D->b_lat), D->lat_e, D->b, D->G, d);
+  }
+  EmbedArgs ea{D->swr, c.P(D->w_pin), c.P(D->act_emb), c.P(D->act_emb_b), c.P(D->reward_embed), c.P(D->w_se),
+               c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
+               D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
+               D->evolutionary, D->reward_keep};
+  hipLaunchKernelGGL(k_embed, dim3(blocks((int64_t)T * d, 256)), dim3(256), 0, s, ea);
+  XTRL_LAUNCHED("train embed");
+  // decoder blocks
+  for (int li = 0; li < D->L; ++li) {
+    const XtrlTrainLayer& Ly = D->layers[li];
+    if ((rc = ln_fwd(c, Ly.x_attn, c.P(Ly.ln_attn), Ly.xn_attn, d, nullptr, 0, Ly.st_attn))) return rc;
+    if ((rc = linear_fwd(c, Ly.xn_attn, d, c.P(Ly.w_proj), c.P(Ly.b_proj), Ly.proj, Ly.n_qkv, T, Ly.n_qkv, d,
+                         EPI_NONE, nullptr, nullptr, 0, 1 << 30, 3 * I)))
+      return rc;
+    const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
+    PrepArgs pa{Ly.proj, D->layers[0].proj, Ly.qkv, D->inv_freq, T, D->n, D->H, D->dh, I, Ly.n_qkv,
+                D->layers[0].n_qkv, D->rot_dim, mix_col};
+    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks((int64_t)T * D->H, 256)), dim3(256), 0, s, pa);
+    XTRL_LAUNCHED("train qkv_prep");
+    const AttnProblem ap = attn_problem(c, Ly, li);
+    if ((rc = attn_fwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse,
+                          D->gate_values ? Ly.proj + 3 * I : nullptr, D->gate_values ? Ly.og : nullptr, s)))
+      return rc;
+    if ((rc = linear_fwd(c, D->gate_values ? Ly.og : Ly.o, I, c.P(Ly.w_out), nullptr, Ly.x_ff, d, T, d, I, EPI_NONE,
+                         Ly.x_attn)))
+      return rc;
+    if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
+    if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, ff, T, ff, d, EPI_GELU_DROP, nullptr,
+                         Ly.u, ff, 1 << 30, 0, D->ff_offset + (uint32_t)li)))
+      return rc;
+    float* x_out = li + 1 < D->L ? D->layers[li + 1].x_attn : D->x_final;
+    if ((rc = linear_fwd(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
+  }
+  // final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
+  if ((rc = ln_fwd(c, D->x_final, c.P(D->ln_final), D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final))) return rc;
+  // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
+  if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
+                       nullptr, D->zp, ldp, d)))
+    return rc;
+  const int S1x2 = 2 * (D->S + 1);
+  if ((rc = linear_fwd(c, D->hp, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred, S1x2, T, S1x2, d, EPI_NONE)))
+    return rc;
+  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->hp + d, ldp, D->done, 1, T);
+  // actor | critic first layers in one GEMM, then the two output layers
+  if ((rc = linear_fwd(c, D->ac_in, D->in_dim, c.P(D->w_h1), c.P(D->b_h1), D->h1, 4 * d, T, 4 * d, D->in_dim,
+                       EPI_SILU_SAVE, nullptr, D->z1, 4 * d)))
+    return rc;
+  if ((rc = linear_fwd(c, D->h1, 4 * d, c.P(D->w_a2), c.P(D->b_a2), D->raw, D->n_out, T, D->n_out, 2 * d, EPI_NONE)))
+    return rc;
+  if ((rc = linear_fwd(c, D->h1 + 2 * d, 4 * d, c.P(D->w_c2), c.P(D->b_c2), D->values, D->B, T, D->B, 2 * d,
+                       EPI_NONE)))
+    return rc;
+  XTRL_LAUNCHED("train forward");
+  return XTRL_OK;
+}
+
+// ============================================================================================
+int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
+  if (int rc = validate(D)) return rc;
+  XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "train: missing loss gradients");
+  const Ctx c{D, s, D->b * D->n};
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4, S1x2 = 2 * (D->S + 1);
+  int rc;
+  // ---- actor / critic heads
+  if ((rc = wgrad(c, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d))) return rc;
+  if ((rc = colsum(c, D->d_raw, D->n_out, T, D->n_out, c.G(D->b_a2)))) return rc;
+  if ((rc = wgrad(c, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d))) return rc;
+  if ((rc = colsum(c, D->d_values, D->B, T, D->B, c.G(D->b_c2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_DSILU, D->z1,
+                         4 * d)))
+    return rc;
+  if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_DSILU,
+                         D->z1 + 2 * d, 4 * d)))
+    return rc;
+  if ((rc = wgrad(c, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim))) return rc;
+  if ((rc = colsum(c, D->dz1, 4 * d, T, 4 * d, c.G(D->b_h1)))) return rc;
+  if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
+  // state embedding and gene conditioning
+  if ((rc = wgrad(c, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S))) return rc;
+  if ((rc = colsum(c, D->dac + d, D->in_dim, T, d, c.G(D->b_se)))) return rc;
+  if (D->evolutionary) {
+    XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
+    hipLaunchKernelGGL(k_latent_grad, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->dac, D->in_dim, 2 * d, D->b,
+                       D->n, d, D->part);
+    hipLaunchKernelGGL(k_latent_wgrad, dim3(blocks(d * (D->G + 1), 256)), dim3(256), 0, s, D->part, D->latent, D->b,
+                       d, D->G, c.G(D->w_lat), c.G(D->b_lat));
+    XTRL_LAUNCHED("train latent grad");
+  }
+  // ---- world-model heads
+  if ((rc = wgrad(c, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d))) return rc;
+  if ((rc = colsum(c, D->d_pred, S1x2, T, S1x2, c.G(D->b_pred2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_DSILU, D->zp, ldp))) return rc;
+  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);
+  if ((rc = wgrad(c, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d))) return rc;
+  if ((rc = colsum(c, D->dzp, ldp, T, d + 1, c.G(D->b_pd)))) return rc;
+  if ((rc = linear_dgrad(c, D->dzp, ldp, c.P(D->w_pd), D->dewa, 2 * d, T, d + 1, 2 * d, EPI_NONE))) return rc;
+  // action-embedding gradient of the next-action input (and, below, of the previous action)
+  // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
+  if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
+                   c.P(D->ln_final), nullptr, D->dx, c.G(D->ln_final))))
+    return rc;
+  // ---- decoder blocks, last to first
+  for (int li = D->L - 1; li >= 0; --li) {
+    const XtrlTrainLayer& Ly = D->layers[li];
+    // FF2 (+ residual): dx is the gradient w.r.t. the block output
+    if ((rc = wgrad(c, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff))) return rc;
+    if ((rc = colsum(c, D->dx, d, T, d, c.G(Ly.b_ff2)))) return rc;
+    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, ff, T, d, ff, EPI_DGELU_DROP, Ly.u, ff, 1 << 30,
+                           D->ff_offset + (uint32_t)li)))
+      return rc;
+    if ((rc = wgrad(c, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d))) return rc;
+    if ((rc = colsum(c, D->dff, ff, T, ff, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+    if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
+      return rc;
+    // attention out-projection (+ residual) and the value gate
+    if ((rc = wgrad(c, D->dx, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
+    if (D->gate_values) {
+      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30, 0,
+                             Ly.proj + 3 * I, Ly.n_qkv, D->dproj + 3 * I, Ly.n_qkv)))
+        return rc;
+    } else {
+      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_NONE))) return rc;
+    }
+    const AttnProblem ap = attn_problem(c, Ly, li);
+    if ((rc = attn_bwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse, D->dog, D->dproj, D->dproj + I,
+                          D->dproj + 2 * I, D->delta, s)))
+      return rc;
+    const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
+    const bool any_mix = [&] {
+      for (int j = 1; j < D->L; ++j)
+        if (D->layers[j].mix) return true;
+      return false;
+    }();
+    // dvfirst: the first mixing layer processed (the deepest) writes, the others accumulate
+    bool deeper_mix = false;
+    for (int j = li + 1; j < D->L; ++j) deeper_mix = deeper_mix || D->layers[j].mix;
+    PrepBwdArgs pb{D->dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
+                   Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
+                   (li == 0 ? any_mix : deeper_mix) ? 1 : 0};
+    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * D->H, 256)), dim3(256), 0, s, pb);
+    XTRL_LAUNCHED("train qkv_prep_bwd");
+    // q | k | v | gate | mix projection
+    if ((rc = wgrad(c, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d))) return rc;
+    if (Ly.b_proj >= 0 && (rc = colsum(c, D->dproj + 3 * I, Ly.n_qkv, T, Ly.n_qkv - 3 * I, c.G(Ly.b_proj)))) return rc;
+    if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
+    if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
+                     c.G(Ly.ln_attn))))
+      return rc;
+  }
+  // ---- embeddings: dx is d x0
+  if ((rc = wgrad(c, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
+  if ((rc = colsum(c, D->dx, d, T, d, c.G(D->reward_embed), D->swr + D->S, D->S + 1, D->reward_keep))) return rc;
+  if (D->continuous) {
+    if ((rc = wgrad(c, D->dx, d, D->prev_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
+    if ((rc = wgrad(c, D->dewa + d, 2 * d, D->next_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
+    if ((rc = colsum(c, D->dx, d, T, d, c.G(D->act_emb_b)))) return rc;
+    if ((rc = colsum(c, D->dewa + d, 2 * d, T, d, c.G(D->act_emb_b)))) return rc;
+  } else {
+    int chunks = std::min(128, std::max(1, T / 64));
+    const int chunk_rows = (T + chunks - 1) / chunks;
+    chunks = (T + chunk_rows - 1) / chunk_rows;
+    XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");
+    hipLaunchKernelGGL(k_embed_grad_part, dim3(blocks(d, 256), chunks), dim3(256), 0, s, D->dx, d, D->prev_action,
+                       D->dewa + d, 2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 256)), dim3(256), 0, s, D->part, chunks, D->A * d,
+                       c.G(D->act_emb));
+    XTRL_LAUNCHED("train embed grad");
+  }
+  return XTRL_OK;
+}
+
+}  // namespace xtrl
+
+extern "C" int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream) {
+  return xtrl::train_forward(desc, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream) {
+  return xtrl::train_backward(desc, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset,
+                                    void* stream) {
+  XTRL_REQUIRE(mask && M >= 0 && N >= 0 && p >= 0.f && p < 1.f, "ff_dropout_mask: bad arguments");
+  if ((int64_t)M * N == 0) return XTRL_OK;
+  hipLaunchKernelGGL(xtrl::k_ff_mask, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0,
+                     xtrl::as_stream(stream), mask, M, N, xtrl::dropout_thresh(p), seed, offset);
+  XTRL_LAUNCHED("ff_dropout_mask");
+  return XTRL_OK;
+}

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(__file__).resolve().parent / 'libxtrl_hip.so'
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -59,6 +59,30 @@ class LossDesc(C.Structure):
                                     'tok', 'stats', 'd_raw_actions', 'd_values', 'd_pred_raw', 'd_done_logit')])
 
 
+class TrainLayer(C.Structure):
+    _fields_ = ([(n, I64) for n in ('ln_attn', 'w_proj', 'b_proj', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2',
+                                    'b_ff2')]
+                + [('n_qkv', I32), ('mix', I32)]
+                + [(n, P) for n in ('x_attn', 'x_ff', 'xn_attn', 'xn_ff', 'st_attn', 'st_ff', 'proj', 'qkv', 'o', 'og',
+                                    'lse', 'u', 'hd')])
+
+
+class TrainDesc(C.Structure):
+    _fields_ = ([(n, I32) for n in ('b', 'n', 'S', 'A', 'd', 'L', 'H', 'dh', 'ff', 'B', 'in_dim', 'n_out', 'G',
+                                    'continuous', 'evolutionary', 'gate_values', 'rot_dim')]
+                + [(n, F32) for n in ('dropout', 'frac_head_grad', 'reward_keep', 'attn_scale')]
+                + [('seed', U64), ('attn_offset', U32), ('ff_offset', U32), ('flat', P), ('grad', P)]
+                + [(n, I64) for n in ('w_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final',
+                                      'w_pd', 'b_pd', 'w_pred2', 'b_pred2', 'w_lat', 'b_lat', 'w_h1', 'b_h1', 'w_a2',
+                                      'b_a2', 'w_c2', 'b_c2')]
+                + [(n, P) for n in ('inv_freq', 'swr', 'prev_action', 'next_action', 'prev_action_f',
+                                    'next_action_f', 'latent', 'lens', 'raw', 'values', 'pred', 'done', 'x_final',
+                                    'st_final', 'ac_in', 'ewa', 'zp', 'hp', 'z1', 'h1', 'lat_e', 'd_raw', 'd_values',
+                                    'd_pred', 'd_done', 'dx', 'dxn', 'dff', 'dproj', 'dog', 'dvfirst', 'dz1', 'dac',
+                                    'dzp', 'dewa', 'delta', 'part')]
+                + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer))])
+
+
 SIGNATURES = {
     'xtrl_abi_version': (I32, []),
     'xtrl_last_error': (C.c_char_p, []),
@@ -80,6 +104,9 @@ SIGNATURES = {
                                I32, P]),
     'xtrl_ema_lerp': (I32, [P, P, I64, F32, P]),
     'xtrl_sim_reset': (I32, [P, I32, I32, U64, U32, P, P]),
+    'xtrl_train_forward': (I32, [C.POINTER(TrainDesc), P]),
+    'xtrl_train_backward': (I32, [C.POINTER(TrainDesc), P]),
+    'xtrl_ff_dropout_mask': (I32, [P, I32, I32, F32, U64, U32, P]),
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
 }
@@ -129,4 +156,4 @@ def rng_uniform(seed, update, slot, t, field, sub=0):
     return load().xtrl_rng_uniform(seed & 0xFFFFFFFFFFFFFFFF, update, slot, t, field, sub)
 
 
-FIELD_STATE, FIELD_REWARD, FIELD_TERM, FIELD_SAMPLE, FIELD_COIN, FIELD_DROPOUT = 1, 2, 3, 4, 5, 6
+FIELD_STATE, FIELD_REWARD, FIELD_TERM, FIELD_SAMPLE, FIELD_COIN, FIELD_DROPOUT, FIELD_FF_DROPOUT = 1, 2, 3, 4, 5, 6, 7

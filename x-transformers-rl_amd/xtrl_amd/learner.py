@@ -81,7 +81,7 @@ class Agent(nn.Module):
                  actor_loss_weight=1., critic_loss_weight=1., autoregressive_loss_weight=1.,
                  # extensions (decision log in DESIGN.md)
                  reward_dropout=0.5, seed=0, rotary_abs_rollout=False, hl_reduction_mean=True, hl_sigma_ratio=2.0,
-                 device=None):
+                 fused_learn=True, device=None):
         super().__init__()
         self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
         dev = self.accelerator.device
@@ -147,6 +147,8 @@ class Agent(nn.Module):
         self.logs = []
         self._deploy = None
         self._genes_dev = None
+        self.fused_learn = fused_learn   # False: reference-mode autograd learn step (tests)
+        self._train_step = None
 
     @property
     def device(self):
@@ -244,11 +246,18 @@ class Agent(nn.Module):
                 swr = swr.contiguous()
                 keep = reward_coin(self.seed, update, epoch, mbi, c.reward_dropout)
                 latent = self.latent(gene_ids[idx]) if c.evolutionary else None
-                act_in = prev_act if c.continuous else prev_act.long()
-                nxt = mb_act if c.continuous else mb_act.long()
-                raw, values, pred_raw, done_logit = model.forward_train(
-                    swr[..., :-1], act_in, swr[..., -1], nxt, latent, mb_lens, keep,
-                    attn_seed=self.seed * 1000003 + update, attn_offset=(epoch * 4096 + mbi) * 1024)
+                attn_seed, attn_off, ff_off = self.seed * 1000003 + update, (epoch * 4096 + mbi) * 1024, \
+                    (epoch * 4096 + mbi) * 64
+                if self.fused_learn:
+                    step = self.train_step(b, n)
+                    step.forward(swr, prev_act.contiguous(), mb_act, latent, mb_lens, keep, attn_seed, attn_off,
+                                 ff_off, c.dropout)
+                else:
+                    act_in = prev_act if c.continuous else prev_act.long()
+                    nxt = mb_act if c.continuous else mb_act.long()
+                    raw, values, pred_raw, done_logit = model.forward_train(
+                        swr[..., :-1], act_in, swr[..., -1], nxt, latent, mb_lens, keep,
+                        attn_seed=attn_seed, attn_offset=attn_off, ff_offset=ff_off)
                 K = ops.LossConsts(actions=mb_act, old_logp=old_lp[idx].contiguous(), returns=returns[idx].contiguous(),
                                    old_values=old_values[idx].contiguous(), dones=bounds[idx].contiguous(),
                                    lens=mb_lens, real=swr, support=model.hl_support, centers=model.hl_centers,
@@ -257,9 +266,14 @@ class Agent(nn.Module):
                                    w_actor=self.actor_loss_weight, w_critic=self.critic_loss_weight,
                                    w_autoreg=self.autoregressive_loss_weight, lo=float(lo), hi=float(hi),
                                    sigma=float(model.hl_sigma))
-                loss, stats = ops.fused_loss(raw, values, pred_raw, done_logit, K)
                 self.flat.zero_grad()
-                loss.backward()
+                if self.fused_learn:
+                    stats = step.loss(K)
+                    step.backward()
+                    loss = stats[L.LS['loss']]
+                else:
+                    loss, stats = ops.fused_loss(raw, values, pred_raw, done_logit, K)
+                    loss.backward()
                 dist_.mean_(self.flat.grad)
                 if probe is not None:
                     probe(epoch, mbi, idx, loss, stats)
@@ -282,6 +296,15 @@ class Agent(nn.Module):
                 self.logs.append(stats)
         self.rs_mean, self.rs_var, self.rs_step = rs_mean, rs_var, rs_step
         self.step += 1
+
+    def train_step(self, b, n):
+        """The fused learn step, with activation buffers for up to (batch_size, n) minibatches."""
+        ts = self._train_step
+        if ts is None or b > ts.b_max or n > ts.n_max:
+            from .train import FusedTrainStep
+            self._train_step = ts = FusedTrainStep(self.model, self.flat, self.gemm_ws, max(b, self.batch_size),
+                                                   max(n, ts.n_max if ts is not None else 0))
+        return ts
 
     def pop_logs(self):
         """Per-minibatch dict(loss, actor_loss, critic_loss, autoreg_loss, pred_done_loss)."""

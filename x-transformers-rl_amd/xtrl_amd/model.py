@@ -182,8 +182,9 @@ class WorldModelActorCritic(nn.Module):
 
     # ---- flat-buffer layout / binding ---------------------------------------------------------------
     def flat_order(self):
-        """Parameter order of the flat buffer: the q|k|v|gate|mix weights of each attention block and
-        the first actor / critic head layers are adjacent so their concatenations are views."""
+        """Parameter order of the flat buffer: the q|k|v|gate|mix weights of each attention block, the
+        first actor / critic head layers and to_pred.0 | to_pred_done are adjacent so their
+        concatenations are views (one GEMM operand each)."""
         c = self.cfg
         names = [n for n, _ in self.named_parameters()]
         pri = []
@@ -196,6 +197,7 @@ class WorldModelActorCritic(nn.Module):
             pri += [pre + 'to_v_gate.bias'] if c.gate_values else []
             pri += [pre + 'to_value_residual_mix.0.bias'] if mix else []
         pri += ['action_head.0.weight', 'critic_head.0.weight', 'action_head.0.bias', 'critic_head.0.bias']
+        pri += ['to_pred.0.weight', 'to_pred_done.0.weight', 'to_pred.0.bias', 'to_pred_done.0.bias']
         taken = set(pri)
         return pri + [n for n in names if n not in taken]
 
@@ -227,7 +229,9 @@ class WorldModelActorCritic(nn.Module):
 
     # ---- learn-step forward (xtrl.py:479-559 with the mask path of x-transformers) --------------
     def forward_train(self, state, actions, rewards, next_actions, latent_gene, lens, reward_keep=True,
-                      attn_seed=0, attn_offset=0):
+                      attn_seed=0, attn_offset=0, ff_offset=0):
+        """Reference-mode (autograd) learn forward; the product learn step is train.FusedTrainStep.
+        Dropout masks are the same counter-based streams as the fused step's."""
         c = self.cfg
         b, n, _ = state.shape
         tr = self.transformer
@@ -269,7 +273,10 @@ class WorldModelActorCritic(nn.Module):
             x = self._lin(o, blk.to_out) + x
             (ln_f, _, _), ffb, _ = ff_l
             h = F.gelu(self._lin(ln_f(x), ffb.ff[0][0]))
-            h = F.dropout(h, p_drop, self.training) if p_drop > 0 else h
+            if p_drop > 0:
+                from .train import ff_dropout_mask
+                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset + li, h.device)
+                h = h * keep.view(b, n, -1).to(h.dtype) * (1.0 / (1.0 - p_drop))
             x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)
         ewa = torch.cat((embed, self.embed_actions(next_actions)), dim=-1)

@@ -1,0 +1,189 @@
+"""Hand-scheduled learn step: one minibatch forward + loss + backward through libxtrl_hip without
+autograd (xtrl_train_forward / xtrl_loss_fwd / xtrl_loss_bwd / xtrl_train_backward).
+
+Replaces, for Agent.learn (x_transformers_rl.py:880-1023), the per-minibatch
+``model(...)`` -> losses -> ``loss.backward()`` sequence.  Activations live in buffers allocated
+once for the largest minibatch (``b_max`` episodes x ``n_max`` steps, token-major) and reused by
+every minibatch; gradients are accumulated into the flat gradient buffer of ``FlatParams``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from .params import FlatParams
+
+
+class FusedTrainStep:
+    def __init__(self, model, flat: FlatParams, ws: torch.Tensor, b_max: int, n_max: int):
+        c = model.cfg
+        self.model, self.flat, self.cfg, self.ws = model, flat, c, ws
+        dev = flat.flat.device
+        self.dev = dev
+        d, H, dh, L_ = c.dim, c.heads, c.dim_head, c.depth
+        I, ff, B = H * dh, c.dim * c.ff_mult, c.num_bins
+        S, A = c.state_dim, c.num_actions
+        n_out = A * (2 if c.continuous else 1)
+        T = b_max * n_max
+        self.b_max, self.n_max, self.T_max = b_max, n_max, T
+        self.inv_freq = model.transformer.attn_layers.rotary_pos_emb.inv_freq.to(dev).contiguous()
+        rot = 2 * self.inv_freq.numel()
+        f32 = dict(device=dev, dtype=torch.float32)
+        E = lambda *shape: torch.empty(*shape, **f32)
+        off = lambda name: flat.index[name][0] if name in flat.index else -1
+        pre = 'transformer.attn_layers.layers.'
+
+        def span_off(names):
+            a0 = flat.index[names[0]][0]
+            flat.span(names)   # asserts adjacency
+            return a0
+
+        self.layers_py = []
+        layers = (L.TrainLayer * L_)()
+        X = [E(T, d) for _ in range(L_ + 1)]
+        max_qkv = 0
+        for li in range(L_):
+            mix = bool(c.value_residual and c.learned_mix and li > 0)
+            pa, pf = f'{pre}{2 * li}.', f'{pre}{2 * li + 1}.'
+            wn = [pa + '1.to_q.weight', pa + '1.to_k.weight', pa + '1.to_v.weight']
+            wn += [pa + '1.to_v_gate.weight'] if c.gate_values else []
+            wn += [pa + '1.to_value_residual_mix.0.weight'] if mix else []
+            bn = ([pa + '1.to_v_gate.bias'] if c.gate_values else []) + \
+                 ([pa + '1.to_value_residual_mix.0.bias'] if mix else [])
+            n_qkv = 3 * I + (I if c.gate_values else 0) + (H if mix else 0)
+            max_qkv = max(max_qkv, n_qkv)
+            bufs = dict(x_attn=X[li], x_ff=E(T, d), xn_attn=E(T, d), xn_ff=E(T, d), st_attn=E(T, 2), st_ff=E(T, 2),
+                        proj=E(T, n_qkv), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), u=E(T, ff),
+                        hd=E(T, ff))
+            bufs['og'] = E(T, I) if c.gate_values else bufs['o']
+            self.layers_py.append(bufs)
+            Ly = layers[li]
+            Ly.ln_attn, Ly.w_proj = off(pa + '0.0.gamma'), span_off(wn)
+            Ly.b_proj = span_off(bn) if bn else -1
+            Ly.w_out, Ly.ln_ff = off(pa + '1.to_out.weight'), off(pf + '0.0.gamma')
+            Ly.w_ff1, Ly.b_ff1 = off(pf + '1.ff.0.0.weight'), off(pf + '1.ff.0.0.bias')
+            Ly.w_ff2, Ly.b_ff2 = off(pf + '1.ff.2.weight'), off(pf + '1.ff.2.bias')
+            Ly.n_qkv, Ly.mix = n_qkv, int(mix)
+            for k, t in bufs.items():
+                setattr(Ly, k, t.data_ptr())
+        self.layers = layers
+        self.X = X
+        ldp = d + 4
+        self.buf = dict(x_final=X[L_], st_final=E(T, 2), ac_in=E(T, c.in_dim), ewa=E(T, 2 * d), zp=E(T, ldp),
+                        hp=E(T, ldp), z1=E(T, 4 * d), h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d),
+                        raw=E(T, n_out), values=E(T, B), pred=E(T, 2 * (S + 1)), done=E(T),
+                        d_raw=E(T, n_out), d_values=E(T, B), d_pred=E(T, 2 * (S + 1)), d_done=E(T),
+                        dx=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
+                        dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
+                        delta=E(b_max * H * n_max))
+        part = max(256 * max(ff, 4 * d, B, max_qkv), (T // 64 + 1) * d, 128 * max(A, 1) * d, b_max * d)
+        self.buf['part'] = E(part)
+        self.tok = torch.empty(b_max, n_max, L.LOSS_TOK, **f32)
+        self.stats = torch.zeros(L.LOSS_STATS, **f32)
+
+        D = L.TrainDesc()
+        D.S, D.A, D.d, D.L, D.H, D.dh, D.ff, D.B = S, A, d, L_, H, dh, ff, B
+        D.in_dim, D.n_out, D.G = c.in_dim, n_out, c.dim_gene if c.evolutionary else 0
+        D.continuous, D.evolutionary, D.gate_values, D.rot_dim = int(c.continuous), int(c.evolutionary), \
+            int(c.gate_values), rot
+        D.frac_head_grad, D.attn_scale = float(c.frac_head_grad), float(dh ** -0.5)
+        D.flat, D.grad = flat.flat.data_ptr(), flat.grad.data_ptr()
+        D.w_pin = off('transformer.project_in.weight')
+        if c.continuous:
+            D.act_emb, D.act_emb_b = off('action_embeds.weight'), off('action_embeds.bias')
+        else:
+            D.act_emb, D.act_emb_b = off('action_embeds.embed.weight'), -1
+        D.reward_embed, D.w_se, D.b_se = off('reward_embed'), off('to_state_embed.weight'), off('to_state_embed.bias')
+        D.ln_final = off('transformer.attn_layers.final_norm.gamma')
+        D.w_pd = span_off(['to_pred.0.weight', 'to_pred_done.0.weight'])
+        D.b_pd = span_off(['to_pred.0.bias', 'to_pred_done.0.bias'])
+        D.w_pred2, D.b_pred2 = off('to_pred.2.weight'), off('to_pred.2.bias')
+        D.w_lat, D.b_lat = off('latent_to_embed.weight'), off('latent_to_embed.bias')
+        D.w_h1 = span_off(['action_head.0.weight', 'critic_head.0.weight'])
+        D.b_h1 = span_off(['action_head.0.bias', 'critic_head.0.bias'])
+        D.w_a2, D.b_a2 = off('action_head.2.weight'), off('action_head.2.bias')
+        D.w_c2, D.b_c2 = off('critic_head.2.weight'), off('critic_head.2.bias')
+        D.inv_freq = self.inv_freq.data_ptr()
+        for k, t in self.buf.items():
+            setattr(D, k, t.data_ptr())
+        D.part_floats = self.buf['part'].numel()
+        D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
+        D.layers = C.cast(layers, C.POINTER(L.TrainLayer))
+        self.D = D
+
+    # ------------------------------------------------------------------------------------------
+    def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
+                dropout):
+        """swr [b][n][S+1] normalised states | previous reward; actions [b][n] int32 (discrete) or
+        [b][n][A] float (continuous); latent [b][G] or None; lens [b] int32.
+        Returns views raw [b][n][n_out], values [b][n][B], pred [b][n][2(S+1)], done [b][n]."""
+        c, D = self.cfg, self.D
+        b, n = swr.shape[0], swr.shape[1]
+        assert b <= self.b_max and n <= self.n_max, (b, n, self.b_max, self.n_max)
+        for t in (swr, prev_action, next_action, lens):
+            assert t.is_cuda and t.is_contiguous()
+        self._keep = [swr, prev_action, next_action, latent, lens]
+        D.b, D.n = b, n
+        D.dropout, D.reward_keep = float(dropout), float(reward_keep)
+        D.seed, D.attn_offset, D.ff_offset = int(seed) & (2 ** 64 - 1), int(attn_offset) & 0xFFFFFFFF, \
+            int(ff_offset) & 0xFFFFFFFF
+        D.swr, D.lens = swr.data_ptr(), lens.data_ptr()
+        if c.continuous:
+            D.prev_action_f, D.next_action_f, D.prev_action, D.next_action = prev_action.data_ptr(), \
+                next_action.data_ptr(), None, None
+        else:
+            assert prev_action.dtype == torch.int32 and next_action.dtype == torch.int32
+            D.prev_action, D.next_action, D.prev_action_f, D.next_action_f = prev_action.data_ptr(), \
+                next_action.data_ptr(), None, None
+        D.latent = latent.contiguous().data_ptr() if latent is not None else None
+        if latent is not None:
+            self._keep.append(latent.contiguous())
+            D.latent = self._keep[-1].data_ptr()
+        L.check(L.lib().xtrl_train_forward(C.byref(D), L.stream()), 'train_forward')
+        T = b * n
+        bf = self.buf
+        return (bf['raw'][:T].view(b, n, -1), bf['values'][:T].view(b, n, -1), bf['pred'][:T].view(b, n, -1),
+                bf['done'][:T].view(b, n))
+
+    def loss(self, K):
+        """Fused loss forward + backward (upstream gradient 1) into the d_* buffers.
+        Returns the stats tensor (XTRL_LS_* slots)."""
+        c, D = self.cfg, self.D
+        b, n = D.b, D.n
+        T = b * n
+        bf = self.buf
+        S1 = c.state_dim + 1
+        A = c.num_actions
+        self.stats.zero_()
+        d = L.LossDesc(b=b, n=n, A=A, B=c.num_bins, S1=S1, continuous=int(K.continuous), squash=int(K.squash),
+                       hl_reduction_mean=int(K.hl_mean), eps_clip=K.eps_clip, value_clip=K.value_clip,
+                       entropy_weight=K.entropy_weight, w_actor=K.w_actor, w_critic=K.w_critic,
+                       w_autoreg=K.w_autoreg, lo=K.lo, hi=K.hi, sigma=K.sigma)
+        fields = dict(raw_actions=bf['raw'], values=bf['values'], pred_raw=bf['pred'], done_logit=bf['done'],
+                      actions=None if K.continuous else K.actions, actions_f=K.actions if K.continuous else None,
+                      old_logp=K.old_logp, returns=K.returns, old_values=K.old_values, dones=K.dones, lens=K.lens,
+                      real=K.real, support=K.support, centers=K.centers, tok=self.tok, stats=self.stats,
+                      d_raw_actions=bf['d_raw'], d_values=bf['d_values'], d_pred_raw=bf['d_pred'],
+                      d_done_logit=bf['d_done'])
+        for name, t in fields.items():
+            if t is not None:
+                assert t.is_cuda and t.is_contiguous(), name
+                setattr(d, name, t.data_ptr())
+        lib = L.lib()
+        L.check(lib.xtrl_loss_fwd(C.byref(d), L.stream()), 'loss_fwd')
+        L.check(lib.xtrl_loss_bwd(C.byref(d), 1.0, L.stream()), 'loss_bwd')
+        del T
+        return self.stats.clone()   # the stats buffer is reused by the next minibatch
+
+    def backward(self):
+        L.check(L.lib().xtrl_train_backward(C.byref(self.D), L.stream()), 'train_backward')
+
+
+def ff_dropout_mask(M, N, p, seed, offset, device):
+    """The feed-forward dropout keep mask the fused step uses (uint8 [M][N]) — reference mode."""
+    m = torch.empty(M, N, device=device, dtype=torch.uint8)
+    L.check(L.lib().xtrl_ff_dropout_mask(L.ptr(m), M, N, float(p), int(seed) & (2 ** 64 - 1),
+                                         int(offset) & 0xFFFFFFFF, L.stream()), 'ff_dropout_mask')
+    return m
