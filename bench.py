@@ -68,13 +68,24 @@ def build_learner(cfg, seed, use_graph=True):
     return learner, env
 
 
-def one_update(learner, env, T, probe=None):
+PHASES = []   # (start, after rollout, after learn) events of the timed updates
+
+
+def one_update(learner, env, T, probe=None, phases=False):
     agent = learner.agent
     u = agent.step
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if phases else None
+    if ev:
+        ev[0].record()
     traj, lens, genes, cum = learner.rollout_device(env, u, T)
+    if ev:
+        ev[1].record()
     fit = learner.fitness(cum, genes)
     steps = lens.sum()
     agent.learn(traj, lens, genes, fit, update=u, probe=probe)
+    if ev:
+        ev[2].record()
+        PHASES.append(ev)
     agent.logs = []
     return steps, lens
 
@@ -243,7 +254,7 @@ def main():
     total = torch.zeros((), device='cuda', dtype=torch.int64)
     lens_log = []
     for _ in range(args.steps):
-        steps, lens = one_update(learner, env, T)
+        steps, lens = one_update(learner, env, T, phases=True)
         total += steps
         if timer is not None:
             lens_log.append(lens.clone())
@@ -261,6 +272,8 @@ def main():
     env_steps = int(total)
     value = env_steps / elapsed
 
+    phase_ms = dict(rollout=round(sum(e[0].elapsed_time(e[1]) for e in PHASES) / len(PHASES), 2),
+                    learn=round(sum(e[1].elapsed_time(e[2]) for e in PHASES) / len(PHASES), 2))
     roofline = None
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
@@ -287,7 +300,7 @@ def main():
                     data='synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)',
                     config=dict(workload=cfg['workload'], global_batch=cfg['episodes'] * (3 if cfg['evo'] else 1) * world,
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
-                    roofline=roofline, cpu_baseline=cpu, ppo_loss=loss_delta)
+                    roofline=roofline, cpu_baseline=cpu, ppo_loss=loss_delta, phase_ms=phase_ms)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

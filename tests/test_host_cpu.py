@@ -135,3 +135,20 @@ def test_flat_params_views():
     assert torch.equal(m.reward_embed, before['reward_embed'] + 1)
     (m.reward_embed.sum() * 2).backward()
     assert torch.equal(fp.grad[:m.reward_embed.numel()], torch.full_like(m.reward_embed, 2.))
+
+
+def test_flat_layout_aligns_gemm_weights():
+    """Every GEMM weight of the C3 model starts 16-byte aligned in the flat buffer (float4 operand
+    loads in the HIP GEMM), and the concatenated operands stay adjacent."""
+    from xtrl_amd.model import ModelConfig, WorldModelActorCritic
+    from xtrl_amd.params import FlatParams
+    c = ModelConfig(8, 4, dim=256, depth=4, heads=4, dim_head=16, gate_values=True, value_residual=True,
+                    learned_mix=True, evolutionary=True, dim_gene=32)
+    m = WorldModelActorCritic(c)
+    flat = FlatParams(m, 'cpu', order=m.flat_order())
+    for name, (a, b) in flat.index.items():
+        p = dict(m.named_parameters())[name]
+        if p.dim() == 2 and p.shape[1] % 4 == 0:
+            assert a % 4 == 0, (name, a)
+    flat.span(['to_pred.0.weight', 'to_pred_done.0.weight'])
+    flat.span(['action_head.0.weight', 'critic_head.0.weight'])

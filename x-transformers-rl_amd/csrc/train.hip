@@ -27,39 +27,55 @@ struct EmbedArgs {
   float keep;
 };
 
+constexpr int EMB_TOK = 32, EMB_MAXS = 32;
+// block: EMB_TOK tokens x all d columns; thread c keeps its project_in / to_state_embed rows in
+// registers (S <= EMB_MAXS) and walks the block's tokens
 __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)a.T * a.d) return;
-  const int t = (int)(i / a.d), c = (int)(i - (int64_t)t * a.d);
-  const float* st = a.swr + (int64_t)t * (a.S + 1);
-  float pin = 0.f, se = 0.f;
-  for (int s = 0; s < a.S; ++s) {
-    const float x = st[s];
-    pin += x * a.w_pin[(int64_t)c * a.S + s];
-    se += x * a.w_se[(int64_t)c * a.S + s];
-  }
-  se += a.b_se[c];
-  float ap, an;
-  if (a.continuous) {
-    const float* w = a.act_emb + (int64_t)c * a.A;
-    ap = 0.f;
-    an = 0.f;
-    for (int k = 0; k < a.A; ++k) {
-      ap += a.prev_af[(int64_t)t * a.A + k] * w[k];
-      an += a.next_af[(int64_t)t * a.A + k] * w[k];
+  const int t0 = blockIdx.x * EMB_TOK, t1 = min(a.T, t0 + EMB_TOK);
+  for (int c = threadIdx.x; c < a.d; c += 256) {
+    float wp[EMB_MAXS], ws[EMB_MAXS];
+#pragma unroll
+    for (int s = 0; s < EMB_MAXS; ++s) {
+      wp[s] = s < a.S ? a.w_pin[(int64_t)c * a.S + s] : 0.f;
+      ws[s] = s < a.S ? a.w_se[(int64_t)c * a.S + s] : 0.f;
     }
-    ap += a.act_emb_b[c];
-    an += a.act_emb_b[c];
-  } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
-    const int p = a.prev_a[t], q = a.next_a[t];
-    ap = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
-    an = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
+    const float bse = a.b_se[c], re = a.reward_embed[c];
+    const float bemb = a.continuous ? a.act_emb_b[c] : 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const float* st = a.swr + (int64_t)t * (a.S + 1);
+      float pin = 0.f, se = 0.f;
+#pragma unroll
+      for (int s = 0; s < EMB_MAXS; ++s) {
+        if (s < a.S) {
+          const float x = st[s];
+          pin += x * wp[s];
+          se += x * ws[s];
+        }
+      }
+      se += bse;
+      float ap, an;
+      if (a.continuous) {
+        const float* w = a.act_emb + (int64_t)c * a.A;
+        ap = 0.f;
+        an = 0.f;
+        for (int k = 0; k < a.A; ++k) {
+          ap += a.prev_af[(int64_t)t * a.A + k] * w[k];
+          an += a.next_af[(int64_t)t * a.A + k] * w[k];
+        }
+        ap += bemb;
+        an += bemb;
+      } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
+        const int p = a.prev_a[t], q = a.next_a[t];
+        ap = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
+        an = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
+      }
+      const float r = st[a.S];
+      a.x0[(int64_t)t * a.d + c] = pin + (ap + (r * re) * a.keep);
+      a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se;
+      a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an;
+      if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = a.lat_e[(int64_t)(t / a.n) * a.d + c];
+    }
   }
-  const float r = st[a.S];
-  a.x0[i] = pin + (ap + (r * a.reward_embed[c]) * a.keep);
-  a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se;
-  a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an;
-  if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = a.lat_e[(int64_t)(t / a.n) * a.d + c];
 }
 
 // lat_e[b][c] = latent[b] . w[c] + bias[c]
@@ -113,60 +129,81 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
   }
 }
 
-// LayerNorm backward for ROWS rows per block (4 waves): upstream gradient g = s1 * g1 + g2 (g2
-// optional), dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)) (+ dres, in place
-// allowed: dx may alias dres); per-block partial d gamma = sum_rows g * xhat -> part[block][d]
-constexpr int LN_ROWS = 64;
-__global__ __launch_bounds__(256) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2, int ldg2,
-                                                const float* x, const float* stats, const float* gamma,
-                                                const float* dres, float* dx, float* part, int T, int d) {
-  __shared__ float red[4][512];
+// LayerNorm backward, LN_ROWS rows per block of 8 waves (each wave 4 rows at a time, loads of all
+// four issued together): upstream gradient g = s1 * g1 + g2 (g2 optional),
+// dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)) (+ dres; dx may alias dres);
+// per-block partial d gamma = sum_rows g * xhat -> part[block][d]
+constexpr int LN_ROWS = 64, LN_WAVES = 8, LN_R = 4;
+template <int DPL>
+__global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2,
+                                                          int ldg2, const float* x, const float* stats,
+                                                          const float* gamma, const float* dres, float* dx,
+                                                          float* part, int T, int d) {
+  __shared__ float red[LN_WAVES][64 * DPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float dg[kMaxDPerLane];
+  float gam[DPL], dg[DPL];
 #pragma unroll
-  for (int k = 0; k < kMaxDPerLane; ++k) dg[k] = 0.f;
-  const int r0 = blockIdx.x * LN_ROWS;
-  for (int r = w; r < LN_ROWS; r += 4) {
-    const int t = r0 + r;
-    if (t >= T) break;
-    const float mean = stats[2 * t], rstd = stats[2 * t + 1];
-    float gg[kMaxDPerLane], xh[kMaxDPerLane];
-    float sa = 0.f, sb = 0.f;
-#pragma unroll
-    for (int k = 0; k < kMaxDPerLane; ++k) {
-      const int c = lane + 64 * k;
-      float g = 0.f, xhat = 0.f, gm = 0.f;
-      if (c < d) {
-        g = s1 * g1[(int64_t)t * ldg1 + c];
-        if (g2) g += g2[(int64_t)t * ldg2 + c];
-        xhat = (x[(int64_t)t * d + c] - mean) * rstd;
-        gm = g * gamma[c];
-        dg[k] += g * xhat;
-      }
-      gg[k] = gm;
-      xh[k] = xhat;
-      sa += gm;
-      sb += gm * xhat;
-    }
-    const float ma = wave_sum(sa) / (float)d, mb = wave_sum(sb) / (float)d;
-#pragma unroll
-    for (int k = 0; k < kMaxDPerLane; ++k) {
-      const int c = lane + 64 * k;
-      if (c < d) {
-        float v = rstd * (gg[k] - ma - xh[k] * mb);
-        if (dres) v += dres[(int64_t)t * d + c];
-        dx[(int64_t)t * d + c] = v;
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kMaxDPerLane; ++k) {
+  for (int k = 0; k < DPL; ++k) {
     const int c = lane + 64 * k;
-    if (c < d) red[w][c] = dg[k];
+    gam[k] = c < d ? gamma[c] : 0.f;
+    dg[k] = 0.f;
   }
+  const int r0 = blockIdx.x * LN_ROWS;
+  for (int rb = w * LN_R; rb < LN_ROWS; rb += LN_WAVES * LN_R) {
+    float g[LN_R][DPL], xv[LN_R][DPL], rs[LN_R], mu[LN_R];
+#pragma unroll
+    for (int q = 0; q < LN_R; ++q) {
+      const int t = r0 + rb + q;
+      const bool ok = t < T;
+      mu[q] = ok ? stats[2 * t] : 0.f;
+      rs[q] = ok ? stats[2 * t + 1] : 0.f;
+#pragma unroll
+      for (int k = 0; k < DPL; ++k) {
+        const int c = lane + 64 * k;
+        const bool in = ok && c < d;
+        float gv = in ? s1 * g1[(int64_t)t * ldg1 + c] : 0.f;
+        if (g2 && in) gv += g2[(int64_t)t * ldg2 + c];
+        g[q][k] = gv;
+        xv[q][k] = in ? x[(int64_t)t * d + c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < LN_R; ++q) {
+      const int t = r0 + rb + q;
+      float sa = 0.f, sb = 0.f;
+      float gm[DPL], xh[DPL];
+#pragma unroll
+      for (int k = 0; k < DPL; ++k) {
+        const int c = lane + 64 * k;
+        xh[k] = c < d ? (xv[q][k] - mu[q]) * rs[q] : 0.f;
+        gm[k] = g[q][k] * gam[k];
+        dg[k] += g[q][k] * xh[k];
+        sa += gm[k];
+        sb += gm[k] * xh[k];
+      }
+      const float ma = wave_sum(sa) / (float)d, mb = wave_sum(sb) / (float)d;
+      if (t < T) {
+#pragma unroll
+        for (int k = 0; k < DPL; ++k) {
+          const int c = lane + 64 * k;
+          if (c < d) {
+            float v = rs[q] * (gm[k] - ma - xh[k] * mb);
+            if (dres) v += dres[(int64_t)t * d + c];
+            dx[(int64_t)t * d + c] = v;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < DPL; ++k) red[w][lane + 64 * k] = dg[k];
   __syncthreads();
-  for (int c = threadIdx.x; c < d; c += 256)
-    part[(int64_t)blockIdx.x * d + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+  for (int c = threadIdx.x; c < d; c += 64 * LN_WAVES) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < LN_WAVES; ++j) v += red[j][c];
+    part[(int64_t)blockIdx.x * d + c] = v;
+  }
 }
 
 // ---- rotary + value-residual mix (x-transformers Attention) --------------
@@ -277,30 +314,55 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, i
   part[(int64_t)blockIdx.y * cols + c] = s;
 }
 
-// dst[c] += sum_k part[k][c]   (fixed order)
+// dst[c] += sum_k part[k][c]: 64 columns per block; wave w sums chunks w, w + 4, ... with four
+// interleaved accumulators; fixed combination order (deterministic)
 __global__ __launch_bounds__(256) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[(int64_t)k * cols + c];
-  dst[c] += s;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    int k = w;
+    for (; k + 12 < chunks; k += 16) {
+      s0 += part[(int64_t)k * cols + c];
+      s1 += part[(int64_t)(k + 4) * cols + c];
+      s2 += part[(int64_t)(k + 8) * cols + c];
+      s3 += part[(int64_t)(k + 12) * cols + c];
+    }
+    for (; k < chunks; k += 4) s0 += part[(int64_t)k * cols + c];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && c < cols) dst[c] += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // discrete action-embedding gradient: part[chunk][a][c] = sum over rows of the chunk with
-// prev[r] == a of g1[r][c]  +  rows with next[r] == a of g2[r][c]
+// prev[r] == a of g1[r][c]  +  rows with next[r] == a of g2[r][c]   (A <= EMB_MAXA, registers)
+constexpr int EMB_MAXA = 32;
 __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld1, const int32_t* prev,
                                                          const float* g2, int ld2, const int32_t* next, int rows,
                                                          int d, int A, int chunk_rows, float* part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= d) return;
   const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
-  float* out = part + (int64_t)blockIdx.y * A * d;
-  for (int a = 0; a < A; ++a) out[(int64_t)a * d + c] = 0.f;
+  float acc[EMB_MAXA];
+#pragma unroll
+  for (int a = 0; a < EMB_MAXA; ++a) acc[a] = 0.f;
   for (int r = r0; r < r1; ++r) {
     const int p = prev[r], q = next[r];
-    if (p >= 0) out[(int64_t)p * d + c] += g1[(int64_t)r * ld1 + c];
-    if (q >= 0) out[(int64_t)q * d + c] += g2[(int64_t)r * ld2 + c];
+    const float x = g1[(int64_t)r * ld1 + c], y = g2[(int64_t)r * ld2 + c];
+#pragma unroll
+    for (int a = 0; a < EMB_MAXA; ++a) {
+      if (a < A) {
+        acc[a] += p == a ? x : 0.f;
+        acc[a] += q == a ? y : 0.f;
+      }
+    }
   }
+  float* out = part + (int64_t)blockIdx.y * A * d;
+#pragma unroll
+  for (int a = 0; a < EMB_MAXA; ++a)
+    if (a < A) out[(int64_t)a * d + c] = acc[a];
 }
 
 // latent gradient of the evolutionary conditioning: dlat[e][c] = sum_steps dac[e*n + s][2d + c]
@@ -402,7 +464,7 @@ int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* ds
   XTRL_REQUIRE((int64_t)chunks * cols <= c.D->part_floats, "train: partial-sum workspace too small");
   hipLaunchKernelGGL(k_colsum_part, dim3(blocks(cols, 256), chunks), dim3(256), 0, c.s, src, ld, rows, cols,
                      chunk_rows, rw, ld_rw, rw_scale, c.D->part);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 256)), dim3(256), 0, c.s, c.D->part, chunks, cols, dst);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 64)), dim3(256), 0, c.s, c.D->part, chunks, cols, dst);
   XTRL_LAUNCHED("train colsum");
   return XTRL_OK;
 }
@@ -418,9 +480,12 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
            const float* st, const float* gamma, const float* dres, float* dx, float* dgamma) {
   const int d = c.D->d, nb = (int)blocks(c.T, LN_ROWS);
   XTRL_REQUIRE((int64_t)nb * d <= c.D->part_floats, "train: partial-sum workspace too small");
-  hipLaunchKernelGGL(k_ln_bwd, dim3(nb), dim3(256), 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx,
-                     c.D->part, c.T, d);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 256)), dim3(256), 0, c.s, c.D->part, nb, d, dgamma);
+  const dim3 g(nb), bl(64 * LN_WAVES);
+  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
+  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
+  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
+  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 64)), dim3(256), 0, c.s, c.D->part, nb, d, dgamma);
   XTRL_LAUNCHED("train ln_bwd");
   return XTRL_OK;
 }
@@ -452,6 +517,8 @@ int validate(const XtrlTrainDesc* D) {
   XTRL_REQUIRE(D->dh % 2 == 0 && D->rot_dim <= D->dh, "train: bad rotary dims");
   XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "train: in_dim mismatch");
   XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "train: evolutionary needs latent buffers");
+  XTRL_REQUIRE(D->S <= EMB_MAXS, "train: state_dim %d > %d unsupported", D->S, EMB_MAXS);
+  XTRL_REQUIRE(D->continuous || D->A <= EMB_MAXA, "train: %d discrete actions > %d unsupported", D->A, EMB_MAXA);
   XTRL_REQUIRE(D->continuous ? (D->prev_action_f && D->next_action_f) : (D->prev_action && D->next_action),
                "train: missing action inputs");
   return XTRL_OK;
@@ -474,7 +541,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
                c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
                D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
                D->evolutionary, D->reward_keep};
-  hipLaunchKernelGGL(k_embed, dim3(blocks((int64_t)T * d, 256)), dim3(256), 0, s, ea);
+  hipLaunchKernelGGL(k_embed, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
   XTRL_LAUNCHED("train embed");
   // decoder blocks
   for (int li = 0; li < D->L; ++li) {
@@ -634,7 +701,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");
     hipLaunchKernelGGL(k_embed_grad_part, dim3(blocks(d, 256), chunks), dim3(256), 0, s, D->dx, d, D->prev_action,
                        D->dewa + d, 2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
-    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 256)), dim3(256), 0, s, D->part, chunks, D->A * d,
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 64)), dim3(256), 0, s, D->part, chunks, D->A * d,
                        c.G(D->act_emb));
     XTRL_LAUNCHED("train embed grad");
   }

@@ -184,22 +184,28 @@ class WorldModelActorCritic(nn.Module):
     def flat_order(self):
         """Parameter order of the flat buffer: the q|k|v|gate|mix weights of each attention block, the
         first actor / critic head layers and to_pred.0 | to_pred_done are adjacent so their
-        concatenations are views (one GEMM operand each)."""
+        concatenations are views (one GEMM operand each).  Groups whose size is a multiple of 4
+        floats come first, so every GEMM weight starts 16-byte aligned (float4 operand loads)."""
         c = self.cfg
-        names = [n for n, _ in self.named_parameters()]
-        pri = []
+        params = dict(self.named_parameters())
+        groups = []
         for li, (_, _) in enumerate(self.blocks()):
             pre = f'transformer.attn_layers.layers.{2 * li}.1.'
             mix = c.value_residual and c.learned_mix and li > 0
-            pri += [pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
-            pri += [pre + 'to_v_gate.weight'] if c.gate_values else []
-            pri += [pre + 'to_value_residual_mix.0.weight'] if mix else []
-            pri += [pre + 'to_v_gate.bias'] if c.gate_values else []
-            pri += [pre + 'to_value_residual_mix.0.bias'] if mix else []
-        pri += ['action_head.0.weight', 'critic_head.0.weight', 'action_head.0.bias', 'critic_head.0.bias']
-        pri += ['to_pred.0.weight', 'to_pred_done.0.weight', 'to_pred.0.bias', 'to_pred_done.0.bias']
-        taken = set(pri)
-        return pri + [n for n in names if n not in taken]
+            groups.append([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
+                          + ([pre + 'to_v_gate.weight'] if c.gate_values else [])
+                          + ([pre + 'to_value_residual_mix.0.weight'] if mix else []))
+            bias = ([pre + 'to_v_gate.bias'] if c.gate_values else []) + \
+                   ([pre + 'to_value_residual_mix.0.bias'] if mix else [])
+            if bias:
+                groups.append(bias)
+        groups += [['action_head.0.weight', 'critic_head.0.weight'], ['action_head.0.bias', 'critic_head.0.bias'],
+                   ['to_pred.0.weight', 'to_pred_done.0.weight'], ['to_pred.0.bias', 'to_pred_done.0.bias']]
+        taken = {n for g in groups for n in g}
+        groups += [[n] for n in params if n not in taken]
+        size = lambda g: sum(params[n].numel() for n in g)
+        groups.sort(key=lambda g: size(g) % 4 != 0)   # stable: aligned groups first
+        return [n for g in groups for n in g]
 
     def bind_flat(self, flat, ws):
         """Record the concatenated weight / gradient views used by forward_train."""
