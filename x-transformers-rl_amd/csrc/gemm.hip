@@ -20,6 +20,8 @@
 // The optional LayerNorm prologue (x-transformers LayerNorm: no affine, eps 1e-5, times gamma;
 // A "N" only) computes per-row mean / rstd for the block's rows (two-pass) and normalises A while
 // staging it.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "philox.h"
 
@@ -64,25 +66,64 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   }
 
   if constexpr (LN) {
-    constexpr int NW = WM * WN * WK;
-    for (int r = wave; r < BM; r += NW) {
-      const int m = m0 + r;
-      float mean = 0.f, rstd = 0.f;
-      if (m < M) {
-        const float* xr = a.A + (int64_t)m * a.lda;
-        float s = 0.f;
-        for (int k = lane; k < K; k += 64) s += xr[k];
-        mean = wave_sum(s) / (float)K;
-        float q = 0.f;
-        for (int k = lane; k < K; k += 64) {
-          const float dlt = xr[k] - mean;
-          q += dlt * dlt;
+    // per-row mean / rstd of the block's rows: each wave takes 4 rows at a time with all their
+    // loads in flight (row held in registers, two-pass variance); K <= 1024 on the VEC path
+    constexpr int NW = WM * WN * WK, RB = 4;
+    if (VEC && K <= 1024) {
+      for (int r0 = wave * RB; r0 < BM; r0 += NW * RB) {
+        float4 v[RB][4];
+        float s[RB];
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {
+          const int m = m0 + r0 + q;
+          const float* xr = a.A + (int64_t)min(m, M - 1) * a.lda;
+          s[q] = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = 4 * (lane + 64 * j);
+            v[q][j] = (m < M && c < K) ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            s[q] += (v[q][j].x + v[q][j].y) + (v[q][j].z + v[q][j].w);
+          }
         }
-        rstd = 1.0f / sqrtf(wave_sum(q) / (float)K + 1e-5f);
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {
+          const float mean = wave_sum(s[q]) / (float)K;
+          float sq = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (4 * (lane + 64 * j) < K) {
+              const float4 x = v[q][j];
+              sq += ((x.x - mean) * (x.x - mean) + (x.y - mean) * (x.y - mean)) +
+                    ((x.z - mean) * (x.z - mean) + (x.w - mean) * (x.w - mean));
+            }
+          }
+          const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+          if (lane == 0 && r0 + q < BM) {
+            row_mean[r0 + q] = mean;
+            row_rstd[r0 + q] = rstd;
+          }
+        }
       }
-      if (lane == 0) {
-        row_mean[r] = mean;
-        row_rstd[r] = rstd;
+    } else {
+      for (int r = wave; r < BM; r += NW) {
+        const int m = m0 + r;
+        float mean = 0.f, rstd = 0.f;
+        if (m < M) {
+          const float* xr = a.A + (int64_t)m * a.lda;
+          float s = 0.f;
+          for (int k = lane; k < K; k += 64) s += xr[k];
+          mean = wave_sum(s) / (float)K;
+          float q = 0.f;
+          for (int k = lane; k < K; k += 64) {
+            const float dlt = xr[k] - mean;
+            q += dlt * dlt;
+          }
+          rstd = 1.0f / sqrtf(wave_sum(q) / (float)K + 1e-5f);
+        }
+        if (lane == 0) {
+          row_mean[r] = mean;
+          row_rstd[r] = rstd;
+        }
       }
     }
     __syncthreads();
@@ -279,15 +320,30 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   if (a.kspan > 0) C += blockIdx.z * a.c_split;
   const bool acc_c = a.beta != 0.f;
   constexpr bool DROP = (EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP);
+  constexpr bool AUX1 = (EPI == EPI_DGELU_DROP || EPI == EPI_DSILU || EPI == EPI_DGATE);
+  constexpr bool AUX2 = (EPI == EPI_DGATE);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);
-    if (n >= N) continue;
-    const float bn = (a.bias && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
+    const bool nok = n < N;
+    const int nc = nok ? n : N - 1;
+    const float bn = (a.bias && nok && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
     const bool act = n < a.act_cols;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
+      // all reads of this lane's 16 elements first (aux inputs, residual, old C): the stores below
+      // may alias them as far as the compiler knows, so interleaving would serialise every access
+      float x1[16], x2[16], rr[16], old[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + (r & 3) + 8 * (r >> 2);
+        const int mc = m < M ? m : M - 1;
+        if constexpr (AUX1) x1[r] = a.aux_in[(int64_t)mc * a.ld_aux_in + nc];
+        if constexpr (AUX2) x2[r] = a.aux_in2[(int64_t)mc * a.ld_aux_in2 + nc];
+        if constexpr (RES) rr[r] = a.R[(int64_t)mc * a.ldr + nc];
+        old[r] = acc_c ? C[(int64_t)mc * a.ldc + nc] : 0.f;
+      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         // rows mb + 8g + 0..3 (a 4-aligned group): one Philox block gives their four keep words
@@ -297,38 +353,41 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
                              a.seed);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+          const int r = 4 * g + q;
           const int m = mb + 8 * g + q;
-          if (m >= M) continue;
-          float v = acc[i][j][4 * g + q] + bn;
+          float v = acc[i][j][r] + bn;
           const uint32_t word = q == 0 ? kw.x : (q == 1 ? kw.y : (q == 2 ? kw.z : kw.w));
+          float aux_o = 0.f;
           if constexpr (EPI == EPI_GELU) v = geluf_(v);
           if constexpr (EPI == EPI_SILU) v = siluf_(v);
           if constexpr (EPI == EPI_GELU_DROP) {
-            a.aux_out[(int64_t)m * a.ld_aux_out + n] = v;
+            aux_o = v;
             v = geluf_(v);
             if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
           }
           if constexpr (EPI == EPI_SILU_SAVE) {
-            a.aux_out[(int64_t)m * a.ld_aux_out + n] = v;
+            aux_o = v;
             if (act) v = siluf_(v);
           }
           if constexpr (EPI == EPI_DGELU_DROP) {
             if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
-            v = v * gelu_grad_(a.aux_in[(int64_t)m * a.ld_aux_in + n]);
+            v = v * gelu_grad_(x1[r]);
           }
           if constexpr (EPI == EPI_DSILU) {
-            if (act) v = v * silu_grad_(a.aux_in[(int64_t)m * a.ld_aux_in + n]);
+            if (act) v = v * silu_grad_(x1[r]);
           }
           if constexpr (EPI == EPI_DGATE) {
-            const float sg = sigmoidf_(a.aux_in2[(int64_t)m * a.ld_aux_in2 + n]);
-            const float o = a.aux_in[(int64_t)m * a.ld_aux_in + n];
-            a.aux_out[(int64_t)m * a.ld_aux_out + n] = (v * o) * (1.0f - sg) * sg;
+            const float sg = sigmoidf_(x2[r]);
+            aux_o = (v * x1[r]) * (1.0f - sg) * sg;
             v = v * sg;
           }
-          if constexpr (RES) v = v + a.R[(int64_t)m * a.ldr + n];
-          float* dst = C + (int64_t)m * a.ldc + n;
-          if (acc_c) v = a.beta * (*dst) + v;
-          *dst = v;
+          if constexpr (RES) v = v + rr[r];
+          if (acc_c) v = a.beta * old[r] + v;
+          if (nok && m < M) {
+            C[(int64_t)m * a.ldc + n] = v;
+            if constexpr (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE)
+              a.aux_out[(int64_t)m * a.ld_aux_out + n] = aux_o;
+          }
         }
       }
     }
@@ -394,16 +453,41 @@ void launch(const GemmArgs& a, hipStream_t s) {
 }
 
 // geometry: 128 x 128 tiles (2 x 2 waves of 64 x 64, four accumulator chains each) when they fill
-// the chip, else 64 x 64 tiles, else 32 x 32 tiles with a 4-way split of K inside the workgroup
-// (decode-sized M).  Operands whose contiguous extent is not a multiple of 4 (or unaligned) take
+// the chip, else 64 x 64 tiles, else (decode-sized M) 64 x 32 tiles with a 2-way or 32 x 32 tiles
+// with a 4-way split of K inside the workgroup.  Operands whose contiguous extent is not a multiple of 4 (or unaligned) take
 // the scalar-load variant, instantiated for the 64 x 64 geometry only.
+int forced_geom() {   // XTRL_GEMM_GEOM=<n> (tuning experiments): force geometry n for VEC launches
+  static int g = [] {
+    const char* e = getenv("XTRL_GEMM_GEOM");
+    return e ? atoi(e) : -1;
+  }();
+  return g;
+}
+
 template <bool TA, bool TB, int EPI, bool LN, bool RES>
 void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   const int64_t tiles128 = (int64_t)((a.M + 127) / 128) * ((a.N + 127) / 128);
   const int64_t tiles64 = (int64_t)((a.M + 63) / 64) * ((a.N + 63) / 64);
+  const int fg = vec ? forced_geom() : -1;
+  if (fg >= 0 && !TA) {
+    switch (fg) {
+      case 0: launch<1, 1, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 1: launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 2: launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 3: launch<1, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 4: launch<1, 2, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 5: launch<2, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 6: launch<1, 1, 8, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      case 7: launch<1, 2, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s); return;
+      default: break;
+    }
+  }
+  // (decode-sized M measured on MI355X, graph-timed: M=1024 N=1024 K=256 64x64 11.6 us vs
+  //  32x32/WK4 17.4; N=260 K=256 64x32/WK2 7.7 vs 8.2; N=256 K=1024 32x32/WK4 13.7 vs 64x64 24.7)
   if (!vec) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, false>(a, s);
   else if (tiles128 >= 192) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
-  else if (tiles64 >= 512 || a.K <= 64) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (tiles64 >= 256 && a.K <= 512) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (a.K <= 256) launch<2, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
   else launch<1, 1, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
 }
 
