@@ -211,7 +211,7 @@ typedef struct XtrlTrainLayer {
   float* o;             /* [T][I] attention output */
   float* og;            /* [T][I] gated output (== o when there are no value gates) */
   float* lse;           /* [b][H][n] */
-  float* u;             /* [T][ff] FF1 pre-activation */
+  float* u;             /* [T][ff] FF1 local derivative: dropout-masked GELU'(pre-activation) */
   float* hd;            /* [T][ff] GELU + dropout output */
 } XtrlTrainLayer;
 
@@ -245,9 +245,9 @@ typedef struct XtrlTrainDesc {
   float* st_final;               /* [T][2] */
   float* ac_in;                  /* [T][in_dim] embed | state_embed | latent_embed */
   float* ewa;                    /* [T][2d] embed | next-action embed */
-  float* zp;                     /* [T][d + 4] pre-activation of to_pred.0 | to_pred_done */
+  float* zp;                     /* [T][d + 4] local derivative of SiLU(to_pred.0) | 1 (done column) */
   float* hp;                     /* [T][d + 4] SiLU(to_pred.0) | done logit */
-  float* z1;                     /* [T][4d] pre-activation of action_head.0 | critic_head.0 */
+  float* z1;                     /* [T][4d] local derivative of SiLU(action_head.0 | critic_head.0) */
   float* h1;                     /* [T][4d] SiLU */
   float* lat_e;                  /* [b][d] */
   /* loss gradients */

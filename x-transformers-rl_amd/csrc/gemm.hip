@@ -29,16 +29,6 @@ namespace xtrl {
 
 namespace {
 
-__device__ __forceinline__ float gelu_grad_(float x) {   // torch GeluBackward (erf form)
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * expf(x * x * -0.5f);
-  return cdf + x * pdf;
-}
-__device__ __forceinline__ float silu_grad_(float x) {   // torch silu_backward factor
-  const float sg = 1.0f / (1.0f + expf(-x));
-  return sg * (1.0f + x * (1.0f - sg));
-}
-
 template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN, BK = 32 * WK, NT = 64 * WM * WN * WK;
@@ -53,7 +43,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int bx = blockIdx.x;
+  const int m0 = blockIdx.y * BM, n0 = bx * BN;
   const int M = a.M, N = a.N;
   int K = a.K;
   const float* __restrict__ Ab = a.A;
@@ -270,6 +261,16 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   // Software pipeline with the only possibly-partial slab (the last) peeled off: the steady-state
   // body is one basic block (loads of slab kt + 1, MFMAs of slab kt, LDS stores of slab kt + 1), so
   // the loads' wait lands at the stores, after the MFMAs.
+  // optional row sums of A (= the bias gradient of a weight-gradient GEMM, whose A is dY^T):
+  // the workgroups of the first column tile add up each staged slab from LDS
+  const bool do_rs = a.rowsum != nullptr && bx == 0;
+  float rs_acc = 0.f;
+  auto rs_slab = [&](int cur) {
+    if (do_rs && tid < BM) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) rs_acc += As[cur][k][tid];
+    }
+  };
   load_slab(0, true);
   store_slab(0);
   __syncthreads();
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMAs (the scheduler sinks them)
     compute(kt & 1);
     __builtin_amdgcn_sched_barrier(0);
+    rs_slab(kt & 1);
     store_slab((kt & 1) ^ 1);
     __syncthreads();
   }
@@ -287,11 +289,20 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     compute(kt & 1);
     __builtin_amdgcn_sched_barrier(0);
+    rs_slab(kt & 1);
     store_slab((kt & 1) ^ 1);
     __syncthreads();
     ++kt;
   }
   compute(kt & 1);
+  rs_slab(kt & 1);
+  if (do_rs && tid < BM) {
+    const int m = m0 + tid;
+    if (m < M && m >= a.rowsum_m0) {
+      if (a.kspan > 0) a.rowsum_ws[(int64_t)blockIdx.z * M + m] = rs_acc;
+      else a.rowsum[m - a.rowsum_m0] += rs_acc;
+    }
+  }
 
   // ---- intra-workgroup split-K: waves wk > 0 hand their tiles to wk == 0 through LDS ----------
   if constexpr (WK > 1) {
@@ -319,8 +330,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
   if (a.kspan > 0) C += blockIdx.z * a.c_split;
   const bool acc_c = a.beta != 0.f;
-  constexpr bool DROP = (EPI == EPI_GELU_DROP || EPI == EPI_DGELU_DROP);
-  constexpr bool AUX1 = (EPI == EPI_DGELU_DROP || EPI == EPI_DSILU || EPI == EPI_DGATE);
+  constexpr bool DROP = (EPI == EPI_GELU_DROP);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE);
   constexpr bool AUX2 = (EPI == EPI_DGATE);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -360,22 +371,27 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
           float aux_o = 0.f;
           if constexpr (EPI == EPI_GELU) v = geluf_(v);
           if constexpr (EPI == EPI_SILU) v = siluf_(v);
-          if constexpr (EPI == EPI_GELU_DROP) {
-            aux_o = v;
-            v = geluf_(v);
-            if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
+          if constexpr (EPI == EPI_GELU_DROP) {   // torch GELU (erf) and GeluBackward's factor
+            const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
+            const float pdf = 0.3989422804014327f * expf(v * v * -0.5f);
+            aux_o = cdf + v * pdf;
+            v = (0.5f * v) * (1.0f + erff(v * 0.70710678118654752f));
+            if (a.drop_thresh) {
+              const bool keep = word >= a.drop_thresh;
+              v = keep ? v * a.inv_keep : 0.f;
+              aux_o = keep ? aux_o * a.inv_keep : 0.f;
+            }
           }
           if constexpr (EPI == EPI_SILU_SAVE) {
-            aux_o = v;
-            if (act) v = siluf_(v);
+            if (act) {
+              const float sg = 1.0f / (1.0f + expf(-v));
+              aux_o = sg * (1.0f + v * (1.0f - sg));
+              v = v / (1.0f + expf(-v));
+            } else {
+              aux_o = 1.0f;
+            }
           }
-          if constexpr (EPI == EPI_DGELU_DROP) {
-            if (a.drop_thresh) v = word >= a.drop_thresh ? v * a.inv_keep : 0.f;
-            v = v * gelu_grad_(x1[r]);
-          }
-          if constexpr (EPI == EPI_DSILU) {
-            if (act) v = v * silu_grad_(x1[r]);
-          }
+          if constexpr (EPI == EPI_MUL_AUX) v = v * x1[r];
           if constexpr (EPI == EPI_DGATE) {
             const float sg = sigmoidf_(x2[r]);
             aux_o = (v * x1[r]) * (1.0f - sg) * sg;
@@ -412,19 +428,44 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
   for (int k = lane; k < D; k += 64) Y[(int64_t)m * ldy + k] = ((xr[k] - mean) * rstd) * gamma[k];
 }
 
-// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] (fixed order: deterministic).
-// Partials are dense [S][M][N]; each thread sums one float4 column of the S slices.
+// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] in a fixed order (deterministic;
+// four interleaved partial sums keep four loads per thread in flight).  Partials are dense
+// [S][M][N]; each thread owns one float4 of C.  Optional row sums (bias gradient): rowsum[m - m0]
+// += sum_z rws[z][m], spread over the grid.
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, int M, int N, float* C, int ldc,
-                                                       float beta) {
+                                                       float beta, const float* rws, float* rowsum, int m0) {
   const int64_t MN = (int64_t)M * N;
+  const int64_t gtid = (int64_t)blockIdx.x * 256 + threadIdx.x, gsz = (int64_t)gridDim.x * 256;
+  if (rowsum) {
+    for (int64_t m = m0 + gtid; m < M; m += gsz) {
+      float acc = rws[m];
+      for (int z = 1; z < S; ++z) acc += rws[(int64_t)z * M + m];
+      rowsum[m - m0] += acc;
+    }
+  }
   if ((N & 3) == 0) {
     const int64_t Q = MN >> 2;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < Q; q += (int64_t)gridDim.x * 256) {
-      float4 acc = reinterpret_cast<const float4*>(ws)[q];
-      for (int z = 1; z < S; ++z) {
-        const float4 p = reinterpret_cast<const float4*>(ws + z * MN)[q];
-        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+    const float4* w4 = reinterpret_cast<const float4*>(ws);
+    for (int64_t q = gtid; q < Q; q += gsz) {
+      float4 a0 = w4[q], a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
+      int z = 1;
+      for (; z + 3 < S; z += 4) {
+        const float4 p0 = w4[(int64_t)z * Q + q], p1 = w4[(int64_t)(z + 1) * Q + q];
+        const float4 p2 = w4[(int64_t)(z + 2) * Q + q], p3 = w4[(int64_t)(z + 3) * Q + q];
+        a0.x += p0.x; a0.y += p0.y; a0.z += p0.z; a0.w += p0.w;
+        a1.x += p1.x; a1.y += p1.y; a1.z += p1.z; a1.w += p1.w;
+        a2.x += p2.x; a2.y += p2.y; a2.z += p2.z; a2.w += p2.w;
+        a3.x += p3.x; a3.y += p3.y; a3.z += p3.z; a3.w += p3.w;
       }
+      for (; z < S; ++z) {
+        const float4 p = w4[(int64_t)z * Q + q];
+        a0.x += p.x; a0.y += p.y; a0.z += p.z; a0.w += p.w;
+      }
+      float4 acc;
+      acc.x = (a0.x + a1.x) + (a2.x + a3.x);
+      acc.y = (a0.y + a1.y) + (a2.y + a3.y);
+      acc.z = (a0.z + a1.z) + (a2.z + a3.z);
+      acc.w = (a0.w + a1.w) + (a2.w + a3.w);
       const int64_t i = q << 2;
       const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
       float* dst = C + (int64_t)m * ldc + n;
@@ -435,7 +476,7 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
     }
     return;
   }
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = gtid; i < MN; i += gsz) {
     float acc = ws[i];
     for (int z = 1; z < S; ++z) acc += ws[z * MN + i];
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
@@ -503,7 +544,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   XTRL_REQUIRE(!(a.gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
   XTRL_REQUIRE(!((epi == EPI_GELU_DROP || epi == EPI_SILU_SAVE || epi == EPI_DGATE) && !a.aux_out),
                "gemm: epilogue %d needs aux_out", epi);
-  XTRL_REQUIRE(!((epi == EPI_DGELU_DROP || epi == EPI_DSILU || epi == EPI_DGATE) && !a.aux_in),
+  XTRL_REQUIRE(!((epi == EPI_MUL_AUX || epi == EPI_DGATE) && !a.aux_in),
                "gemm: epilogue %d needs aux_in", epi);
   XTRL_REQUIRE(!(epi == EPI_DGATE && !a.aux_in2), "gemm: gate epilogue needs aux_in2");
   if (a.M == 0 || a.N == 0) return XTRL_OK;
@@ -527,8 +568,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   XG(0, 0, EPI_SILU_SAVE, false, false)
   // dgrad (B = weight used as [k][n]) with fused activation / dropout / gate backward
   XG(0, 1, EPI_NONE, false, false)
-  XG(0, 1, EPI_DGELU_DROP, false, false)
-  XG(0, 1, EPI_DSILU, false, false)
+  XG(0, 1, EPI_MUL_AUX, false, false)
   XG(0, 1, EPI_DGATE, false, false)
   // wgrad (A = dY^T)
   XG(1, 1, EPI_NONE, false, false)
@@ -552,9 +592,10 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
 // weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
 // split the token range over workgroups (partial 64x64 tiles in ws), then a fixed-order sum
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
-               float* ws, int64_t ws_floats, hipStream_t s) {
+               float* ws, int64_t ws_floats, hipStream_t s, float* db, int db_n0) {
   XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
   XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
+  XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
   // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
   // 128 x 128 tiles (2 workgroups / CU by registers) when the weight is large, else 64 x 64 (4 / CU);
   // split the tokens until one resident round of workgroups covers the chip, keeping at least 8
@@ -567,7 +608,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (M + 255) / 256));
   int kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
   splits = (M + kspan - 1) / kspan;
-  while (splits > 1 && (int64_t)splits * N * K > ws_floats) {   // fit the partial slabs in ws
+  auto need = [&](int sp) { return (int64_t)sp * N * K + (db ? (int64_t)sp * N : 0); };
+  while (splits > 1 && need(splits) > ws_floats) {   // fit the partial slabs in ws
     splits = std::max(1, splits / 2);
     kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
     splits = (M + kspan - 1) / kspan;
@@ -575,21 +617,25 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0) && (N % 4 == 0) && (K % 4 == 0);
   GemmArgs a;
   a.A = dY; a.B = X; a.C = dW; a.lda = ldy; a.ldb = ldx; a.ldc = ldw; a.M = N; a.N = K; a.K = M; a.beta = beta;
+  a.rowsum = db;
+  a.rowsum_m0 = db_n0;
   if (splits > 1) {
-    XTRL_REQUIRE(ws && (int64_t)splits * N * K <= ws_floats, "gemm_wgrad: workspace too small");
+    XTRL_REQUIRE(ws && need(splits) <= ws_floats, "gemm_wgrad: workspace too small");
     a.C = ws;
     a.ldc = K;
     a.beta = 0.f;
     a.kspan = kspan;
     a.c_split = (int64_t)N * K;
+    a.rowsum_ws = ws + (int64_t)splits * N * K;
   }
   if (!vec) launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, false>(a, s);
   else if (big) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
   else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
   if (splits > 1) {
     const int64_t MN = (int64_t)N * K;
-    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::min<int64_t>((MN + 255) / 256, 2048)), dim3(256), 0, s,
-                       ws, splits, N, K, dW, ldw, beta);
+    const int64_t units = (K % 4 == 0) ? MN / 4 : MN;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 2048))),
+                       dim3(256), 0, s, ws, splits, N, K, dW, ldw, beta, a.rowsum_ws, db, db_n0);
   }
   XTRL_LAUNCHED("gemm_wgrad");
   return XTRL_OK;
@@ -626,7 +672,7 @@ extern "C" int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, c
 
 extern "C" int xtrl_gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N,
                                int K, float beta, float* ws, int64_t ws_floats, void* stream) {
-  return xtrl::gemm_wgrad(dY, ldy, X, ldx, dW, ldw, M, N, K, beta, ws, ws_floats, xtrl::as_stream(stream));
+  return xtrl::gemm_wgrad(dY, ldy, X, ldx, dW, ldw, M, N, K, beta, ws, ws_floats, xtrl::as_stream(stream), nullptr, 0);
 }
 
 extern "C" int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D,

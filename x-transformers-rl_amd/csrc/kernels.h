@@ -15,10 +15,11 @@ enum GemmEpi : int {
   EPI_NONE = 0,        // (bias)
   EPI_GELU = 1,        // gelu(v)
   EPI_SILU = 2,        // silu(v)
-  EPI_GELU_DROP = 3,   // aux_out = v; C = dropout(gelu(v))                       (FF1 forward, train)
-  EPI_SILU_SAVE = 4,   // aux_out = v; C = n < act_cols ? silu(v) : v              (head hidden layers)
-  EPI_DGELU_DROP = 5,  // C = dropout_bwd(v) * gelu'(aux_in)                        (FF2 dgrad -> FF1 pre-act)
-  EPI_DSILU = 6,       // C = n < act_cols ? v * silu'(aux_in) : v
+  // forward epilogues that also save the local derivative for the backward (so the backward
+  // epilogue is one multiply: no erf / exp / dropout RNG recomputation)
+  EPI_GELU_DROP = 3,   // C = drop(gelu(v)); aux_out = drop(gelu'(v))   (drop: keep ? x / (1 - p) : 0)
+  EPI_SILU_SAVE = 4,   // n < act_cols: C = silu(v), aux_out = silu'(v);  else C = v, aux_out = 1
+  EPI_MUL_AUX = 5,     // C = v * aux_in                                 (dgrad through a saved derivative)
   EPI_DGATE = 7,       // s = sigmoid(aux_in2): C = v * s; aux_out = v * aux_in * (1 - s) * s   (value gate)
 };
 
@@ -40,17 +41,21 @@ struct GemmArgs {
   const float* aux_in = nullptr;  int ld_aux_in = 0;
   const float* aux_in2 = nullptr; int ld_aux_in2 = 0;
   float* aux_out = nullptr;       int ld_aux_out = 0;
-  uint64_t seed = 0;              // dropout (EPI_GELU_DROP / EPI_DGELU_DROP): keep(m, n) =
+  uint64_t seed = 0;              // dropout (EPI_GELU_DROP): keep(m, n) =
   uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT) word (m & 3)
   uint32_t drop_thresh = 0;       //   >= drop_thresh (0: no dropout)
   float inv_keep = 1.f;
+  float* rowsum = nullptr;        // += row sums of A (rows >= rowsum_m0, at rowsum[m - rowsum_m0]) —
+  int rowsum_m0 = 0;              //   the bias gradient when A = dY^T; with split-K the per-split
+  float* rowsum_ws = nullptr;     //   sums go to rowsum_ws[z][M] and the reduce kernel adds them
 };
 
 // launch C = op(A, B) for the combination (trans_a, trans_b, epi, LN = gamma != 0, RES = R != 0)
 int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s);
-// dW[N][K] (+)= dY^T X over M tokens, split-K over workgroups with a fixed-order reduction
+// dW[N][K] (+)= dY^T X over M tokens, split-K over workgroups with a fixed-order reduction;
+// db (optional, accumulated) [n - db_n0] += sum_m dY[m][n] for n >= db_n0 (the bias gradient)
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
-               float* ws, int64_t ws_floats, hipStream_t s);
+               float* ws, int64_t ws_floats, hipStream_t s, float* db = nullptr, int db_n0 = 0);
 int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
              const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
              int K, int act, hipStream_t s);

@@ -435,23 +435,18 @@ int linear_fwd(const Ctx& c, const float* A, int lda, const float* W, const floa
 // dX[M][K] = dY[M][N] . W[N][K] with an epilogue
 int linear_dgrad(const Ctx& c, const float* dY, int ldy, const float* W, float* dX, int ldx, int M, int N, int K,
                  int epi, const float* aux_in = nullptr, int ld_aux = 0, int act_cols = 1 << 30,
-                 uint32_t drop_off = 0, const float* aux_in2 = nullptr, int ld_aux2 = 0, float* aux_out = nullptr,
-                 int ld_aux_out = 0) {
+                 const float* aux_in2 = nullptr, int ld_aux2 = 0, float* aux_out = nullptr, int ld_aux_out = 0) {
   GemmArgs g;
   g.A = dY; g.lda = ldy; g.B = W; g.ldb = K; g.C = dX; g.ldc = ldx; g.M = M; g.N = K; g.K = N;
   g.aux_in = aux_in; g.ld_aux_in = ld_aux; g.act_cols = act_cols;
   g.aux_in2 = aux_in2; g.ld_aux_in2 = ld_aux2; g.aux_out = aux_out; g.ld_aux_out = ld_aux_out;
-  if (epi == EPI_DGELU_DROP) {
-    g.seed = c.D->seed;
-    g.drop_off = drop_off;
-    g.drop_thresh = dropout_thresh(c.D->dropout);
-    g.inv_keep = c.D->dropout > 0.f ? 1.f / (1.f - c.D->dropout) : 1.f;
-  }
   return gemm_run(g, 0, 1, epi, c.s);
 }
 
-int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float* dW, int M, int N, int K) {
-  return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s);
+// dW += dY^T X (and the bias gradient db[n - db_n0] += column sums of dY for n >= db_n0)
+int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float* dW, int M, int N, int K,
+          float* db = nullptr, int db_n0 = 0) {
+  return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s, db, db_n0);
 }
 
 // dst[0:cols] += sum over rows of src (optionally weighted by rw[r * ld_rw] * rw_scale)
@@ -600,22 +595,18 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4, S1x2 = 2 * (D->S + 1);
   int rc;
   // ---- actor / critic heads
-  if ((rc = wgrad(c, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d))) return rc;
-  if ((rc = colsum(c, D->d_raw, D->n_out, T, D->n_out, c.G(D->b_a2)))) return rc;
-  if ((rc = wgrad(c, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d))) return rc;
-  if ((rc = colsum(c, D->d_values, D->B, T, D->B, c.G(D->b_c2)))) return rc;
-  if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_DSILU, D->z1,
+  if ((rc = wgrad(c, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
+  if ((rc = wgrad(c, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d, c.G(D->b_c2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_MUL_AUX, D->z1,
                          4 * d)))
     return rc;
-  if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_DSILU,
+  if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_MUL_AUX,
                          D->z1 + 2 * d, 4 * d)))
     return rc;
-  if ((rc = wgrad(c, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim))) return rc;
-  if ((rc = colsum(c, D->dz1, 4 * d, T, 4 * d, c.G(D->b_h1)))) return rc;
+  if ((rc = wgrad(c, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
   if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
   // state embedding and gene conditioning
-  if ((rc = wgrad(c, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S))) return rc;
-  if ((rc = colsum(c, D->dac + d, D->in_dim, T, d, c.G(D->b_se)))) return rc;
+  if ((rc = wgrad(c, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
   if (D->evolutionary) {
     XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
     hipLaunchKernelGGL(k_latent_grad, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->dac, D->in_dim, 2 * d, D->b,
@@ -625,12 +616,10 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     XTRL_LAUNCHED("train latent grad");
   }
   // ---- world-model heads
-  if ((rc = wgrad(c, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d))) return rc;
-  if ((rc = colsum(c, D->d_pred, S1x2, T, S1x2, c.G(D->b_pred2)))) return rc;
-  if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_DSILU, D->zp, ldp))) return rc;
+  if ((rc = wgrad(c, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_MUL_AUX, D->zp, ldp))) return rc;
   hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);
-  if ((rc = wgrad(c, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d))) return rc;
-  if ((rc = colsum(c, D->dzp, ldp, T, d + 1, c.G(D->b_pd)))) return rc;
+  if ((rc = wgrad(c, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
   if ((rc = linear_dgrad(c, D->dzp, ldp, c.P(D->w_pd), D->dewa, 2 * d, T, d + 1, 2 * d, EPI_NONE))) return rc;
   // action-embedding gradient of the next-action input (and, below, of the previous action)
   // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
@@ -641,20 +630,16 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   for (int li = D->L - 1; li >= 0; --li) {
     const XtrlTrainLayer& Ly = D->layers[li];
     // FF2 (+ residual): dx is the gradient w.r.t. the block output
-    if ((rc = wgrad(c, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff))) return rc;
-    if ((rc = colsum(c, D->dx, d, T, d, c.G(Ly.b_ff2)))) return rc;
-    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, ff, T, d, ff, EPI_DGELU_DROP, Ly.u, ff, 1 << 30,
-                           D->ff_offset + (uint32_t)li)))
-      return rc;
-    if ((rc = wgrad(c, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d))) return rc;
-    if ((rc = colsum(c, D->dff, ff, T, ff, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = wgrad(c, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
+    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, ff, T, d, ff, EPI_MUL_AUX, Ly.u, ff))) return rc;
+    if ((rc = wgrad(c, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
     if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
     if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
       return rc;
     // attention out-projection (+ residual) and the value gate
     if ((rc = wgrad(c, D->dx, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
     if (D->gate_values) {
-      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30, 0,
+      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30,
                              Ly.proj + 3 * I, Ly.n_qkv, D->dproj + 3 * I, Ly.n_qkv)))
         return rc;
     } else {
@@ -679,8 +664,8 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * D->H, 256)), dim3(256), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
-    if ((rc = wgrad(c, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d))) return rc;
-    if (Ly.b_proj >= 0 && (rc = colsum(c, D->dproj + 3 * I, Ly.n_qkv, T, Ly.n_qkv - 3 * I, c.G(Ly.b_proj)))) return rc;
+    if ((rc = wgrad(c, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
+      return rc;
     if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
     if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
                      c.G(Ly.ln_attn))))
