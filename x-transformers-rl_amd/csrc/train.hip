@@ -207,8 +207,9 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
 }
 
 // ---- rotary + value-residual mix (x-transformers Attention) --------------
-// one thread per (token, head): q, k rotated on their first rot_dim channels (interleaved pairs,
-// position = step within the episode); v mixed towards the first layer's v
+// one thread per (token, column pair) of q | k | v (coalesced float2 traffic): q and k rotated on
+// their first rot_dim channels (interleaved pairs, position = step within the episode); v mixed
+// towards the first layer's v
 struct PrepArgs {
   const float* proj;    // [T][n_qkv]
   const float* vfirst;  // layer-0 proj (v at column 2I)
@@ -218,42 +219,37 @@ struct PrepArgs {
 };
 
 __global__ __launch_bounds__(256) void k_qkv_prep(const PrepArgs a) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.T * a.H) return;
-  const int t = i / a.H, h = i - t * a.H;
-  const float pos = (float)(t % a.n);
-  const float* pr = a.proj + (int64_t)t * a.n_qkv;
-  float* out = a.qkv + (int64_t)t * 3 * a.I;
-  for (int which = 0; which < 2; ++which) {
-    const float* src = pr + which * a.I + h * a.dh;
-    float* dst = out + which * a.I + h * a.dh;
-    for (int j = 0; j < a.dh; j += 2) {
-      const float x0 = src[j], x1 = src[j + 1];
-      if (j < a.rot_dim) {
-        const float f = pos * a.inv_freq[j >> 1];
-        const float cs = cosf(f), sn = sinf(f);
-        dst[j] = x0 * cs + (-x1) * sn;
-        dst[j + 1] = x1 * cs + x0 * sn;
-      } else {
-        dst[j] = x0;
-        dst[j + 1] = x1;
-      }
+  const int P = 3 * a.I / 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)a.T * P) return;
+  const int t = (int)(i / P), col = 2 * (int)(i - (int64_t)t * P);
+  const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
+  const float2 x = *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col);
+  float2 y;
+  if (seg < 2) {
+    if (j < a.rot_dim) {
+      const float f = (float)(t % a.n) * a.inv_freq[j >> 1];
+      const float cs = cosf(f), sn = sinf(f);
+      y.x = x.x * cs + (-x.y) * sn;
+      y.y = x.y * cs + x.x * sn;
+    } else {
+      y = x;
     }
-  }
-  const float* v = pr + 2 * a.I + h * a.dh;
-  float* dv = out + 2 * a.I + h * a.dh;
-  if (a.mix_col >= 0) {
-    const float m = sigmoidf_(pr[a.mix_col + h]);
-    const float* vf = a.vfirst + (int64_t)t * a.ld_vfirst + 2 * a.I + h * a.dh;
-    for (int j = 0; j < a.dh; ++j) dv[j] = lerpf_(v[j], vf[j], m);
+  } else if (a.mix_col >= 0) {
+    const float m = sigmoidf_(a.proj[(int64_t)t * a.n_qkv + a.mix_col + h]);
+    const float2 vf = *reinterpret_cast<const float2*>(a.vfirst + (int64_t)t * a.ld_vfirst + 2 * a.I + within);
+    y.x = lerpf_(x.x, vf.x, m);
+    y.y = lerpf_(x.y, vf.y, m);
   } else {
-    for (int j = 0; j < a.dh; ++j) dv[j] = v[j];
+    y = x;
   }
+  *reinterpret_cast<float2*>(a.qkv + (int64_t)t * 3 * a.I + col) = y;
 }
 
 // backward of k_qkv_prep, in place on dproj ([T][n_qkv], dq | dk | dv written by the attention
 // backward): inverse rotation of dq, dk; lerp backward for v (dv -> (1 - m) dv, dvfirst += m dv,
-// d mix_pre = sum(dv * (vf - v)) * m (1 - m)); layer 0 adds the accumulated dvfirst to its dv
+// d mix_pre = sum over the head's channels of dv (vf - v), times m (1 - m): a shuffle reduction over
+// the head's dh / 2 consecutive lanes); layer 0 adds the accumulated dvfirst to its dv
 struct PrepBwdArgs {
   float* dproj;
   const float* proj;
@@ -264,38 +260,56 @@ struct PrepBwdArgs {
 };
 
 __global__ __launch_bounds__(256) void k_qkv_prep_bwd(const PrepBwdArgs a) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= a.T * a.H) return;
-  const int t = i / a.H, h = i - t * a.H;
-  const float pos = (float)(t % a.n);
-  float* dr = a.dproj + (int64_t)t * a.n_qkv;
-  for (int which = 0; which < 2; ++which) {
-    float* g = dr + which * a.I + h * a.dh;
-    for (int j = 0; j < a.rot_dim && j < a.dh; j += 2) {
-      const float f = pos * a.inv_freq[j >> 1];
-      const float cs = cosf(f), sn = sinf(f);
-      const float g0 = g[j], g1 = g[j + 1];
-      g[j] = g0 * cs + g1 * sn;
-      g[j + 1] = g1 * cs + (-g0) * sn;
+  const int P = 3 * a.I / 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i < (int64_t)a.T * P;
+  const int64_t ic = valid ? i : 0;
+  const int t = (int)(ic / P), col = 2 * (int)(ic - (int64_t)t * P);
+  const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
+  float* g = a.dproj + (int64_t)t * a.n_qkv + col;
+  float dm = 0.f, m = 0.f;
+  if (valid) {
+    float2 gv = *reinterpret_cast<float2*>(g);
+    if (seg < 2) {
+      if (j < a.rot_dim) {
+        const float f = (float)(t % a.n) * a.inv_freq[j >> 1];
+        const float cs = cosf(f), sn = sinf(f);
+        const float g0 = gv.x, g1 = gv.y;
+        gv.x = g0 * cs + g1 * sn;
+        gv.y = g1 * cs + (-g0) * sn;
+        *reinterpret_cast<float2*>(g) = gv;
+      }
+    } else {
+      float2* dvf = reinterpret_cast<float2*>(a.dvfirst + (int64_t)t * a.I + within);
+      if (a.mix_col >= 0) {
+        const float* pr = a.proj + (int64_t)t * a.n_qkv;
+        m = sigmoidf_(pr[a.mix_col + h]);
+        const float2 v = *reinterpret_cast<const float2*>(pr + col);
+        const float2 vf = *reinterpret_cast<const float2*>(a.vfirst + (int64_t)t * a.ld_vfirst + col);
+        dm = gv.x * (vf.x - v.x) + gv.y * (vf.y - v.y);
+        float2 f;
+        f.x = gv.x * m;
+        f.y = gv.y * m;
+        if (a.accumulate) {
+          const float2 o = *dvf;
+          f.x += o.x;
+          f.y += o.y;
+        }
+        *dvf = f;
+        gv.x = gv.x * (1.0f - m);
+        gv.y = gv.y * (1.0f - m);
+        *reinterpret_cast<float2*>(g) = gv;
+      } else if (a.first_layer && a.accumulate) {
+        const float2 o = *dvf;
+        gv.x += o.x;
+        gv.y += o.y;
+        *reinterpret_cast<float2*>(g) = gv;
+      }
     }
   }
-  float* gv = dr + 2 * a.I + h * a.dh;
-  float* dvf = a.dvfirst + (int64_t)t * a.I + h * a.dh;
-  if (a.mix_col >= 0) {
-    const float* pr = a.proj + (int64_t)t * a.n_qkv;
-    const float m = sigmoidf_(pr[a.mix_col + h]);
-    const float* v = pr + 2 * a.I + h * a.dh;
-    const float* vf = a.vfirst + (int64_t)t * a.ld_vfirst + 2 * a.I + h * a.dh;
-    float dm = 0.f;
-    for (int j = 0; j < a.dh; ++j) {
-      const float g = gv[j];
-      dm += g * (vf[j] - v[j]);
-      gv[j] = g * (1.0f - m);
-      dvf[j] = a.accumulate ? dvf[j] + g * m : g * m;
-    }
-    dr[a.mix_col + h] = dm * (1.0f - m) * m;
-  } else if (a.first_layer && a.accumulate) {
-    for (int j = 0; j < a.dh; ++j) gv[j] += dvf[j];
+  if (a.mix_col >= 0) {   // every lane takes part in the shuffles (groups of dh / 2 aligned lanes)
+    for (int o = a.dh >> 2; o > 0; o >>= 1) dm += __shfl_xor(dm, o, 64);
+    if (valid && seg == 2 && j == 0) a.dproj[(int64_t)t * a.n_qkv + a.mix_col + h] = dm * (1.0f - m) * m;
   }
 }
 
@@ -548,7 +562,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
     const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
     PrepArgs pa{Ly.proj, D->layers[0].proj, Ly.qkv, D->inv_freq, T, D->n, D->H, D->dh, I, Ly.n_qkv,
                 D->layers[0].n_qkv, D->rot_dim, mix_col};
-    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks((int64_t)T * D->H, 256)), dim3(256), 0, s, pa);
+    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks((int64_t)T * 3 * I / 2, 256)), dim3(256), 0, s, pa);
     XTRL_LAUNCHED("train qkv_prep");
     const AttnProblem ap = attn_problem(c, Ly, li);
     if ((rc = attn_fwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse,
@@ -661,7 +675,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     PrepBwdArgs pb{D->dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
                    Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
                    (li == 0 ? any_mix : deeper_mix) ? 1 : 0};
-    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * D->H, 256)), dim3(256), 0, s, pb);
+    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * 3 * I / 2, 256)), dim3(256), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
     if ((rc = wgrad(c, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
@@ -680,7 +694,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = colsum(c, D->dx, d, T, d, c.G(D->act_emb_b)))) return rc;
     if ((rc = colsum(c, D->dewa + d, 2 * d, T, d, c.G(D->act_emb_b)))) return rc;
   } else {
-    int chunks = std::min(128, std::max(1, T / 64));
+    int chunks = std::min(512, std::max(1, T / 32));
     const int chunk_rows = (T + chunks - 1) / chunks;
     chunks = (T + chunk_rows - 1) / chunk_rows;
     XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");
