@@ -52,13 +52,14 @@ CONFIGS = {
 }
 
 
-def build_learner(cfg, seed, use_graph=True):
+def build_learner(cfg, seed, use_graph=True, world=1):
     from xtrl_amd import Learner, SynthVecSim
     wm = dict(attn_dim_head=cfg['dim_head'], heads=cfg['heads'], depth=cfg['depth'])
     if cfg['gates']:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
-                      max_timesteps=cfg['T'], batch_size=cfg['batch'], num_episodes_per_update=cfg['episodes'],
+                      max_timesteps=cfg['T'], batch_size=cfg['batch'],
+                      num_episodes_per_update=cfg['episodes'] * world,   # weak scaling: episodes per GPU fixed
                       evolutionary=cfg['evo'], evolve_every=5, evolve_after_step=10,
                       latent_gene_pool=dict(dim=32, num_genes_per_island=3, num_selected=2, tournament_size=2),
                       agent_kwargs=dict(hidden_dim=cfg['dim'], dropout=cfg['dropout'], seed=seed,
@@ -239,7 +240,7 @@ def main():
         torch.cuda.set_device(0)
     cfg = CONFIGS[args.config]
     torch.manual_seed(args.seed)
-    learner, env = build_learner(cfg, args.seed, use_graph=not args.no_graph)
+    learner, env = build_learner(cfg, args.seed, use_graph=not args.no_graph, world=world)
     T = cfg['T']
 
     for _ in range(args.warmup):

@@ -52,21 +52,37 @@ def shard_pairs(pairs, world, rank):
     return pairs[start:start + size], start
 
 
+def _on_backend_device(t):
+    """RCCL ("nccl") only moves device tensors: stage host tensors through the GPU."""
+    if t.device.type == 'cpu' and dist.get_backend() == 'nccl':
+        return t.to(torch.device('cuda', torch.cuda.current_device())), True
+    return t, False
+
+
 def mean_(t):
     """In-place mean over ranks (maybe_distributed_mean, distributed.py:34-40)."""
     if is_distributed():
-        dist.all_reduce(t)
-        t.div_(dist.get_world_size())
+        x, staged = _on_backend_device(t)
+        dist.all_reduce(x)
+        x.div_(dist.get_world_size())
+        if staged:
+            t.copy_(x)
     return t
 
 
 def sum_(t):
     if is_distributed():
-        dist.all_reduce(t)
+        x, staged = _on_backend_device(t)
+        dist.all_reduce(x)
+        if staged:
+            t.copy_(x)
     return t
 
 
 def broadcast_(t, src=0):
     if is_distributed():
-        dist.broadcast(t, src)
+        x, staged = _on_backend_device(t)
+        dist.broadcast(x, src)
+        if staged:
+            t.copy_(x)
     return t

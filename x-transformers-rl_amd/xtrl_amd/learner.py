@@ -107,6 +107,9 @@ class Agent(nn.Module):
         self.cfg = c
         self.model = WorldModelActorCritic(c).to(dev)
         self.flat = FlatParams(self.model, dev, order=self.model.flat_order())
+        dist_.broadcast_(self.flat.flat)          # identical initial weights on every rank (DDP semantics)
+        if self.gene_pool is not None:
+            dist_.broadcast_(self.gene_pool.genes)
 
         # EMA copy (ema-pytorch semantics restated: update_after_step 100, update_every 10, power 2/3)
         self.ema_model = copy.deepcopy(self.model)
@@ -375,6 +378,10 @@ class Learner(nn.Module):
         n_genes = self.agent.gene_pool.num_genes if evolutionary else 1
         self.episode_genes = [(e, g) for e in range(num_episodes_per_update) for g in range(n_genes)]
         world, rank = self.accelerator.num_processes, self.accelerator.process_index
+        # every rank runs the same number of optimiser steps (one gradient all-reduce each), so the
+        # (episode, gene) pairs must split evenly (the reference all-gathers instead, xtrl.py:868-871)
+        assert world == 1 or len(self.episode_genes) % world == 0, \
+            f'{len(self.episode_genes)} (episode, gene) pairs do not split evenly over {world} processes'
         self.episode_genes_for_process, self.slot_offset = dist_.shard_pairs(self.episode_genes, world, rank)
         self.num_actions, self.continuous_actions = num_actions, continuous_actions
         self.continuous_actions_clamp = continuous_actions_clamp
