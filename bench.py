@@ -32,7 +32,7 @@ import torch         # noqa: E402
 import torch.distributed as dist   # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-F32_PEAK_TFLOPS = 157.3    # dense fp32 MFMA / vector peak
+MFMA_F32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
 
 CONFIGS = {
     # configs[2] of BASELINE.json — the north-star workload, per GPU
@@ -126,6 +126,47 @@ class DecodeAttnTimer:
     def detach(self):
         self.eng.desc.prof_events = None
         self.eng.graph = None
+
+
+class WgradGemmTimer:
+    """HIP events around every launch of the dominant learn kernel — the 128x128-tile
+    weight-gradient GEMM k_gemm<2,2,1,2,2,T,T,...> — inside xtrl_train_backward (XtrlTrainDesc
+    prof_events / prof_flops), on the learn stream, over the timed region."""
+
+    KERNEL = 'k_gemm<2, 2, 1, 2, 2, true, true'
+
+    def __init__(self, agent, cap=8192):
+        import ctypes as C
+        self.C, self.cap = C, cap
+        self.events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cap)]
+        for e in self.events:
+            e.record()
+        torch.cuda.synchronize()
+        self.arr = (C.c_void_p * (2 * cap))(*[e.cuda_event for e in self.events])
+        self.flops = (C.c_double * cap)()
+        self.n = C.c_int(0)
+        self.agent = agent
+        self.ms, self.launches, self.total_flops = 0.0, 0, 0.0
+
+    def attach(self):
+        D = self.agent._train_step.D
+        D.prof_events = self.C.cast(self.arr, self.C.POINTER(self.C.c_void_p))
+        D.prof_flops = self.C.cast(self.flops, self.C.c_void_p)
+        D.prof_cap = self.cap
+        D.prof_n = self.C.cast(self.C.pointer(self.n), self.C.c_void_p)
+        self.n.value = 0
+
+    def collect(self):
+        torch.cuda.synchronize()
+        for i in range(self.n.value):
+            self.ms += self.events[2 * i].elapsed_time(self.events[2 * i + 1])
+            self.total_flops += self.flops[i]
+        self.launches += self.n.value
+        self.n.value = 0
+
+    def detach(self):
+        D = self.agent._train_step.D
+        D.prof_events, D.prof_flops, D.prof_cap, D.prof_n = None, None, 0, None
 
 
 def pmc_traffic(kernel):
@@ -249,6 +290,9 @@ def main():
     if timer is not None:
         one_update(learner, env, T)        # capture the graph with the event records inside (untimed)
         timer.ms, timer.launches, timer.bytes = 0.0, 0, 0.0
+    gtimer = None if args.no_roofline else WgradGemmTimer(learner.agent)
+    if gtimer is not None:
+        gtimer.attach()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -276,14 +320,26 @@ def main():
 
     phase_ms = dict(rollout=round(sum(e[0].elapsed_time(e[1]) for e in PHASES) / len(PHASES), 2),
                     learn=round(sum(e[1].elapsed_time(e[2]) for e in PHASES) / len(PHASES), 2))
-    roofline = None
+    roofline = attn_roofline = None
+    if gtimer is not None:
+        gtimer.collect()
+        gtimer.detach()
+        if gtimer.launches:
+            avg_s = gtimer.ms / gtimer.launches / 1e3
+            flops = gtimer.total_flops / gtimer.launches
+            achieved = flops / avg_s / 1e12
+            roofline = dict(kernel='k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, 128x128 tiles, split-K; '
+                                   'the largest kernel of the update)', bound='mfma', achieved=round(achieved, 2),
+                            peak=MFMA_F32_PEAK_TFLOPS, unit='TFLOP/s', frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                            traffic=pmc_traffic(WgradGemmTimer.KERNEL), avg_launch_us=round(avg_s * 1e6, 2),
+                            flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
         achieved = timer.bytes / timer.launches / avg_s / 1e9
-        roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache)', bound='hbm',
-                        achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s', frac=round(achieved / HBM_PEAK_GBS, 4),
-                        traffic=pmc_traffic('k_attn_decode'), avg_launch_us=round(avg_s * 1e6, 2),
-                        bytes_per_launch=round(timer.bytes / timer.launches))
+        attn_roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache)', bound='hbm',
+                             achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
+                             frac=round(achieved / HBM_PEAK_GBS, 4), traffic=pmc_traffic('k_attn_decode'),
+                             avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=round(timer.bytes / timer.launches))
         timer.detach()
 
     loss_delta = None
@@ -302,7 +358,8 @@ def main():
                     data='synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)',
                     config=dict(workload=cfg['workload'], global_batch=cfg['episodes'] * (3 if cfg['evo'] else 1) * world,
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
-                    roofline=roofline, cpu_baseline=cpu, ppo_loss=loss_delta, phase_ms=phase_ms)
+                    roofline=roofline, attention_roofline=attn_roofline, cpu_baseline=cpu, ppo_loss=loss_delta,
+                    phase_ms=phase_ms)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -272,6 +272,13 @@ typedef struct XtrlTrainDesc {
   float* ws;                     /* split-K weight-gradient partial tiles */
   int64_t ws_floats;
   const XtrlTrainLayer* layers;  /* host array [L] */
+  /* optional live timing of the dominant kernel (the 128x128-tile weight-gradient GEMM): event pair
+   * (prof_events[2i], prof_events[2i+1]) brackets its i-th launch and prof_flops[i] = 2 M N K;
+   * *prof_n counts launches (the caller resets it); NULL prof_events = off */
+  void** prof_events;
+  double* prof_flops;
+  int prof_cap;
+  int* prof_n;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

@@ -592,7 +592,7 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
 // weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
 // split the token range over workgroups (partial 64x64 tiles in ws), then a fixed-order sum
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
-               float* ws, int64_t ws_floats, hipStream_t s, float* db, int db_n0) {
+               float* ws, int64_t ws_floats, hipStream_t s, float* db, int db_n0, const GemmProfile* prof) {
   XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
   XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
   XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
@@ -629,8 +629,16 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
     a.rowsum_ws = ws + (int64_t)splits * N * K;
   }
   if (!vec) launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, false>(a, s);
-  else if (big) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
-  else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
+  else if (big) {
+    const bool timed = prof && prof->events && *prof->n < prof->cap;
+    if (timed) (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n], s);
+    launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
+    if (timed) {
+      (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n + 1], s);
+      prof->flops[*prof->n] = 2.0 * (double)M * (double)N * (double)K;
+      ++*prof->n;
+    }
+  } else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
   if (splits > 1) {
     const int64_t MN = (int64_t)N * K;
     const int64_t units = (K % 4 == 0) ? MN / 4 : MN;

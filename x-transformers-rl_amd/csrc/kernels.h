@@ -54,8 +54,16 @@ struct GemmArgs {
 int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s);
 // dW[N][K] (+)= dY^T X over M tokens, split-K over workgroups with a fixed-order reduction;
 // db (optional, accumulated) [n - db_n0] += sum_m dY[m][n] for n >= db_n0 (the bias gradient)
+// prof (optional): events recorded around the main GEMM launch when it is the 128x128 kernel
+struct GemmProfile {
+  void** events;
+  double* flops;
+  int cap;
+  int* n;
+};
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
-               float* ws, int64_t ws_floats, hipStream_t s, float* db = nullptr, int db_n0 = 0);
+               float* ws, int64_t ws_floats, hipStream_t s, float* db = nullptr, int db_n0 = 0,
+               const GemmProfile* prof = nullptr);
 int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
              const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
              int K, int act, hipStream_t s);

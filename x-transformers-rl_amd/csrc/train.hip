@@ -460,7 +460,9 @@ int linear_dgrad(const Ctx& c, const float* dY, int ldy, const float* W, float* 
 // dW += dY^T X (and the bias gradient db[n - db_n0] += column sums of dY for n >= db_n0)
 int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float* dW, int M, int N, int K,
           float* db = nullptr, int db_n0 = 0) {
-  return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s, db, db_n0);
+  const GemmProfile prof{c.D->prof_events, c.D->prof_flops, c.D->prof_cap, c.D->prof_n};
+  return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s, db, db_n0,
+                    c.D->prof_events && c.D->prof_n ? &prof : nullptr);
 }
 
 // dst[0:cols] += sum over rows of src (optionally weighted by rw[r * ld_rw] * rw_scale)

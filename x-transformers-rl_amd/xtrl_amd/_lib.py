@@ -80,7 +80,8 @@ class TrainDesc(C.Structure):
                                     'st_final', 'ac_in', 'ewa', 'zp', 'hp', 'z1', 'h1', 'lat_e', 'd_raw', 'd_values',
                                     'd_pred', 'd_done', 'dx', 'dxn', 'dff', 'dproj', 'dog', 'dvfirst', 'dz1', 'dac',
                                     'dzp', 'dewa', 'delta', 'part')]
-                + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer))])
+                + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer)),
+                   ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P)])
 
 
 SIGNATURES = {
