@@ -330,7 +330,149 @@ void run_glds(const char* tag, const float* A, const float* B, float* C, int M, 
   printf("%-28s M=%5d N=%5d K=%5d  %8.1f us  %6.1f TF  err %.1e\n", tag, M, N, K, us, 2.0 * M * N * K / us / 1e6, maxerr);
 }
 
+// ---- "TT" layouts (the weight-gradient GEMM): A given as [K][M], B as [K][N] (contiguous along
+// m / n); both staged with float4 writes into k-major LDS images.  ROT: row k stored rotated by
+// 32 columns when k is odd, so the two half-waves of a fragment read (rows k, k+1) hit disjoint
+// LDS banks.
+template <int ROT, int PADC>
+__global__ __launch_bounds__(256) void k_tt(const float* __restrict__ A, const float* __restrict__ B,
+                                           float* __restrict__ C, int M, int N, int K) {
+  constexpr int BM = 128, BN = 128, BK = 32, NT = 256, ST = BM + PADC;
+  constexpr int F4 = BM * BK / 4 / NT;   // 4 float4 per thread per operand
+  __shared__ __attribute__((aligned(16))) float As[2][BK][ST];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][ST];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  float4 ra[F4], rb[F4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int e = tid + i * NT, r = e / (BM / 4), q = e % (BM / 4);
+      ra[i] = *reinterpret_cast<const float4*>(A + (int64_t)(k0 + r) * M + m0 + 4 * q);
+      rb[i] = *reinterpret_cast<const float4*>(B + (int64_t)(k0 + r) * N + n0 + 4 * q);
+    }
+  };
+  auto col = [&](int k, int c) { return ROT ? ((c + 32 * (k & 1)) & (BM - 1)) : c; };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int e = tid + i * NT, r = e / (BM / 4), q = e % (BM / 4);
+      *reinterpret_cast<float4*>(&As[buf][r][col(r, 4 * q)]) = ra[i];
+      *reinterpret_cast<float4*>(&Bs[buf][r][col(r, 4 * q)]) = rb[i];
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int fi = wm * 64 + (lane & 31), fj = wn * 64 + (lane & 31), fk = lane >> 5;
+  auto compute = [&](int cur) {
+    float av[2][2], bv[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      av[0][i] = As[cur][fk][col(fk, fi + 32 * i)];
+      bv[0][i] = Bs[cur][fk][col(fk, fj + 32 * i)];
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int pb = st & 1;
+      if (st + 1 < 16) {
+        const int k = fk + 2 * st + 2;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          av[pb ^ 1][i] = As[cur][k][col(k, fi + 32 * i)];
+          bv[pb ^ 1][i] = Bs[cur][k][col(k, fj + 32 * i)];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[pb][i], bv[pb][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  const int nk = K / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load((kt + 1) * BK);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(kt & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) store((kt & 1) ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        C[(int64_t)m * N + n] = acc[i][j][r];
+      }
+  }
+}
+
+template <int ROT, int PADC>
+void run_tt(const char* tag, int M, int N, int K) {
+  std::vector<float> hA((size_t)K * M), hB((size_t)K * N);
+  srand(2);
+  for (auto& x : hA) x = (float)rand() / RAND_MAX - 0.5f;
+  for (auto& x : hB) x = (float)rand() / RAND_MAX - 0.5f;
+  float *A, *B, *C;
+  CK(hipMalloc(&A, hA.size() * 4));
+  CK(hipMalloc(&B, hB.size() * 4));
+  CK(hipMalloc(&C, (size_t)M * N * 4));
+  CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(B, hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
+  dim3 grid(N / 128, M / 128);
+  auto launch = [&] { hipLaunchKernelGGL((k_tt<ROT, PADC>), grid, dim3(256), 0, 0, A, B, C, M, N, K); };
+  launch();
+  CK(hipDeviceSynchronize());
+  std::vector<float> hC((size_t)M * N);
+  CK(hipMemcpy(hC.data(), C, hC.size() * 4, hipMemcpyDeviceToHost));
+  double maxerr = 0;
+  for (int t = 0; t < 32; ++t) {
+    const int m = (t * 7919) % M, n = (t * 104729) % N;
+    double s = 0;
+    for (int k = 0; k < K; ++k) s += (double)hA[(size_t)k * M + m] * hB[(size_t)k * N + n];
+    maxerr = fmax(maxerr, fabs(s - hC[(size_t)m * N + n]) / (1 + fabs(s)));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < 20; ++i) launch();
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / 20;
+  printf("%-28s M=%5d N=%5d K=%5d  %8.1f us  %6.1f TF  err %.1e\n", tag, M, N, K, us, 2.0 * M * N * K / us / 1e6, maxerr);
+  CK(hipFree(A));
+  CK(hipFree(B));
+  CK(hipFree(C));
+}
+
 int main() {
+  // weight-gradient-like: M = 1024 out, N = 256 in, K = 512 tokens per split (one workgroup round)
+  for (int rep = 0; rep < 1; ++rep) {
+    run_tt<0, 4>("TT pad4", 1024, 256, 16384);
+    run_tt<1, 4>("TT pad4 rot32", 1024, 256, 16384);
+    run_tt<1, 0>("TT pad0 rot32", 1024, 256, 16384);
+    run_tt<0, 32>("TT pad32", 1024, 256, 16384);
+    run_tt<0, 4>("TT pad4 4k", 4096, 4096, 4096);
+    run_tt<1, 0>("TT pad0 rot32 4k", 4096, 4096, 4096);
+  }
+  if (getenv("LAB_TT_ONLY")) return 0;
   const int shapes[][3] = {{16384, 1024, 256}, {16384, 256, 1024}, {16384, 512, 512}, {4096, 4096, 4096}};
   for (auto& sh : shapes) {
     const int M = sh[0], N = sh[1], K = sh[2];

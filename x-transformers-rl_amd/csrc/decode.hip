@@ -6,28 +6,24 @@
 //   k_embed        RSNorm eval of [state, prev_reward] (xtrl.py:1254-1259, 591), project_in +
 //                  action embedding + reward embedding (xtrl.py:492-503), to_state_embed;
 //                  writes the raw state into the trajectory (Memory.state, xtrl.py:1315)
-//   per layer      LN -> [q|k|v|gate|mix] GEMM (gemm.hip, LN prologue)
+//   per layer      LN -> [q|k|v|gate|mix] GEMM (gemm.hip)
 //                  k_attn_decode: value-residual mix, rotary, KV append at t, softmax(q k^T) v
 //                  over positions 0..t, value gate        (x-transformers Attention, cached)
 //                  out-proj GEMM + residual, LN -> FF1 GELU GEMM, FF2 GEMM + residual
 //   final LN       into ac_in[:, 0:d]; heads: [actor|critic] hidden GEMM (SiLU), logits GEMMs
-//                  (critic logits straight into traj_values[:, t, :])
+//                  (critic logits straight into traj_values[:, t, :] of live envs)
 //   k_sample       softmax -> Categorical -> inverse-CDF sample on Philox uniforms, log_prob
-//                  (xtrl.py:1280-1289; torch Categorical(probs) semantics)
-//   k_sim_step     synthetic LunarLander-shaped Sim (philox.h): reward, termination, next state,
-//                  alive mask, episode length, cumulative reward (xtrl.py:1297-1351)
+//                  (xtrl.py:1280-1289; torch Categorical(probs) semantics), then the synthetic
+//                  LunarLander-shaped Sim step (philox.h): reward, termination, next state, alive
+//                  mask, episode length, cumulative reward (xtrl.py:1297-1351)
 //
 // Layouts in HBM: activations are [E][·] row-major; KV caches [E][H][Tmax][dh] so one (env, head)
 // streams a contiguous Tmax*dh block; trajectories [E][Tmax][·] so the learner reads whole
 // episodes contiguously.
-#include "common.h"
+#include "kernels.h"
 #include "philox.h"
 
 namespace xtrl {
-int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
-             const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
-             int K, int act, hipStream_t s);
-int layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, hipStream_t s);
 
 namespace {
 
@@ -180,38 +176,55 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
 // ---------------------------------------------------------------------------------------------
 // sampling (one thread per env)
 // ---------------------------------------------------------------------------------------------
+// sampling (xtrl.py:197-277) and, for the device Sim, its step (one thread per live env).  The
+// value logits were written straight into the trajectory by the critic GEMM (masked to live envs).
+__device__ __forceinline__ float reward_factor(int a) { return (float)(1.0 + 0.1 * (double)a); }
+
+__device__ __forceinline__ void sim_step_env(const XtrlDecodeDesc& D, int e, int t, const XtrlRngState& R) {
+  const uint32_t ep = (uint32_t)D.episode_of_slot[e];
+  const float z = rng_normal(R.seed, R.update, ep, t, FIELD_REWARD, 0);
+  const float reward = (D.sim_mode == 1 && !D.continuous) ? z * reward_factor(D.prev_action[e]) : z;
+  bool term = false;
+  if (D.sim_mode == 1 && D.hazard_log2 > 0)
+    term = (rng_u32(R.seed, R.update, ep, t, FIELD_TERM, 0) & ((1u << D.hazard_log2) - 1u)) == 0u;
+  D.traj_rewards[(int64_t)e * D.Tmax + t] = reward;
+  D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
+  D.prev_reward[e] = reward;
+  D.cum_reward[e] += (double)reward;
+  D.lens[e] = t + 1;
+  for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
+  if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
+}
+
 __global__ void k_sample(const XtrlDecodeDesc D, int t) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= D.E || !D.alive[e]) return;
   const XtrlRngState R = *D.rng;
   const uint32_t slot = R.slot_offset + e;
   const int A = D.A;
-  // Memory.value (xtrl.py:1315): critic logits of live episodes only; padding stays zero
-  for (int k = 0; k < D.B; ++k) D.traj_values[((int64_t)e * D.Tmax + t) * D.B + k] = D.vals[(int64_t)e * D.B + k];
   const float* lg = D.logits + (int64_t)e * (D.continuous ? 2 * A : A);
   if (!D.continuous) {
-    float p[64];
+    // softmax (xtrl.py:203), Categorical(probs) re-normalisation, inverse CDF on the supplied
+    // uniform; probabilities recomputed on the fly (no per-thread array)
     float mx = -INFINITY;
     for (int i = 0; i < A; ++i) mx = fmaxf(mx, lg[i]);
     float s = 0.f;
-    for (int i = 0; i < A; ++i) {
-      p[i] = expf(lg[i] - mx);
-      s += p[i];
-    }
+    for (int i = 0; i < A; ++i) s += expf(lg[i] - mx);
     float s2 = 0.f;
-    for (int i = 0; i < A; ++i) {
-      p[i] = p[i] / s;   // softmax (xtrl.py:203)
-      s2 += p[i];
-    }
-    for (int i = 0; i < A; ++i) p[i] = p[i] / s2;   // Categorical(probs) re-normalisation
+    for (int i = 0; i < A; ++i) s2 += expf(lg[i] - mx) / s;
     const float u = rng_uniform(R.seed, R.update, slot, t, FIELD_SAMPLE, 0);
     int a = 0;
-    float cdf = 0.f;
-    for (int i = 0; i < A - 1; ++i) {
-      cdf += p[i];
-      a += (u >= cdf) ? 1 : 0;
+    float cdf = 0.f, pa = 0.f;
+    for (int i = 0; i < A; ++i) {
+      const float p = (expf(lg[i] - mx) / s) / s2;
+      if (i < A - 1) {
+        cdf += p;
+        a += (u >= cdf) ? 1 : 0;
+      }
     }
-    const float pa = fminf(fmaxf(p[a], F32_EPS), 1.f - F32_EPS);
+    for (int i = 0; i < A; ++i)
+      if (i == a) pa = (expf(lg[i] - mx) / s) / s2;
+    pa = fminf(fmaxf(pa, F32_EPS), 1.f - F32_EPS);
     D.traj_actions[(int64_t)e * D.Tmax + t] = a;
     D.traj_logp[(int64_t)e * D.Tmax + t] = logf(pa);
     D.prev_action[e] = a;
@@ -231,30 +244,7 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
       D.prev_action_f[e * A + i] = s;
     }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// synthetic Sim (one thread per env)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float reward_factor(int a) { return (float)(1.0 + 0.1 * (double)a); }
-
-__global__ void k_sim_step(const XtrlDecodeDesc D, int t) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D.E || !D.alive[e]) return;
-  const XtrlRngState R = *D.rng;
-  const uint32_t ep = (uint32_t)D.episode_of_slot[e];
-  const float z = rng_normal(R.seed, R.update, ep, t, FIELD_REWARD, 0);
-  const float reward = (D.sim_mode == 1 && !D.continuous) ? z * reward_factor(D.prev_action[e]) : z;
-  bool term = false;
-  if (D.sim_mode == 1 && D.hazard_log2 > 0)
-    term = (rng_u32(R.seed, R.update, ep, t, FIELD_TERM, 0) & ((1u << D.hazard_log2) - 1u)) == 0u;
-  D.traj_rewards[(int64_t)e * D.Tmax + t] = reward;
-  D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
-  D.prev_reward[e] = reward;
-  D.cum_reward[e] += (double)reward;
-  D.lens[e] = t + 1;
-  for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
-  if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
+  if (D.sim_mode >= 0) sim_step_env(D, e, t, R);
 }
 
 __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
@@ -362,15 +352,15 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   if ((rc = gemm_f32(D->hff, 4 * d, D->w_a2, 2 * d, D->b_a2, nullptr, nullptr, 0, D->logits, n_act, nullptr, 0, E,
                      n_act, 2 * d, XTRL_ACT_NONE, s)))
     return rc;
-  if ((rc = gemm_f32(D->hff + 2 * d, 4 * d, D->w_c2, 2 * d, D->b_c2, nullptr, nullptr, 0, D->vals, D->B, nullptr, 0,
-                     E, D->B, 2 * d, XTRL_ACT_NONE, s)))
-    return rc;
+  {   // critic bins straight into the trajectory row t (Memory.value, xtrl.py:1315), live envs only
+    GemmArgs g;
+    g.A = D->hff + 2 * d; g.lda = 4 * d; g.B = D->w_c2; g.ldb = 2 * d; g.bias = D->b_c2;
+    g.C = D->traj_values + (int64_t)t * D->B; g.ldc = D->Tmax * D->B; g.M = E; g.N = D->B; g.K = 2 * d;
+    g.row_mask = D->alive;
+    if ((rc = gemm_run(g, 0, 0, EPI_NONE, s))) return rc;
+  }
   hipLaunchKernelGGL(k_sample, dim3((E + 255) / 256), dim3(256), 0, s, *D, t);
   XTRL_LAUNCHED("sample");
-  if (D->sim_mode >= 0) {
-    hipLaunchKernelGGL(k_sim_step, dim3((E + 255) / 256), dim3(256), 0, s, *D, t);
-    XTRL_LAUNCHED("sim_step");
-  }
   return XTRL_OK;
 }
 

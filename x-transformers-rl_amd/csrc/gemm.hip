@@ -32,14 +32,23 @@ namespace {
 template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
 __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN, BK = 32 * WK, NT = 64 * WM * WN * WK;
-  // k-major LDS images; row stride +1 for transposed staging writes ("N" operand), +4 (16-byte rows,
-  // ds_write_b128) when the global rows are already k-major ("T" operand)
-  constexpr int AST = TA ? BM + 4 : BM + 1, BST = TB ? BN + 4 : BN + 1;
+  // k-major LDS images [buf][k][m]: +1 pad ("N", transposed scalar staging writes), +4 (16-byte
+  // rows, "T").  SWZ (kept for experiments, off): row stride = 32 mod 64 banks so the two
+  // half-waves of a fragment read (rows k, k+1) use disjoint banks, plus an XOR-by-8 column
+  // swizzle for conflict-free transposed writes.  Isolated TT GEMM at 4096^3 +22 %, but the C3
+  // update measured 2 % slower with it (tools/gemm_lab.hip, A/B bench), so it is disabled.
+  constexpr bool SWZ = false && (WK == 1 && BM >= 64 && BN >= 64);
+  constexpr int AST = SWZ ? BM + 32 : (TA ? BM + 4 : BM + 1), BST = SWZ ? BN + 32 : (TB ? BN + 4 : BN + 1);
   constexpr int A_F4 = BM * BK / 4 / NT, B_F4 = BN * BK / 4 / NT;   // float4 loads per thread per slab
   static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small for the thread count");
-  __shared__ __attribute__((aligned(16))) float As[2][BK][AST];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BST];
-  __shared__ float row_mean[LN ? BM : 1], row_rstd[LN ? BM : 1];
+  // one static LDS block carved exactly (128 x 128 SWZ tiles need 80 KiB: two workgroups per CU)
+  constexpr int SMEM = 2 * BK * AST + 2 * BK * BST + (LN ? 2 * BM : 0);
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  float(*As)[BK][AST] = reinterpret_cast<float(*)[BK][AST]>(smem);
+  float(*Bs)[BK][BST] = reinterpret_cast<float(*)[BK][BST]>(smem + 2 * BK * AST);
+  float* row_mean = smem + 2 * BK * AST + 2 * BK * BST;
+  float* row_rstd = row_mean + BM;
+  auto sw = [](int k, int m) { return SWZ ? (m ^ (8 * ((k >> 2) & 7))) : m; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
@@ -197,13 +206,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TA) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        As[buf][4 * q + 0][r] = ra[i].x;
-        As[buf][4 * q + 1][r] = ra[i].y;
-        As[buf][4 * q + 2][r] = ra[i].z;
-        As[buf][4 * q + 3][r] = ra[i].w;
+        As[buf][4 * q + 0][sw(4 * q + 0, r)] = ra[i].x;
+        As[buf][4 * q + 1][sw(4 * q + 1, r)] = ra[i].y;
+        As[buf][4 * q + 2][sw(4 * q + 2, r)] = ra[i].z;
+        As[buf][4 * q + 3][sw(4 * q + 3, r)] = ra[i].w;
       } else {
         const int r = e / (BM / 4), q = e % (BM / 4);
-        *reinterpret_cast<float4*>(&As[buf][r][4 * q]) = ra[i];
+        *reinterpret_cast<float4*>(&As[buf][r][sw(r, 4 * q)]) = ra[i];
       }
     }
 #pragma unroll
@@ -211,13 +220,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TB) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        Bs[buf][4 * q + 0][r] = rb[i].x;
-        Bs[buf][4 * q + 1][r] = rb[i].y;
-        Bs[buf][4 * q + 2][r] = rb[i].z;
-        Bs[buf][4 * q + 3][r] = rb[i].w;
+        Bs[buf][4 * q + 0][sw(4 * q + 0, r)] = rb[i].x;
+        Bs[buf][4 * q + 1][sw(4 * q + 1, r)] = rb[i].y;
+        Bs[buf][4 * q + 2][sw(4 * q + 2, r)] = rb[i].z;
+        Bs[buf][4 * q + 3][sw(4 * q + 3, r)] = rb[i].w;
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        *reinterpret_cast<float4*>(&Bs[buf][r][4 * q]) = rb[i];
+        *reinterpret_cast<float4*>(&Bs[buf][r][sw(r, 4 * q)]) = rb[i];
       }
     }
   };
@@ -237,17 +246,17 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   auto compute = [&](int cur) {
     float av[2][TM], bv[2][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) av[0][i] = As[cur][fk][fi + 32 * i];
+    for (int i = 0; i < TM; ++i) av[0][i] = As[cur][fk][sw(fk, fi + 32 * i)];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bv[0][j] = Bs[cur][fk][fj + 32 * j];
+    for (int j = 0; j < TN; ++j) bv[0][j] = Bs[cur][fk][sw(fk, fj + 32 * j)];
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
       const int pb = st & 1;
       if (st + 1 < 16) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) av[pb ^ 1][i] = As[cur][fk + 2 * st + 2][fi + 32 * i];
+        for (int i = 0; i < TM; ++i) av[pb ^ 1][i] = As[cur][fk + 2 * st + 2][sw(fk + 2 * st + 2, fi + 32 * i)];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bv[pb ^ 1][j] = Bs[cur][fk + 2 * st + 2][fj + 32 * j];
+        for (int j = 0; j < TN; ++j) bv[pb ^ 1][j] = Bs[cur][fk + 2 * st + 2][sw(fk + 2 * st + 2, fj + 32 * j)];
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   auto rs_slab = [&](int cur) {
     if (do_rs && tid < BM) {
 #pragma unroll 8
-      for (int k = 0; k < BK; ++k) rs_acc += As[cur][k][tid];
+      for (int k = 0; k < BK; ++k) rs_acc += As[cur][k][sw(k, tid)];
     }
   };
   load_slab(0, true);
@@ -399,7 +408,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
           }
           if constexpr (RES) v = v + rr[r];
           if (acc_c) v = a.beta * old[r] + v;
-          if (nok && m < M) {
+          if (nok && m < M && (!a.row_mask || a.row_mask[m])) {
             C[(int64_t)m * a.ldc + n] = v;
             if constexpr (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE)
               a.aux_out[(int64_t)m * a.ld_aux_out + n] = aux_o;

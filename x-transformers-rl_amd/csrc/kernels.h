@@ -45,6 +45,7 @@ struct GemmArgs {
   uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT) word (m & 3)
   uint32_t drop_thresh = 0;       //   >= drop_thresh (0: no dropout)
   float inv_keep = 1.f;
+  const uint8_t* row_mask = nullptr;   // rows m with row_mask[m] == 0 are not stored (dead envs)
   float* rowsum = nullptr;        // += row sums of A (rows >= rowsum_m0, at rowsum[m - rowsum_m0]) —
   int rowsum_m0 = 0;              //   the bias gradient when A = dY^T; with split-K the per-split
   float* rowsum_ws = nullptr;     //   sums go to rowsum_ws[z][M] and the reduce kernel adds them

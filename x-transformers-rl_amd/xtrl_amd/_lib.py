@@ -12,7 +12,7 @@ from pathlib import Path
 
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
-LIB_PATH = Path(__file__).resolve().parent / 'libxtrl_hip.so'
+LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
 ABI_VERSION = 2
 
 P = C.c_void_p
