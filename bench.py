@@ -268,6 +268,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--no-loss-delta', action='store_true')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -346,7 +347,7 @@ def main():
     cpu = None
     if rank == 0:
         try:
-            loss_delta = ppo_loss_delta(learner, env, cfg)
+            loss_delta = None if args.no_loss_delta else ppo_loss_delta(learner, env, cfg)
         except Exception as e:   # reported, never hidden
             loss_delta = dict(error=repr(e))
         if not args.no_cpu_baseline:
