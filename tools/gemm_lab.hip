@@ -486,19 +486,15 @@ int main() {
     CK(hipMalloc(&C, (size_t)M * N * 4));
     CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(B, hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
-    run_glds<2>("glds 128x128x32 ns2", A, B, C, M, N, K, hA, hB);
-    run_glds<3>("glds 128x128x32 ns3", A, B, C, M, N, K, hA, hB);
-    run_glds<4>("glds 128x128x32 ns4", A, B, C, M, N, K, hA, hB);
-    run<128, 128, 32, 2, 2, 2>("128x128x32 4w dbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 128, 64, 2, 2, 1>("128x128x64 4w sbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 128, 32, 2, 2, 1>("128x128x32 4w sbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 128, 64, 2, 2, 2>("128x128x64 4w dbuf", A, B, C, M, N, K, hA, hB);
-    run<256, 128, 32, 4, 2, 2>("256x128x32 8w dbuf", A, B, C, M, N, K, hA, hB);
-    run<256, 128, 32, 2, 2, 1>("256x128x32 4w(128x64) sbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 256, 32, 2, 4, 2>("128x256x32 8w dbuf", A, B, C, M, N, K, hA, hB);
-    run<64, 128, 32, 1, 2, 2>("64x128x32 2w dbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 64, 32, 2, 1, 2>("128x64x32 2w dbuf", A, B, C, M, N, K, hA, hB);
-    run<128, 64, 64, 2, 1, 2>("128x64x64 2w dbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 128, 32, 2, 2, 2>("128x128 4w(64x64) dbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 128, 32, 2, 2, 1>("128x128 4w(64x64) sbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 128, 32, 1, 2, 2>("128x128 2w(128x64) dbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 128, 32, 2, 1, 2>("128x128 2w(64x128) dbuf", A, B, C, M, N, K, hA, hB);
+    run<256, 128, 32, 2, 2, 1>("256x128 4w(128x64) sbuf", A, B, C, M, N, K, hA, hB);
+    run<256, 128, 32, 2, 2, 2>("256x128 4w(128x64) dbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 256, 32, 2, 2, 1>("128x256 4w(64x128) sbuf", A, B, C, M, N, K, hA, hB);
+    run<256, 256, 32, 2, 2, 1>("256x256 4w(128x128) sbuf", A, B, C, M, N, K, hA, hB);
+    run<128, 128, 16, 2, 2, 2>("128x128x16 4w dbuf", A, B, C, M, N, K, hA, hB);
     CK(hipFree(A));
     CK(hipFree(B));
     CK(hipFree(C));
