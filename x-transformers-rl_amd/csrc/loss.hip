@@ -193,8 +193,9 @@ __device__ __forceinline__ bool critic_zeroed(float v, float ret, float vold, fl
 __global__ __launch_bounds__(1024) void k_loss_reduce(const XtrlLossDesc D) {
   __shared__ double sh[16];
   const int N = D.b * D.n;
-  // pass 1: masked counts and sums
+  // pass 1: masked counts and sums (4 tokens per thread in flight)
   double n_mask = 0, s_adv = 0, s_ceu = 0, s_cec = 0, s_wm = 0, n_wm = 0, s_bce = 0;
+#pragma unroll 4
   for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
     const int bi = tk / D.n, ti = tk - bi * D.n;
     const float* tok = D.tok + (int64_t)tk * NT;
@@ -221,6 +222,7 @@ __global__ __launch_bounds__(1024) void k_loss_reduce(const XtrlLossDesc D) {
   const float adv_mean = (float)(s_adv / n_mask);
   // pass 2: unbiased variance of the masked advantages
   double s_var = 0;
+#pragma unroll 4
   for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
     const int bi = tk / D.n, ti = tk - bi * D.n;
     if (ti < D.lens[bi]) {
@@ -233,37 +235,61 @@ __global__ __launch_bounds__(1024) void k_loss_reduce(const XtrlLossDesc D) {
   const float den = sqrtf(fmaxf(var, 1e-5f));
   const float L = (float)(s_ceu / N), Lc = (float)(s_cec / N);
   const float lo = 1.f - D.eps_clip, hi = 1.f + D.eps_clip;
-  // pass 3: per-token actor / critic terms
+  // pass 3: per-token actor / critic terms; the inputs of four tokens are read before their T_ACT
+  // stores (which the compiler cannot prove disjoint), so four tokens' loads are in flight
   double s_actor_all = 0, s_critic_all = 0, s_ac = 0, k_crit = 0;
-  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
-    const int bi = tk / D.n, ti = tk - bi * D.n;
-    float* tok = D.tok + (int64_t)tk * NT;
-    const bool mask = ti < D.lens[bi];
-    const float advn = (tok[T_ADV] - adv_mean) / den;
-    float actor = 0.f;
-    if (!D.continuous) {
-      const float r = expf(tok[T_LP] - D.old_logp[tk]);
-      const float rc = fminf(fmaxf(r, lo), hi);
-      actor = -fminf(r * advn, rc * advn) - D.entropy_weight * tok[T_ENT];
-    } else {
-      for (int i = 0; i < D.A; ++i) {
-        ContTerms C;
-        cont_terms(D.raw_actions + (int64_t)tk * 2 * D.A, D.actions_f[(int64_t)tk * D.A + i], i, D.squash, C);
-        const float r = expf(C.lp - D.old_logp[(int64_t)tk * D.A + i]);
-        const float rc = fminf(fmaxf(r, lo), hi);
-        actor += -fminf(r * advn, rc * advn) - D.entropy_weight * C.ent;
-      }
+  constexpr int U = 4;
+  for (int base = 0; base < N; base += U * blockDim.x) {
+    float adv[U], lp[U], ent[U], v[U], vold[U], ceu[U], cec[U], olp[U], ret[U];
+    bool mask[U], ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tk = base + u * blockDim.x + threadIdx.x;
+      ok[u] = tk < N;
+      const int tc = ok[u] ? tk : 0;
+      const int bi = tc / D.n, ti = tc - bi * D.n;
+      const float* tok = D.tok + (int64_t)tc * NT;
+      mask[u] = ti < D.lens[bi];
+      adv[u] = tok[T_ADV];
+      lp[u] = tok[T_LP];
+      ent[u] = tok[T_ENT];
+      v[u] = tok[T_V];
+      vold[u] = tok[T_VOLD];
+      ceu[u] = tok[T_CEU];
+      cec[u] = tok[T_CEC];
+      olp[u] = D.continuous ? 0.f : D.old_logp[tc];
+      ret[u] = D.returns[tc];
     }
-    const bool zero = critic_zeroed(tok[T_V], D.returns[tk], tok[T_VOLD], D.value_clip);
-    float critic;
-    if (D.hl_reduction_mean) critic = zero ? 0.f : fminf(L, Lc);
-    else critic = zero ? 0.f : fminf(tok[T_CEU], tok[T_CEC]);
-    tok[T_ACT] = actor;
-    s_actor_all += actor;
-    s_critic_all += critic;
-    if (mask) {
-      s_ac += actor * D.w_actor + critic * D.w_critic;
-      if (!zero) k_crit += 1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const int tk = base + u * blockDim.x + threadIdx.x;
+      const float advn = (adv[u] - adv_mean) / den;
+      float actor = 0.f;
+      if (!D.continuous) {
+        const float r = expf(lp[u] - olp[u]);
+        const float rc = fminf(fmaxf(r, lo), hi);
+        actor = -fminf(r * advn, rc * advn) - D.entropy_weight * ent[u];
+      } else {
+        for (int i = 0; i < D.A; ++i) {
+          ContTerms C;
+          cont_terms(D.raw_actions + (int64_t)tk * 2 * D.A, D.actions_f[(int64_t)tk * D.A + i], i, D.squash, C);
+          const float r = expf(C.lp - D.old_logp[(int64_t)tk * D.A + i]);
+          const float rc = fminf(fmaxf(r, lo), hi);
+          actor += -fminf(r * advn, rc * advn) - D.entropy_weight * C.ent;
+        }
+      }
+      const bool zero = critic_zeroed(v[u], ret[u], vold[u], D.value_clip);
+      float critic;
+      if (D.hl_reduction_mean) critic = zero ? 0.f : fminf(L, Lc);
+      else critic = zero ? 0.f : fminf(ceu[u], cec[u]);
+      D.tok[(int64_t)tk * NT + T_ACT] = actor;
+      s_actor_all += actor;
+      s_critic_all += critic;
+      if (mask[u]) {
+        s_ac += actor * D.w_actor + critic * D.w_critic;
+        if (!zero) k_crit += 1;
+      }
     }
   }
   s_actor_all = block_sum(s_actor_all, sh);
