@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 2
+#define XTRL_ABI_VERSION 3
 
 int xtrl_abi_version(void);
 const char* xtrl_last_error(void);
@@ -285,6 +285,48 @@ int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
 int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream);
 /* the feed-forward dropout keep mask of layer `layer` as uint8 [M][N] (tests / reference mode) */
 int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Minibatch assembly for the learn step (Agent.learn data prep, xtrl.py:816-924): gathers the
+ * minibatch's episodes (idx) from the device trajectory, shifts actions / rewards right by one
+ * step (pad_at_dim, xtrl.py:127-138, fill -1 for discrete actions), normalises [state, previous
+ * reward] with the RSNorm statistics (xtrl.py:591), and produces the masked column mean of the
+ * normalised rows that feeds the RSNorm copy update (xtrl.py:598-610, 1005).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct XtrlBatchDesc {
+  int N, Tmax, n, b, S, A, B, continuous;
+  /* trajectory [N][Tmax][.] (rollout buffers) and per-update tensors */
+  const float* states;        /* [N][Tmax][S] */
+  const int32_t* actions;     /* [N][Tmax] discrete */
+  const float* actions_f;     /* [N][Tmax][A] continuous */
+  const float* rewards;       /* [N][Tmax] */
+  const float* logp;          /* [N][Tmax] (continuous [N][Tmax][A]) */
+  const uint8_t* bounds;      /* [N][Tmax] */
+  const float* values;        /* [N][Tmax][B] */
+  const float* returns;       /* [N][n] */
+  const int32_t* lens;        /* [N] */
+  const int64_t* idx;         /* [b] episode indices of the minibatch */
+  const float* rs_mean;       /* [S + 1] normalisation statistics */
+  const float* rs_var;
+  /* outputs [b][n][.] */
+  float* swr;                 /* [b][n][S + 1] */
+  int32_t* prev_action;       /* [b][n] discrete (-1 at step 0) */
+  int32_t* action;
+  float* prev_action_f;       /* [b][n][A] continuous (0 at step 0) */
+  float* action_f;
+  float* old_logp;            /* [b][n] (continuous [b][n][A]) */
+  float* mb_returns;          /* [b][n] */
+  float* old_values;          /* [b][n][B] */
+  uint8_t* dones;             /* [b][n] */
+  int32_t* mb_lens;           /* [b] */
+  float* rs_part;             /* workspace >= 64 * (S + 2) floats */
+  float* rs_m;                /* [S + 1] masked mean of swr over the valid steps */
+} XtrlBatchDesc;
+
+int xtrl_minibatch_gather(const XtrlBatchDesc* desc, void* stream);
+/* RSNorm running update with a batch mean m (xtrl.py:602-610): mean += (m - mean) / t;
+ * var = (t - 1) / t * (var + (m - mean_old)^2 / t) */
+int xtrl_rsnorm_update(float* mean, float* var, const float* m, int D, int t, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused PPO / critic / world-model / done loss   (xtrl.py:398-477 losses, :939-978 combination)

@@ -152,3 +152,38 @@ def test_flat_layout_aligns_gemm_weights():
             assert a % 4 == 0, (name, a)
     flat.span(['to_pred.0.weight', 'to_pred_done.0.weight'])
     flat.span(['action_head.0.weight', 'critic_head.0.weight'])
+
+
+def test_full_checkpoint_roundtrip(tmp_path):
+    """save_checkpoint / load_checkpoint restore the whole training state (model with reference
+    key names, optimiser moments, EMA, RSNorm, gene pool, counters); a reference-format
+    {'model': state_dict} file still loads as weights only."""
+    from xtrl_amd import Learner
+    torch.manual_seed(0)
+    kw = dict(world_model=dict(attn_dim_head=16, heads=4, depth=1), evolutionary=True,
+              latent_gene_pool=dict(dim=8, num_genes_per_island=3, num_selected=2, tournament_size=2),
+              num_episodes_per_update=4, batch_size=2, accelerate_kwargs=dict(device='cpu'),
+              agent_kwargs=dict(hidden_dim=16, save_path=str(tmp_path / 'ppo.pt')), use_graph=False)
+    a = Learner(5, 2, (-1., 1.), **kw).agent
+    with torch.no_grad():
+        a.flat.flat.normal_()
+        a.opt_m.normal_()
+        a.opt_v.uniform_()
+        a.ema_flat.normal_()
+        a.rs_mean.normal_()
+        a.rs_var.uniform_()
+        a.gene_pool.genes.normal_()
+    a.opt_first, a.ema_step, a.ema_initted, a.rs_step, a.step, a.gene_pool.step = False, 37, True, 9, 4, 2
+    a.save_checkpoint()
+    torch.manual_seed(1)
+    b = Learner(5, 2, (-1., 1.), **kw).agent
+    b.load_checkpoint()
+    for x, y in ((a.flat.flat, b.flat.flat), (a.opt_m, b.opt_m), (a.opt_v, b.opt_v), (a.ema_flat, b.ema_flat),
+                 (a.rs_mean, b.rs_mean), (a.rs_var, b.rs_var), (a.gene_pool.genes, b.gene_pool.genes)):
+        assert torch.equal(x, y)
+    assert (b.opt_first, b.ema_step, b.ema_initted, b.rs_step, b.step, b.gene_pool.step) == (False, 37, True, 9, 4, 2)
+    # reference format: weights only (xtrl.py:792-806)
+    a.save()
+    c = Learner(5, 2, (-1., 1.), **kw).agent
+    c.load_checkpoint()
+    assert torch.equal(c.flat.flat, a.flat.flat) and c.step == 0

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -84,6 +84,14 @@ class TrainDesc(C.Structure):
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P)])
 
 
+class BatchDesc(C.Structure):
+    _fields_ = ([(n, I32) for n in ('N', 'Tmax', 'n', 'b', 'S', 'A', 'B', 'continuous')]
+                + [(n, P) for n in ('states', 'actions', 'actions_f', 'rewards', 'logp', 'bounds', 'values', 'returns',
+                                    'lens', 'idx', 'rs_mean', 'rs_var', 'swr', 'prev_action', 'action',
+                                    'prev_action_f', 'action_f', 'old_logp', 'mb_returns', 'old_values', 'dones',
+                                    'mb_lens', 'rs_part', 'rs_m')])
+
+
 SIGNATURES = {
     'xtrl_abi_version': (I32, []),
     'xtrl_last_error': (C.c_char_p, []),
@@ -108,6 +116,8 @@ SIGNATURES = {
     'xtrl_train_forward': (I32, [C.POINTER(TrainDesc), P]),
     'xtrl_train_backward': (I32, [C.POINTER(TrainDesc), P]),
     'xtrl_ff_dropout_mask': (I32, [P, I32, I32, F32, U64, U32, P]),
+    'xtrl_minibatch_gather': (I32, [C.POINTER(BatchDesc), P]),
+    'xtrl_rsnorm_update': (I32, [P, P, P, I32, I32, P]),
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
 }

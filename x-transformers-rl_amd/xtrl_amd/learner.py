@@ -37,6 +37,7 @@ from .evolution import LatentGenePool, evolve_seed
 from .model import ModelConfig, WorldModelActorCritic
 from .params import FlatParams
 from .rollout import SIM_HOST, SIM_LANDER, SIM_README, RolloutEngine
+from .train import rsnorm_update
 
 
 def epoch_permutation(seed, update, epoch, n):
@@ -171,6 +172,52 @@ class Agent(nn.Module):
             for k, v in data['model'].items():
                 self.model.state_dict()[k].copy_(v)
 
+    # ---- full training state (improves on the reference, which saves the model only) ----------------
+    def state_dict_full(self):
+        """Everything needed to resume bit-for-bit: model (reference key names), the AdoptAtan2
+        moments and regen anchor, the EMA weights and schedule, RSNorm statistics, the gene pool,
+        the update counter and seed."""
+        out = dict(model=self.model.state_dict(), format='xtrl_amd/1',
+                   opt_m=self.opt_m, opt_v=self.opt_v, opt_first=torch.tensor(int(self.opt_first)),
+                   ema_flat=self.ema_flat, ema_step=torch.tensor(self.ema_step),
+                   ema_initted=torch.tensor(int(self.ema_initted)), rs_mean=self.rs_mean, rs_var=self.rs_var,
+                   rs_step=torch.tensor(self.rs_step), step=torch.tensor(self.step), seed=torch.tensor(self.seed))
+        if self.opt_p_init is not None:
+            out['opt_p_init'] = self.opt_p_init
+        if self.gene_pool is not None:
+            out.update(genes=self.gene_pool.genes, gene_step=torch.tensor(self.gene_pool.step))
+        return out
+
+    def save_checkpoint(self, path=None):
+        if not self.accelerator.is_main_process:
+            return
+        torch.save({k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
+                    for k, v in self.state_dict_full().items()}, str(path or self.save_path))
+
+    def load_checkpoint(self, path=None):
+        data = torch.load(str(path or self.save_path), weights_only=True, map_location='cpu')
+        dev = self.device
+        with torch.no_grad():
+            for k, v in data['model'].items():
+                self.model.state_dict()[k].copy_(v)
+            if 'opt_m' not in data:    # a reference-format checkpoint: weights only
+                return
+            self.opt_m.copy_(data['opt_m'])
+            self.opt_v.copy_(data['opt_v'])
+            if self.opt_p_init is not None and 'opt_p_init' in data:
+                self.opt_p_init.copy_(data['opt_p_init'])
+            self.opt_first = bool(int(data['opt_first']))
+            self.ema_flat.copy_(data['ema_flat'].to(dev))
+            self.ema_step, self.ema_initted = int(data['ema_step']), bool(int(data['ema_initted']))
+            self.rs_mean = data['rs_mean'].to(dev).clone()
+            self.rs_var = data['rs_var'].to(dev).clone()
+            self.rs_step, self.step, self.seed = int(data['rs_step']), int(data['step']), int(data['seed'])
+            if self.gene_pool is not None and 'genes' in data:
+                self.gene_pool.genes = data['genes'].clone()
+                self.gene_pool.step = int(data['gene_step'])
+                self._genes_dev = None
+        self._deploy = None
+
     # ---- genes ------------------------------------------------------------------------------------
     def latent(self, gene_ids):
         return F.normalize(self.genes_device()[gene_ids], dim=-1)
@@ -234,36 +281,46 @@ class Agent(nn.Module):
         perms = torch.stack(perms).to(dev)
         sd = self.rs_var.sqrt().clamp(min=1e-5)
         lo, hi = c.reward_range
+        fused = self.fused_learn
+        if fused:
+            returns = returns.contiguous()
+            gather = self.batch_gather(traj['rewards'].shape[1])
         for epoch in range(self.epochs):
             for mbi, k in enumerate(range(0, N, self.batch_size)):
                 idx = perms[epoch, k:k + self.batch_size]
                 b = idx.shape[0]
-                mb_lens = lens[idx].contiguous()
-                mb_act = actions[idx].contiguous()
-                mb_rew = rewards[idx]
-                prev_act = torch.full_like(mb_act, 0. if c.continuous else -1)
-                prev_act[:, 1:] = mb_act[:, :-1]
-                prev_rew = torch.zeros_like(mb_rew)
-                prev_rew[:, 1:] = mb_rew[:, :-1]
-                swr = (torch.cat((states[idx], prev_rew[..., None]), dim=-1) - self.rs_mean) / sd
-                swr = swr.contiguous()
+                if fused:   # device minibatch assembly (xtrl_minibatch_gather)
+                    g = gather(traj, returns, lens, idx, self.rs_mean, self.rs_var, n)
+                    mb_lens, mb_act, prev_act, swr = g['lens'], g['action'], g['prev_action'], g['swr']
+                    mb_old_lp, mb_ret, mb_old_v, mb_done = g['old_logp'], g['returns'], g['old_values'], g['dones']
+                else:
+                    mb_lens = lens[idx].contiguous()
+                    mb_act = actions[idx].contiguous()
+                    mb_rew = rewards[idx]
+                    prev_act = torch.full_like(mb_act, 0. if c.continuous else -1)
+                    prev_act[:, 1:] = mb_act[:, :-1]
+                    prev_rew = torch.zeros_like(mb_rew)
+                    prev_rew[:, 1:] = mb_rew[:, :-1]
+                    swr = (torch.cat((states[idx], prev_rew[..., None]), dim=-1) - self.rs_mean) / sd
+                    swr = swr.contiguous()
+                    mb_old_lp, mb_ret = old_lp[idx].contiguous(), returns[idx].contiguous()
+                    mb_old_v, mb_done = old_values[idx].contiguous(), bounds[idx].contiguous()
                 keep = reward_coin(self.seed, update, epoch, mbi, c.reward_dropout)
                 latent = self.latent(gene_ids[idx]) if c.evolutionary else None
                 attn_seed, attn_off, ff_off = self.seed * 1000003 + update, (epoch * 4096 + mbi) * 1024, \
                     (epoch * 4096 + mbi) * 64
                 if self.fused_learn:
                     step = self.train_step(b, n)
-                    step.forward(swr, prev_act.contiguous(), mb_act, latent, mb_lens, keep, attn_seed, attn_off,
-                                 ff_off, c.dropout)
+                    step.forward(swr, prev_act, mb_act, latent, mb_lens, keep, attn_seed, attn_off, ff_off,
+                                 c.dropout)
                 else:
                     act_in = prev_act if c.continuous else prev_act.long()
                     nxt = mb_act if c.continuous else mb_act.long()
                     raw, values, pred_raw, done_logit = model.forward_train(
                         swr[..., :-1], act_in, swr[..., -1], nxt, latent, mb_lens, keep,
                         attn_seed=attn_seed, attn_offset=attn_off, ff_offset=ff_off)
-                K = ops.LossConsts(actions=mb_act, old_logp=old_lp[idx].contiguous(), returns=returns[idx].contiguous(),
-                                   old_values=old_values[idx].contiguous(), dones=bounds[idx].contiguous(),
-                                   lens=mb_lens, real=swr, support=model.hl_support, centers=model.hl_centers,
+                K = ops.LossConsts(actions=mb_act, old_logp=mb_old_lp, returns=mb_ret, old_values=mb_old_v,
+                                   dones=mb_done, lens=mb_lens, real=swr, support=model.hl_support, centers=model.hl_centers,
                                    continuous=c.continuous, squash=c.squash, hl_mean=c.hl_reduction_mean,
                                    eps_clip=c.eps_clip, value_clip=c.value_clip, entropy_weight=c.entropy_weight,
                                    w_actor=self.actor_loss_weight, w_critic=self.critic_loss_weight,
@@ -283,13 +340,17 @@ class Agent(nn.Module):
                 self.optimizer_step()
                 # RSNorm copy update with the normalised masked rows (xtrl.py:1005, 598-610)
                 with torch.no_grad():
-                    mask = (torch.arange(n, device=dev)[None, :] < mb_lens[:, None]).float()
-                    m = (swr * mask[..., None]).sum((0, 1)) / mask.sum()
-                    m = dist_.mean_(m)
-                    t = rs_step
-                    delta = m - rs_mean
-                    rs_mean = rs_mean + delta / t
-                    rs_var = (t - 1) / t * (rs_var + delta ** 2 / t)
+                    if fused:
+                        m = dist_.mean_(g['rs_m'])
+                        rsnorm_update(rs_mean, rs_var, m, rs_step)
+                    else:
+                        mask = (torch.arange(n, device=dev)[None, :] < mb_lens[:, None]).float()
+                        m = (swr * mask[..., None]).sum((0, 1)) / mask.sum()
+                        m = dist_.mean_(m)
+                        t = rs_step
+                        delta = m - rs_mean
+                        rs_mean = rs_mean + delta / t
+                        rs_var = (t - 1) / t * (rs_var + delta ** 2 / t)
                     rs_step += 1
                 if (c.evolutionary and fitnesses is not None and self.step > self.evolve_after_step
                         and self.step % self.evolve_every == 0):
@@ -299,6 +360,13 @@ class Agent(nn.Module):
                 self.logs.append(stats)
         self.rs_mean, self.rs_var, self.rs_step = rs_mean, rs_var, rs_step
         self.step += 1
+
+    def batch_gather(self, Tmax):
+        bg = getattr(self, '_batch_gather', None)
+        if bg is None or bg.n_max < Tmax:
+            from .train import BatchGather
+            self._batch_gather = bg = BatchGather(self.cfg, self.batch_size, Tmax, self.device)
+        return bg
 
     def train_step(self, b, n):
         """The fused learn step, with activation buffers for up to (batch_size, n) minibatches."""

@@ -187,3 +187,58 @@ def ff_dropout_mask(M, N, p, seed, offset, device):
     L.check(L.lib().xtrl_ff_dropout_mask(L.ptr(m), M, N, float(p), int(seed) & (2 ** 64 - 1),
                                          int(offset) & 0xFFFFFFFF, L.stream()), 'ff_dropout_mask')
     return m
+
+
+class BatchGather:
+    """Device minibatch assembly (xtrl_minibatch_gather) into persistent [b_max][n_max] buffers."""
+
+    def __init__(self, cfg, b_max, n_max, device):
+        c = cfg
+        self.c, self.b_max, self.n_max = c, b_max, n_max
+        S, A, B = c.state_dim, c.num_actions, c.num_bins
+        f32, i32, u8 = dict(device=device, dtype=torch.float32), dict(device=device, dtype=torch.int32), \
+            dict(device=device, dtype=torch.uint8)
+        T = b_max * n_max
+        self.buf = dict(swr=torch.empty(T * (S + 1), **f32), old_logp=torch.empty(T * (A if c.continuous else 1), **f32),
+                        mb_returns=torch.empty(T, **f32), old_values=torch.empty(T * B, **f32),
+                        dones=torch.empty(T, **u8), mb_lens=torch.empty(b_max, **i32),
+                        rs_part=torch.empty(64 * (S + 2), **f32), rs_m=torch.empty(S + 1, **f32))
+        if c.continuous:
+            self.buf.update(prev_action_f=torch.empty(T * A, **f32), action_f=torch.empty(T * A, **f32))
+        else:
+            self.buf.update(prev_action=torch.empty(T, **i32), action=torch.empty(T, **i32))
+
+    def __call__(self, traj, returns, lens, idx, rs_mean, rs_var, n):
+        c, bf = self.c, self.buf
+        b = idx.shape[0]
+        assert b <= self.b_max and n <= self.n_max
+        N, Tmax = traj['rewards'].shape
+        S, A, B = c.state_dim, c.num_actions, c.num_bins
+        D = L.BatchDesc(N=N, Tmax=Tmax, n=n, b=b, S=S, A=A, B=B, continuous=int(c.continuous))
+        src = dict(states=traj['states'], actions=None if c.continuous else traj['actions'],
+                   actions_f=traj['actions_f'] if c.continuous else None, rewards=traj['rewards'], logp=traj['logp'],
+                   bounds=traj['bounds'], values=traj['values'], returns=returns, lens=lens, idx=idx,
+                   rs_mean=rs_mean, rs_var=rs_var)
+        for k, t in src.items():
+            if t is not None:
+                assert t.is_cuda and t.is_contiguous(), k
+                setattr(D, k, t.data_ptr())
+        for k, t in bf.items():
+            setattr(D, k, t.data_ptr())
+        L.check(L.lib().xtrl_minibatch_gather(C.byref(D), L.stream()), 'minibatch_gather')
+        T = b * n
+        out = dict(swr=bf['swr'][:T * (S + 1)].view(b, n, S + 1), returns=bf['mb_returns'][:T].view(b, n),
+                   old_values=bf['old_values'][:T * B].view(b, n, B), dones=bf['dones'][:T].view(b, n),
+                   lens=bf['mb_lens'][:b], rs_m=bf['rs_m'])
+        if c.continuous:
+            out.update(prev_action=bf['prev_action_f'][:T * A].view(b, n, A), action=bf['action_f'][:T * A].view(b, n, A),
+                       old_logp=bf['old_logp'][:T * A].view(b, n, A))
+        else:
+            out.update(prev_action=bf['prev_action'][:T].view(b, n), action=bf['action'][:T].view(b, n),
+                       old_logp=bf['old_logp'][:T].view(b, n))
+        return out
+
+
+def rsnorm_update(mean, var, m, t):
+    L.check(L.lib().xtrl_rsnorm_update(L.ptr(mean), L.ptr(var), L.ptr(m), mean.numel(), int(t), L.stream()),
+            'rsnorm_update')
