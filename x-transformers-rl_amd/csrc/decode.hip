@@ -129,6 +129,7 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
   const float* Kc = Ly.k_cache + cache_base;
   const float* Vc = Ly.v_cache + cache_base;
   float mx = -INFINITY;
+#pragma unroll 2
   for (int j = lane; j <= t; j += 64) {
     float s = 0.f;
     if (j < t) {
@@ -159,6 +160,9 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
   sum = wave_sum(sum);
   wave_sync();
   float acc = 0.f;
+  // eight V rows in flight per lane group (the loads are independent; only the adds chain).
+  // (A one-key-per-lane P.V with a reduce-scatter butterfly measured slower: 14.9 vs 11.5 us.)
+#pragma unroll 8
   for (int j = g; j <= t; j += G) {
     const float p = sc[j] / sum;
     const float vv = (j < t) ? Vc[(int64_t)j * DH + c] : vs[c];
