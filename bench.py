@@ -246,7 +246,8 @@ def ppo_loss_delta(learner, env, cfg):
         mb = R.Minibatch(states, actions, rewards, old_lp, returns, values, bounds, genes.cpu()[idx_c], mb_lens)
         from xtrl_amd.learner import reward_coin
         keep = reward_coin(agent.seed, u, epoch, mbi, c.reward_dropout)
-        ref, _, _, _ = R.minibatch_loss(model, rs, mb, None, R.LossWeights(agent.actor_loss_weight,
+        latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if c.evolutionary else None
+        ref, _, _, _ = R.minibatch_loss(model, rs, mb, latent, R.LossWeights(agent.actor_loss_weight,
                                                                             agent.critic_loss_weight,
                                                                             agent.autoregressive_loss_weight), keep)
         out.update(gpu=float(loss), cpu=float(ref))

@@ -12,8 +12,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
+#ifndef LAB_MINB
+#define LAB_MINB 1
+#endif
 template <int BM, int BN, int BK, int WM, int WN, int NBUF>
-__global__ __launch_bounds__(64 * WM * WN) void k_lab(const float* __restrict__ A, const float* __restrict__ B,
+__global__ __launch_bounds__(64 * WM * WN, LAB_MINB) void k_lab(const float* __restrict__ A, const float* __restrict__ B,
                                                      float* __restrict__ C, int M, int N, int K) {
   constexpr int NT = 64 * WM * WN, TM = BM / (32 * WM), TN = BN / (32 * WN);
   constexpr int AST = BM + 1, BST = BN + 1;
