@@ -33,6 +33,10 @@ import torch.distributed as dist   # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3   # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
+MFMA_BF16_PEAK_TFLOPS = 16 * MFMA_F32_PEAK_TFLOPS   # dense bf16 MFMA (v_mfma_f32_32x32x16_bf16): 16x the f32 rate
+# The large-tile GEMMs compute each fp32 product as six bf16 piece products (csrc/gemm.hip, X6), so
+# their MFMA ceiling in fp32-GEMM FLOP/s is the bf16 peak / 6 (XTRL_GEMM_F32=1: native f32 MFMA).
+X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
 
 CONFIGS = {
     # configs[2] of BASELINE.json — the north-star workload, per GPU
@@ -330,9 +334,13 @@ def main():
             avg_s = gtimer.ms / gtimer.launches / 1e3
             flops = gtimer.total_flops / gtimer.launches
             achieved = flops / avg_s / 1e12
+            x6 = os.environ.get('XTRL_GEMM_F32', '0') in ('', '0')
+            peak = X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
             roofline = dict(kernel='k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, 128x128 tiles, split-K; '
-                                   'the largest kernel of the update)', bound='mfma', achieved=round(achieved, 2),
-                            peak=MFMA_F32_PEAK_TFLOPS, unit='TFLOP/s', frac=round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                                   'the largest kernel of the update; fp32 products as ' +
+                                   ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
+                                    'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
+                            peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
                             traffic=pmc_traffic(WgradGemmTimer.KERNEL), avg_launch_us=round(avg_s * 1e6, 2),
                             flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:

@@ -56,6 +56,43 @@ def test_gemm_f32(M, N, K, mode):
     tol(out, ref, 1e-5, 1e-5)
 
 
+def _dot_scale(a, b):
+    """sum_k |a[m, k] b[k, n]| (the scale of an fp32 dot product's rounding error)."""
+    return a.abs() @ b.abs()
+
+
+@pytest.mark.parametrize('layout', ['NN', 'NT', 'TT'])
+def test_gemm_large_tile_split_bf16_accuracy(layout):
+    """The large-tile geometry computes fp32 products as six bf16 piece products (csrc/gemm.hip,
+    X6).  Its error against fp64 must stay at the native fp32 level: max |C - C64| / sum|a b| below
+    7 x 2^-24 (native f32 MFMA: 3-5 x 2^-24 at these K; a two-piece bf16x3 split would sit near
+    2^-17).  Ragged M / N / K exercise the masked tail slabs and clamped tiles."""
+    from xtrl_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(11)
+    M, N, K = 4100, 772, 260
+    scale = torch.exp2(torch.randint(-4, 4, (M, 1), generator=g).double())
+    a = (torch.randn(M, K, generator=g, dtype=torch.float64) * scale).float()
+    b = torch.randn(K, N, generator=g, dtype=torch.float64).float() * 0.1
+    ad, bd = a.double(), b.double()
+    out = torch.empty(M, N, device=DEV)
+    if layout == 'NN':     # A [M][K], B as an nn.Linear weight [N][K]
+        ops.gemm_ex(a.to(DEV), b.t().contiguous().to(DEV), 0, 0, M, N, K, out)
+        ref, sc = ad @ bd, _dot_scale(ad, bd)
+    elif layout == 'NT':   # A [M][K], B [K][N] (input-gradient GEMM)
+        ops.gemm_ex(a.to(DEV), b.to(DEV), 0, 1, M, N, K, out)
+        ref, sc = ad @ bd, _dot_scale(ad, bd)
+    else:                  # weight gradient: dW[N][K'] = dY^T X over M tokens (split over tokens)
+        dy, x = a[:, :256].contiguous(), torch.randn(M, 1024, generator=g).float()
+        dw = torch.zeros(256, 1024, device=DEV)
+        ws = torch.empty(32 << 20, device=DEV)
+        ops.wgrad(dy.to(DEV), x.to(DEV), dw, ws, beta=0.)
+        out = dw
+        ref, sc = dy.double().t() @ x.double(), _dot_scale(dy.double().t(), x.double())
+    torch.cuda.synchronize()
+    err = ((out.double().cpu() - ref).abs() / sc).max().item()
+    assert err < 7 * 2.0 ** -24, f'{layout}: max error {err / 2.0 ** -24:.2f} x 2^-24 of sum |a b|'
+
+
 # ----------------------------------------------------------------------------------------------
 # training attention
 # ----------------------------------------------------------------------------------------------
@@ -505,8 +542,20 @@ def test_fused_train_step_matches_autograd(cont, evo, gates, p, T):
     autograd step (model.forward_train + fused loss + loss.backward) on identical weights and
     minibatch, dropout on (the same counter-based masks): loss within 1e-5 relative, every
     gradient within 1e-4 of the gradient scale.  n > 64 exercises multi-tile attention."""
-    learner, env, _ = make_learner(depth=3, gates=gates, evo=evo, cont=cont, T=T, episodes=8, batch=4, seed=9,
-                                   hazard=5, dim=64)
+    _fused_vs_autograd(cont, evo, gates, p, T, depth=3, episodes=8, batch=4, hazard=5, dim=64)
+
+
+@pytest.mark.gpu
+def test_fused_train_step_large_tiles_matches_autograd():
+    """As above at a size where the forward, input-gradient and weight-gradient GEMMs take the
+    large-tile split-bf16 geometry (96 episodes x 131 tokens, d 128, ff 512) with every fused
+    epilogue (LayerNorm prologue, GELU + dropout, SiLU save, residual, GELU' and gate backward)."""
+    _fused_vs_autograd(False, False, True, 0.25, 130, depth=2, episodes=96, batch=96, hazard=9, dim=128)
+
+
+def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, dim):
+    learner, env, _ = make_learner(depth=depth, gates=gates, evo=evo, cont=cont, T=T, episodes=episodes,
+                                   batch=batch, seed=9, hazard=hazard, dim=dim)
     agent = learner.agent
     agent.cfg.dropout = p
     agent.model.cfg.dropout = p

@@ -32,7 +32,18 @@ run_pmc() {
   done
   cd $GRAFT_REPO_ROOT && python3 tools/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.txt; cat gpurun_out/pmc_summary.txt
 }
+run_trace() {
+  # kernel trace of one C3 update (tools/update_trace.py): per-phase totals, one minibatch, one decode step
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/trace -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/update_trace.py run > $GRAFT_REPO_ROOT/gpurun_out/trace.log 2>&1
+  rc=$?; cd $GRAFT_REPO_ROOT; tail -3 gpurun_out/trace.log
+  if [ $rc -ne 0 ]; then echo "trace rc=$rc"; exit $rc; fi
+  python3 tools/update_trace.py show $(find gpurun_out/trace -name '*kernel_trace.csv' | head -1) > gpurun_out/trace_summary.txt
+  find gpurun_out/trace -type f -name '*kernel_trace.csv' -delete
+  head -80 gpurun_out/trace_summary.txt
+}
 case $what in
+  trace) run_trace ;;
   pmc) run_pmc "$@" ;;
   tests) run_tests ;;
   bench) run_bench "$@" ;;

@@ -1,0 +1,85 @@
+"""Kernel-by-kernel breakdown of one C3 update (run under `rocprofv3 --kernel-trace`).
+
+  python tools/update_trace.py run            # (under rocprofv3) 1 warmup + 1 update, then exit
+  python tools/update_trace.py show TRACE.csv # per-phase totals and one minibatch's kernels in order
+
+The measured update is everything from the last rollout-begin / env-reset launches on.
+"""
+import csv
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
+
+
+def run():
+    import torch
+    import bench
+    cfg = bench.CONFIGS['c3']
+    learner, env = bench.build_learner(cfg, 0)
+    bench.one_update(learner, env, cfg['T'])
+    torch.cuda.synchronize()
+    bench.one_update(learner, env, cfg['T'])
+    torch.cuda.synchronize()
+
+
+def short(name):
+    name = name.replace('xtrl::(anonymous namespace)::', '').replace('void ', '')
+    if name.startswith('k_gemm<'):
+        return name.split('(')[0]
+    return name.split('(')[0][:60]
+
+
+def show(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r['Start_Timestamp']))
+    names = [r['Kernel_Name'] for r in rows]
+    dur = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3 for r in rows]
+    # the measured update starts at its rollout: the last k_sim_reset / k_rollout_begin pair
+    begins = [i for i, n in enumerate(names) if 'k_rollout_begin' in n or 'k_sim_reset' in n]
+    start = begins[-1]
+    while start - 1 in begins:
+        start -= 1
+    upd = list(range(start, len(rows)))
+    t0 = int(rows[upd[0]]['Start_Timestamp'])
+    t1 = int(rows[upd[-1]]['End_Timestamp'])
+    print(f'update: {len(upd)} kernels, wall {(t1 - t0) / 1e6:.2f} ms, busy {sum(dur[i] for i in upd) / 1e3:.2f} ms')
+    gathers = [i for i in upd if 'k_gather' in names[i]]
+    if gathers:
+        roll = [i for i in upd if i < gathers[0]]
+        learn = [i for i in upd if i >= gathers[0]]
+        for label, seg in (('rollout', roll), ('learn', learn)):
+            ts = int(rows[seg[0]]['Start_Timestamp']); te = int(rows[seg[-1]]['End_Timestamp'])
+            print(f'{label}: {len(seg)} kernels, wall {(te - ts) / 1e6:.2f} ms, busy {sum(dur[i] for i in seg) / 1e3:.2f} ms')
+            agg = defaultdict(lambda: [0, 0.0])
+            for i in seg:
+                a = agg[short(names[i])]; a[0] += 1; a[1] += dur[i]
+            for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+                print(f'  {us / 1e3:8.2f} ms {n:6d} {us / n:8.1f} us  {k}')
+        # one minibatch: between the 2nd and 3rd gather
+        if len(gathers) > 2:
+            a, b = gathers[1], gathers[2]
+            ts = int(rows[a]['Start_Timestamp']); te = int(rows[b]['Start_Timestamp'])
+            print(f'\nminibatch (gather #2..#3): {b - a} kernels, wall {(te - ts) / 1e3:.1f} us, '
+                  f'busy {sum(dur[a:b]):.1f} us')
+            for i in range(a, b):
+                gap = (int(rows[i]['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp'])) / 1e3
+                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  {short(names[i])}')
+        # one decode step: the kernels between two consecutive k_sample launches in the rollout
+        samples = [i for i in roll if 'k_sample' in names[i]]
+        if len(samples) > 12:
+            a, b = samples[10], samples[11]
+            ts = int(rows[a]['End_Timestamp']); te = int(rows[b]['End_Timestamp'])
+            print(f'\ndecode step (k_sample #10..#11): {b - a} kernels, wall {(te - ts) / 1e3:.1f} us')
+            for i in range(a + 1, b + 1):
+                gap = (int(rows[i]['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp'])) / 1e3
+                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  {short(names[i])}')
+
+
+if __name__ == '__main__':
+    if sys.argv[1] == 'run':
+        run()
+    else:
+        show(sys.argv[2])

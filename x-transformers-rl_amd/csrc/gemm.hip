@@ -17,10 +17,21 @@
 // half-wave — conflict-free); the next slab's global loads are issued before the current slab's
 // MFMAs (register double buffering, one barrier per slab).
 //
+// X6 (split-bf16 products, the large-tile geometry): every staged fp32 operand x is split into
+// three bf16 pieces x = hi + mid + lo (each the round-to-nearest bf16 of the running remainder;
+// the subtractions are exact and the three pieces hold all 24 significand bits) and the product is
+// the sum of the six largest piece products lo.hi + hi.lo + mid.mid + mid.hi + hi.mid + hi.hi on
+// the bf16 matrix cores (v_mfma_f32_32x32x16_bf16, fp32 accumulate, 6 x 32 cycles per 32x32x16
+// step vs 8 x 64 for v_mfma_f32_32x32x2_f32).  The dropped terms (mid.lo, lo.mid, lo.lo) are
+// below 2^-24 of each product: measured error vs fp64 equals the native f32 path's
+// (tools/x6_lab.hip: rms 0.51-0.57 vs 0.58-0.69 x 2^-24 of sum |a b|, K = 256 ... 4096).
+// XTRL_GEMM_F32=1 selects the native f32 MFMA path everywhere (A/B experiments).
+//
 // The optional LayerNorm prologue (x-transformers LayerNorm: no affine, eps 1e-5, times gamma;
 // A "N" only) computes per-row mean / rstd for the block's rows (two-pass) and normalises A while
 // staging it.
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 #include "philox.h"
@@ -29,9 +40,27 @@ namespace xtrl {
 
 namespace {
 
-template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
-__global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// x = hi + mid + lo exactly (round-to-nearest bf16 of the running remainder; exact subtractions)
+__device__ __forceinline__ void split3(float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+  const f32x4 x{v.x, v.y, v.z, v.w};
+  h = __builtin_convertvector(x, bf16x4);
+  const f32x4 r1 = x - __builtin_convertvector(h, f32x4);
+  m = __builtin_convertvector(r1, bf16x4);
+  const f32x4 r2 = r1 - __builtin_convertvector(m, f32x4);
+  l = __builtin_convertvector(r2, bf16x4);
+}
+
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC,
+          bool X6 = false>
+__global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1) void k_gemm(const GemmArgs a) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN, BK = 32 * WK, NT = 64 * WM * WN * WK;
+  // X6 images: [piece][row][k] bf16, rows padded to XRS = BK + 8 (conflict-light 16-byte reads)
+  constexpr int XRS = BK + 8;
+  static_assert(!X6 || (WK == 1 && VEC && (!TA || BM * BK % (16 * NT) == 0) && (!TB || BN * BK % (16 * NT) == 0)),
+                "X6: one wave along K, vector staging, whole 4 x 4 transposed groups");
   // k-major LDS images [buf][k][m]: +1 pad ("N", transposed scalar staging writes), +4 (16-byte
   // rows, "T").  SWZ (kept for experiments, off): row stride = 32 mod 64 banks so the two
   // half-waves of a fragment read (rows k, k+1) use disjoint banks, plus an XOR-by-8 column
@@ -42,24 +71,40 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   constexpr int A_F4 = BM * BK / 4 / NT, B_F4 = BN * BK / 4 / NT;   // float4 loads per thread per slab
   static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small for the thread count");
   // ONE LDS stage (the next slab waits in registers; see the main loop): one static block
-  constexpr int SMEM = BK * AST + BK * BST + (LN ? 2 * BM : 0);
+  constexpr int STAGE = X6 ? 3 * (BM + BN) * XRS / 2 : BK * AST + BK * BST;   // floats
+  constexpr int SMEM = STAGE + (LN ? 2 * BM : 0);
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
   float(*As)[BK][AST] = reinterpret_cast<float(*)[BK][AST]>(smem);
   float(*Bs)[BK][BST] = reinterpret_cast<float(*)[BK][BST]>(smem + BK * AST);
-  float* row_mean = smem + BK * AST + BK * BST;
+  __bf16(*Xa)[BM][XRS] = reinterpret_cast<__bf16(*)[BM][XRS]>(smem);
+  __bf16(*Xb)[BN][XRS] = reinterpret_cast<__bf16(*)[BN][XRS]>(reinterpret_cast<__bf16*>(smem) + 3 * BM * XRS);
+  float* row_mean = smem + STAGE;
   float* row_rstd = row_mean + BM;
   auto sw = [](int k, int m) { return SWZ ? (m ^ (8 * ((k >> 2) & 7))) : m; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
-  const int bx = blockIdx.x;
-  const int m0 = blockIdx.y * BM, n0 = bx * BN;
+  // workgroup -> (column tile, row tile, K split).  The hardware deals workgroups to the 8 XCDs
+  // round-robin by linear id; with xcd_remap the ids are permuted so each XCD runs a contiguous
+  // range of logical tiles (column tile fastest): the column tiles of a row tile — which all read
+  // the same A rows — then share that XCD's L2 instead of fetching A once per XCD
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_remap) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int total = nx * ny * gridDim.z;
+    const int lin = bx + nx * (by + ny * bz);
+    const int lg = (lin & 7) * (total >> 3) + (lin >> 3);
+    bx = lg % nx;
+    by = (lg / nx) % ny;
+    bz = lg / (nx * ny);
+  }
+  const int m0 = by * BM, n0 = bx * BN;
   const int M = a.M, N = a.N;
   int K = a.K;
   const float* __restrict__ Ab = a.A;
   const float* __restrict__ Bb = a.B;
   if (a.kspan > 0) {   // cross-workgroup split of K: shift the operands to this split's K range
-    const int kb = blockIdx.z * a.kspan;
+    const int kb = bz * a.kspan;
     K = min(a.kspan, a.K - kb);
     Ab += TA ? (int64_t)kb * a.lda : kb;
     Bb += TB ? (int64_t)kb * a.ldb : kb;
@@ -129,7 +174,9 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     __syncthreads();
   }
 
-  float4 ra[A_F4], rb[B_F4];
+  // staging registers (one slab; the buffer index P is a compile-time constant)
+  float4 ra[1][A_F4], rb[1][B_F4];
+  using I0 = std::integral_constant<int, 0>;
   // Branch-free staging loads.  Indices are clamped into the operand, so every load is in bounds;
   // rows / columns past M or N then hold duplicates that only feed output rows / columns the
   // epilogue discards, and only the reduction index k needs zeroing past K — which can only happen
@@ -161,7 +208,9 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     }
     return f;
   };
-  auto load_slab = [&](int k0, bool tail) {
+  auto load_slab = [&](auto P, int k0, bool tail) {
+    float4(&RA)[A_F4] = ra[decltype(P)::value];
+    float4(&RB)[B_F4] = rb[decltype(P)::value];
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int e = tid + i * NT;
@@ -182,10 +231,14 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
             f.w = k + 3 < K ? f.w : 0.f;
           }
         }
-        ra[i] = f;
+        RA[i] = f;
+      } else if constexpr (X6) {   // 4 x 4 groups: k rows 4 kq .. 4 kq + 3 of m quad q (kq fastest
+                                   // over lanes: conflict-free transposed LDS writes)
+        const int g = tid + (i >> 2) * NT, kq = g % (BK / 4), q = g / (BK / 4);
+        RA[i] = load4(Ab, a.lda, k0 + 4 * kq + (i & 3), m0 + 4 * q, K, M, true, tail);
       } else {               // [BK rows][BM/4 quads]
         const int r = e / (BM / 4), q = e % (BM / 4);
-        ra[i] = load4(Ab, a.lda, k0 + r, m0 + 4 * q, K, M, true, tail);
+        RA[i] = load4(Ab, a.lda, k0 + r, m0 + 4 * q, K, M, true, tail);
       }
     }
 #pragma unroll
@@ -193,26 +246,78 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TB) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        rb[i] = load4(Bb, a.ldb, n0 + r, k0 + 4 * q, N, K, false, tail);
+        RB[i] = load4(Bb, a.ldb, n0 + r, k0 + 4 * q, N, K, false, tail);
+      } else if constexpr (X6) {
+        const int g = tid + (i >> 2) * NT, kq = g % (BK / 4), q = g / (BK / 4);
+        RB[i] = load4(Bb, a.ldb, k0 + 4 * kq + (i & 3), n0 + 4 * q, K, N, true, tail);
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        rb[i] = load4(Bb, a.ldb, k0 + r, n0 + 4 * q, K, N, true, tail);
+        RB[i] = load4(Bb, a.ldb, k0 + r, n0 + 4 * q, K, N, true, tail);
       }
     }
   };
-  auto store_slab = [&](int buf) {
+  // X6 staging: split each row's 4 consecutive k values into the three piece images
+  auto store_slab_x6 = [&](auto P) {
+    const float4(&RA)[A_F4] = ra[decltype(P)::value];
+    const float4(&RB)[B_F4] = rb[decltype(P)::value];
+    __bf16* xa = &Xa[0][0][0];
+    __bf16* xb = &Xb[0][0][0];
+    auto put = [&](__bf16* img, int rows, int row, int k, float4 v) {
+      bf16x4 h, m, l;
+      split3(v, h, m, l);
+      __bf16* p = img + row * XRS + k;
+      *reinterpret_cast<bf16x4*>(p) = h;
+      *reinterpret_cast<bf16x4*>(p + rows * XRS) = m;
+      *reinterpret_cast<bf16x4*>(p + 2 * rows * XRS) = l;
+    };
+#pragma unroll
+    for (int i = 0; i < A_F4; ++i) {
+      if constexpr (!TA) {
+        const int e = tid + i * NT, r = e / (BK / 4), q = e % (BK / 4);
+        put(xa, BM, r, 4 * q, RA[i]);
+      } else if ((i & 3) == 3) {   // transpose the 4 x 4 group: row m = 4 q + c gets k 4 kq .. 4 kq + 3
+        const int g = tid + (i >> 2) * NT, kq = g % (BK / 4), q = g / (BK / 4);
+        const float4 k0v = RA[i - 3], k1v = RA[i - 2], k2v = RA[i - 1], k3v = RA[i];
+        put(xa, BM, 4 * q + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
+        put(xa, BM, 4 * q + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
+        put(xa, BM, 4 * q + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
+        put(xa, BM, 4 * q + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_F4; ++i) {
+      if constexpr (!TB) {
+        const int e = tid + i * NT, r = e / (BK / 4), q = e % (BK / 4);
+        put(xb, BN, r, 4 * q, RB[i]);
+      } else if ((i & 3) == 3) {
+        const int g = tid + (i >> 2) * NT, kq = g % (BK / 4), q = g / (BK / 4);
+        const float4 k0v = RB[i - 3], k1v = RB[i - 2], k2v = RB[i - 1], k3v = RB[i];
+        put(xb, BN, 4 * q + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
+        put(xb, BN, 4 * q + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
+        put(xb, BN, 4 * q + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
+        put(xb, BN, 4 * q + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+      }
+    }
+  };
+  auto store_slab = [&](auto P, int buf) {
+    if constexpr (X6) {
+      store_slab_x6(P);
+      return;
+    }
+    const float4(&RA)[A_F4] = ra[decltype(P)::value];
+    const float4(&RB)[B_F4] = rb[decltype(P)::value];
 #pragma unroll
     for (int i = 0; i < A_F4; ++i) {
       const int e = tid + i * NT;
       if constexpr (!TA) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        As[buf][4 * q + 0][sw(4 * q + 0, r)] = ra[i].x;
-        As[buf][4 * q + 1][sw(4 * q + 1, r)] = ra[i].y;
-        As[buf][4 * q + 2][sw(4 * q + 2, r)] = ra[i].z;
-        As[buf][4 * q + 3][sw(4 * q + 3, r)] = ra[i].w;
+        As[buf][4 * q + 0][sw(4 * q + 0, r)] = RA[i].x;
+        As[buf][4 * q + 1][sw(4 * q + 1, r)] = RA[i].y;
+        As[buf][4 * q + 2][sw(4 * q + 2, r)] = RA[i].z;
+        As[buf][4 * q + 3][sw(4 * q + 3, r)] = RA[i].w;
       } else {
         const int r = e / (BM / 4), q = e % (BM / 4);
-        *reinterpret_cast<float4*>(&As[buf][r][sw(r, 4 * q)]) = ra[i];
+        *reinterpret_cast<float4*>(&As[buf][r][sw(r, 4 * q)]) = RA[i];
       }
     }
 #pragma unroll
@@ -220,13 +325,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
       const int e = tid + i * NT;
       if constexpr (!TB) {
         const int r = e / (BK / 4), q = e % (BK / 4);
-        Bs[buf][4 * q + 0][sw(4 * q + 0, r)] = rb[i].x;
-        Bs[buf][4 * q + 1][sw(4 * q + 1, r)] = rb[i].y;
-        Bs[buf][4 * q + 2][sw(4 * q + 2, r)] = rb[i].z;
-        Bs[buf][4 * q + 3][sw(4 * q + 3, r)] = rb[i].w;
+        Bs[buf][4 * q + 0][sw(4 * q + 0, r)] = RB[i].x;
+        Bs[buf][4 * q + 1][sw(4 * q + 1, r)] = RB[i].y;
+        Bs[buf][4 * q + 2][sw(4 * q + 2, r)] = RB[i].z;
+        Bs[buf][4 * q + 3][sw(4 * q + 3, r)] = RB[i].w;
       } else {
         const int r = e / (BN / 4), q = e % (BN / 4);
-        *reinterpret_cast<float4*>(&Bs[buf][r][sw(r, 4 * q)]) = rb[i];
+        *reinterpret_cast<float4*>(&Bs[buf][r][sw(r, 4 * q)]) = RB[i];
       }
     }
   };
@@ -243,7 +348,51 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   const int fi = wm * 32 * TM + (lane & 31), fj = wn * 32 * TN + (lane & 31), fk = wk * 32 + (lane >> 5);
   // MFMA fragments double-buffered in registers: the LDS reads of step s + 1 are issued (and pinned
   // by a scheduling barrier) ahead of step s's MFMAs, so their latency hides behind them
+  auto compute_x6 = [&]() {
+    const int xi = wm * 32 * TM + (lane & 31), xj = wn * 32 * TN + (lane & 31), xk = 8 * (lane >> 5);
+    const __bf16* xa = &Xa[0][0][0];
+    const __bf16* xb = &Xb[0][0][0];
+    // fragments double-buffered: the reads of k-step s + 1 fly across k-step s's MFMAs
+    constexpr int FB = 2;
+    bf16x8 av[FB][3][TM], bv[FB][3][TN];
+    auto rd = [&](int buf, int st) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[buf][p][i] = *reinterpret_cast<const bf16x8*>(xa + (p * BM + xi + 32 * i) * XRS + 16 * st + xk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[buf][p][j] = *reinterpret_cast<const bf16x8*>(xb + (p * BN + xj + 32 * j) * XRS + 16 * st + xk);
+      }
+    };
+    if constexpr (FB == 2) rd(0, 0);
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) {
+      const int pb = FB == 2 ? (st & 1) : 0;
+      if constexpr (FB == 2) {
+        if (st + 1 < BK / 16) rd(pb ^ 1, st + 1);
+      } else {
+        rd(0, st);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // smallest products first: (A piece, B piece) = lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+      constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][PA[t]][i], bv[pb][PB[t]][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   auto compute = [&](int cur) {
+    if constexpr (X6) {
+      compute_x6();
+      return;
+    }
     float av[2][TM], bv[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) av[0][i] = As[cur][fk][sw(fk, fi + 32 * i)];
@@ -273,18 +422,26 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   float rs_acc = 0.f;
   auto rs_slab = [&](int cur) {
     if (do_rs && tid < BM) {
+      if constexpr (X6) {   // hi + mid + lo reassembles x exactly
+        const __bf16* row = &Xa[0][0][0] + tid * XRS;
 #pragma unroll 8
-      for (int k = 0; k < BK; ++k) rs_acc += As[cur][k][sw(k, tid)];
+        for (int k = 0; k < BK; ++k)
+          rs_acc += ((float)row[k] + (float)row[BM * XRS + k]) + (float)row[2 * BM * XRS + k];
+      } else {
+#pragma unroll 8
+        for (int k = 0; k < BK; ++k) rs_acc += As[cur][k][sw(k, tid)];
+      }
     }
   };
   // Pipeline: one LDS stage, slab t + 1 waiting in registers.  Per slab: MFMAs from LDS, barrier,
   // write slab t + 1 to LDS, issue the global loads of slab t + 2, barrier — the loads then fly
   // across a whole compute phase (measured 5-10 % faster than two LDS stages with one barrier,
-  // tools/gemm_lab.hip).  Only the last slab can be partial: the steady-state loop loads full
-  // slabs (no masking, straight-line body); the last few iterations load masked.
-  load_slab(0, true);
-  store_slab(0);
-  if (nk > 1) load_slab(BK, true);
+  // tools/gemm_lab.hip; a second slab in flight for X6 needs more than 256 registers and spills).
+  // Only the last slab can be partial: the steady-state loop loads full slabs (no masking,
+  // straight-line body); the last few iterations load masked.
+  load_slab(I0{}, 0, true);
+  store_slab(I0{}, 0);
+  if (nk > 1) load_slab(I0{}, BK, true);
   __syncthreads();
   int kt = 0;
   for (; kt + 3 < nk; ++kt) {
@@ -292,8 +449,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     rs_slab(0);
     __syncthreads();
-    store_slab(0);
-    load_slab((kt + 2) * BK, false);
+    store_slab(I0{}, 0);
+    load_slab(I0{}, (kt + 2) * BK, false);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
@@ -302,15 +459,15 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
     rs_slab(0);
     __syncthreads();
     if (kt + 1 < nk) {
-      store_slab(0);
-      if (kt + 2 < nk) load_slab((kt + 2) * BK, true);
+      store_slab(I0{}, 0);
+      if (kt + 2 < nk) load_slab(I0{}, (kt + 2) * BK, true);
       __syncthreads();
     }
   }
   if (do_rs && tid < BM) {
     const int m = m0 + tid;
     if (m < M && m >= a.rowsum_m0) {
-      if (a.kspan > 0) a.rowsum_ws[(int64_t)blockIdx.z * M + m] = rs_acc;
+      if (a.kspan > 0) a.rowsum_ws[(int64_t)bz * M + m] = rs_acc;
       else a.rowsum[m - a.rowsum_m0] += rs_acc;
     }
   }
@@ -339,7 +496,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void k_gemm(const GemmArgs a) {
   // ---- epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 -------------
   float* C = a.C;
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
-  if (a.kspan > 0) C += blockIdx.z * a.c_split;
+  if (a.kspan > 0) C += bz * a.c_split;
   const bool acc_c = a.beta != 0.f;
   constexpr bool DROP = (EPI == EPI_GELU_DROP);
   constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE);
@@ -496,12 +653,39 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
   }
 }
 
-template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC>
+bool xcd_env() {   // XTRL_GEMM_XCD=0: hardware workgroup order (A/B experiments)
+  static const bool on = [] {
+    const char* e = getenv("XTRL_GEMM_XCD");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC,
+          bool X6 = false>
 void launch(const GemmArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * WN * TN;
   const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
-  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, EPI, LN, RES, VEC>), grid, dim3(64 * WM * WN * WK), 0, s, a);
+  if constexpr (X6) {
+    if (xcd_env() && (int64_t)grid.x * grid.y * grid.z % 8 == 0) {
+      GemmArgs r = a;
+      r.xcd_remap = 1;
+      hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, EPI, LN, RES, VEC, X6>), grid, dim3(64 * WM * WN * WK), 0,
+                         s, r);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_gemm<WM, WN, WK, TM, TN, TA, TB, EPI, LN, RES, VEC, X6>), grid, dim3(64 * WM * WN * WK), 0, s,
+                     a);
+}
+
+bool use_x6() {   // XTRL_GEMM_F32=1: native f32 MFMA products everywhere
+  static const bool x6 = [] {
+    const char* e = getenv("XTRL_GEMM_F32");
+    return !(e && atoi(e) != 0);
+  }();
+  return x6;
 }
 
 // geometry: 128 x 128 tiles (2 x 2 waves of 64 x 64, four accumulator chains each) when they fill
@@ -537,7 +721,10 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   // (decode-sized M measured on MI355X, graph-timed: M=1024 N=1024 K=256 64x64 11.6 us vs
   //  32x32/WK4 17.4; N=260 K=256 64x32/WK2 7.7 vs 8.2; N=256 K=1024 32x32/WK4 13.7 vs 64x64 24.7)
   if (!vec) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, false>(a, s);
-  else if (tiles128 >= 192) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (tiles128 >= 192) {
+    if (use_x6()) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true, true>(a, s);
+    else launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
+  }
   else if (tiles64 >= 256 && a.K <= 512) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
   else if (a.K <= 256) launch<2, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
   else launch<1, 1, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
@@ -643,7 +830,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   else if (big) {
     const bool timed = prof && prof->events && *prof->n < prof->cap;
     if (timed) (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n], s);
-    launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
+    if (use_x6()) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true, true>(a, s);
+    else launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
     if (timed) {
       (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n + 1], s);
       prof->flops[*prof->n] = 2.0 * (double)M * (double)N * (double)K;

@@ -49,6 +49,7 @@ struct GemmArgs {
   float* rowsum = nullptr;        // += row sums of A (rows >= rowsum_m0, at rowsum[m - rowsum_m0]) —
   int rowsum_m0 = 0;              //   the bias gradient when A = dY^T; with split-K the per-split
   float* rowsum_ws = nullptr;     //   sums go to rowsum_ws[z][M] and the reduce kernel adds them
+  int xcd_remap = 0;              // 1: workgroup ids permuted so each XCD runs consecutive tiles
 };
 
 // launch C = op(A, B) for the combination (trans_a, trans_b, epi, LN = gamma != 0, RES = R != 0)
