@@ -596,10 +596,10 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
   for (int k = lane; k < D; k += 64) Y[(int64_t)m * ldy + k] = ((xr[k] - mean) * rstd) * gamma[k];
 }
 
-// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] in a fixed order (deterministic;
-// four interleaved partial sums keep four loads per thread in flight).  Partials are dense
-// [S][M][N]; each thread owns one float4 of C.  Optional row sums (bias gradient): rowsum[m - m0]
-// += sum_z rws[z][m], spread over the grid.
+// phase 2 of the split-K GEMM: C = beta * C + sum_z partial[z] in a fixed order (deterministic:
+// partial z goes to accumulator z % 8, the eight are summed as a fixed tree; eight loads per
+// thread in flight).  Partials are dense [S][M][N]; each thread owns one float4 of C.  Optional
+// row sums (bias gradient): rowsum[m - m0] += sum_z rws[z][m], spread over the grid.
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, int M, int N, float* C, int ldc,
                                                        float beta, const float* rws, float* rowsum, int m0) {
   const int64_t MN = (int64_t)M * N;
@@ -612,35 +612,42 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
     }
   }
   if ((N & 3) == 0) {
+    // four lanes per float4 of C: lane g sums partials g, g + 4, g + 8, ... (eight loads in
+    // flight), then the four lane sums combine as (l0 + l1) + (l2 + l3)
+    constexpr int G = 4, U = 8;
     const int64_t Q = MN >> 2;
+    const int g = threadIdx.x & (G - 1);
     const float4* w4 = reinterpret_cast<const float4*>(ws);
-    for (int64_t q = gtid; q < Q; q += gsz) {
-      float4 a0 = w4[q], a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
-      int z = 1;
-      for (; z + 3 < S; z += 4) {
-        const float4 p0 = w4[(int64_t)z * Q + q], p1 = w4[(int64_t)(z + 1) * Q + q];
-        const float4 p2 = w4[(int64_t)(z + 2) * Q + q], p3 = w4[(int64_t)(z + 3) * Q + q];
-        a0.x += p0.x; a0.y += p0.y; a0.z += p0.z; a0.w += p0.w;
-        a1.x += p1.x; a1.y += p1.y; a1.z += p1.z; a1.w += p1.w;
-        a2.x += p2.x; a2.y += p2.y; a2.z += p2.z; a2.w += p2.w;
-        a3.x += p3.x; a3.y += p3.y; a3.z += p3.z; a3.w += p3.w;
+    for (int64_t q = gtid / G; q < Q; q += gsz / G) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z0 = g; z0 < S; z0 += G * U) {
+        float4 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int z = z0 + G * u;
+          p[u] = z < S ? w4[(int64_t)z * Q + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          a.x += p[u].x; a.y += p[u].y; a.z += p[u].z; a.w += p[u].w;
+        }
       }
-      for (; z < S; ++z) {
-        const float4 p = w4[(int64_t)z * Q + q];
-        a0.x += p.x; a0.y += p.y; a0.z += p.z; a0.w += p.w;
+      float4 b;
+      b.x = __shfl_xor(a.x, 1); b.y = __shfl_xor(a.y, 1); b.z = __shfl_xor(a.z, 1); b.w = __shfl_xor(a.w, 1);
+      if (g & 1) { const float4 t = a; a = b; b = t; }   // (even + odd) in both lanes, same order
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      b.x = __shfl_xor(a.x, 2); b.y = __shfl_xor(a.y, 2); b.z = __shfl_xor(a.z, 2); b.w = __shfl_xor(a.w, 2);
+      if (g & 2) { const float4 t = a; a = b; b = t; }
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      if (g == 0) {
+        const int64_t i = q << 2;
+        const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+        float* dst = C + (int64_t)m * ldc + n;
+        if (beta != 0.f) {
+          a.x += beta * dst[0]; a.y += beta * dst[1]; a.z += beta * dst[2]; a.w += beta * dst[3];
+        }
+        dst[0] = a.x; dst[1] = a.y; dst[2] = a.z; dst[3] = a.w;
       }
-      float4 acc;
-      acc.x = (a0.x + a1.x) + (a2.x + a3.x);
-      acc.y = (a0.y + a1.y) + (a2.y + a3.y);
-      acc.z = (a0.z + a1.z) + (a2.z + a3.z);
-      acc.w = (a0.w + a1.w) + (a2.w + a3.w);
-      const int64_t i = q << 2;
-      const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
-      float* dst = C + (int64_t)m * ldc + n;
-      if (beta != 0.f) {
-        acc.x += beta * dst[0]; acc.y += beta * dst[1]; acc.z += beta * dst[2]; acc.w += beta * dst[3];
-      }
-      dst[0] = acc.x; dst[1] = acc.y; dst[2] = acc.z; dst[3] = acc.w;
     }
     return;
   }
@@ -840,8 +847,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   } else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
   if (splits > 1) {
     const int64_t MN = (int64_t)N * K;
-    const int64_t units = (K % 4 == 0) ? MN / 4 : MN;
-    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 2048))),
+    const int64_t units = MN;   // scalar path: a thread per element; float4 path: four lanes per float4
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 4096))),
                        dim3(256), 0, s, ws, splits, N, K, dW, ldw, beta, a.rowsum_ws, db, db_n0);
   }
   XTRL_LAUNCHED("gemm_wgrad");
