@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 3
+#define XTRL_ABI_VERSION 4
 
 int xtrl_abi_version(void);
 const char* xtrl_last_error(void);
@@ -38,11 +38,12 @@ const char* xtrl_last_error(void);
  *   Y[m, n] = act( LN?(X)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])
  *   X [M][K] (ldx), W [N][K] (ldw, nn.Linear layout), Y [M][N] (ldy; Y += (*t_dev) * y_t_stride)
  *   ln_gamma != NULL -> X rows are layer-normalised (eps 1e-5, no beta) and scaled by gamma
- *   act: 0 none, 1 GELU(erf), 2 SiLU;  R may alias Y (in-place residual add)
+ *   act: 0 none, 1 GELU(erf), 2 SiLU, 3 ReLU;  R may alias Y (in-place residual add)
  * ------------------------------------------------------------------------------------------- */
 #define XTRL_ACT_NONE 0
 #define XTRL_ACT_GELU 1
 #define XTRL_ACT_SILU 2
+#define XTRL_ACT_RELU 3
 
 int xtrl_gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
                   const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M,
@@ -405,6 +406,35 @@ float xtrl_rng_normal(uint64_t seed, uint32_t update, uint32_t slot, uint32_t t,
 
 int xtrl_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const int32_t* episode_of_slot,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fractal encoder body (x_transformers_rl/fractal_rl.py FractalEncoder :137-346 and
+ * FractalWorldModelActorCritic.forward :549-619).  The reference composes x-transformers modules
+ * in Python; its matrix work maps to xtrl_gemm_f32 (Linear, act 3 = the ReLU of
+ * final_aggregation :235-239) and xtrl_attn_fwd_tokens (Attention, bidirectional: the
+ * FractalProcessingBlock self-attention :127-129); the rest is these row kernels.  The host side
+ * (xtrl_amd/fractal.py) mirrors the reference modules and their state_dict names.
+ * ------------------------------------------------------------------------------------------- */
+/* attention forward on token-major q/k/v (rows b*n + i, head h at columns h*dh, one row stride);
+ * causal = 0: key-padding mask only (keys j < lens[b]) */
+int xtrl_attn_fwd_tokens(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                         const int32_t* lens, float* o, int ldo, float* lse, int b, int H, int n, int dh, float scale,
+                         int causal, void* stream);
+/* y = x + v (v broadcast over rows; x NULL: y = v): level embedding add, fractal_rl.py:312-314 */
+int xtrl_rows_add(const float* x, int ldx, const float* v, float* y, int ldy, int M, int D, void* stream);
+/* y = LayerNorm(x + r) * gamma + beta (nn.LayerNorm, eps): post-norm blocks fractal_rl.py:127-136.
+ * Residual row m / r_rep (r_rep = n broadcasts one row per sequence: the cross-attention read of
+ * the one-token global state, whose softmax over a single key is exactly 1). r may be NULL. */
+int xtrl_add_layernorm(const float* x, int ldx, const float* r, int ldr, int r_rep, const float* gamma,
+                       const float* beta, float* y, int ldy, int M, int D, float eps, void* stream);
+/* y[b, :] = mean over the n rows of sequence b (einops reduce 'b n d -> b d', fractal_rl.py:321, :338) */
+int xtrl_seq_mean(const float* x, int ldx, int B, int n, int D, float* y, int ldy, void* stream);
+/* SafeEmbedding (x_transformers_rl.py:181-195): y[m] = actions[m] >= 0 ? W[actions[m]] : 0 */
+int xtrl_safe_embed(const int32_t* actions, int M, const float* W, int D, float* y, int ldy, void* stream);
+/* Continuous(raw).mean_variance (x_transformers_rl.py:224-241) -> mean_var [2][M][P];
+ * optional done = sigmoid(done_logit) (to_pred_done, fractal_rl.py:402-406) */
+int xtrl_wm_post(const float* raw, int ldr, int M, int P, float* mean_var, const float* done_logit, int ldd,
+                 float* done, void* stream);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,7 @@ struct AttnArgs {
   uint32_t thresh;    // keep iff word >= thresh (thresh = 0: no dropout)
   uint64_t seed;
   uint32_t offset;
+  int causal;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 #pragma unroll
   for (int d = 0; d < ND; ++d) o[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  const int last_key = min(min(q0 + TQ - 1, n - 1), len - 1);
+  const int last_key = min(min(a.causal ? q0 + TQ - 1 : n - 1, n - 1), len - 1);
   for (int kt = 0; kt * TK <= last_key; ++kt) {
     __syncthreads();
     for (int x = tid; x < TK * DH; x += 256) {
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
         const int j = kt * TK + 16 * sub + lr;
-        const bool ok = (j <= i) && (j < len);
+        const bool ok = (j <= i || !a.causal) && (j < len);
         sv[sub] = ok ? sacc[sub][r] * a.scale : -INFINITY;
         mx = fmaxf(mx, sv[sub]);
       }
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
   f32x4v dq[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) dq[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  const int last_key = min(min(q0 + TQ - 1, n - 1), len - 1);
+  const int last_key = min(min(a.causal ? q0 + TQ - 1 : n - 1, n - 1), len - 1);
   for (int kt = 0; kt * TK <= last_key; ++kt) {
     __syncthreads();
     for (int x = tid; x < TK * DH; x += 256) {
@@ -345,6 +346,7 @@ int fill_args(AttnArgs& a, const AttnProblem& p) {
   a.thresh = dropout_thresh(p.dropout);
   a.seed = p.seed;
   a.offset = p.offset;
+  a.causal = p.causal;
   return XTRL_OK;
 }
 
@@ -377,6 +379,7 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
   AttnArgs a{};
   if (int rc = fill_args(a, p)) return rc;
   XTRL_REQUIRE(q && k && v && o && lse && dout && dq && dk && dv && delta_ws, "attn_bwd: null operand");
+  XTRL_REQUIRE(p.causal, "attn_bwd: bidirectional attention is forward-only");
   a.Q = q;
   a.K = k;
   a.V = v;
@@ -428,4 +431,19 @@ extern "C" int xtrl_attn_bwd(const float* q, const float* k, const float* v, con
                              uint32_t offset, void* stream) {
   return xtrl::attn_bwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset), q, k, v, o,
                            lse, dout, dq, dk, dv, delta_ws, xtrl::as_stream(stream));
+}
+
+/* bidirectional / causal attention forward on token-major operands (rows b * n + i, head h at
+ * columns h * dh): q, k, v with row strides ldq / ldk / ldv, out o [b * n][ldo]. */
+extern "C" int xtrl_attn_fwd_tokens(const float* q, int ldq, const float* k, int ldk, const float* v, int ldv,
+                                    const int32_t* lens, float* o, int ldo, float* lse, int b, int H, int n, int dh,
+                                    float scale, int causal, void* stream) {
+  XTRL_REQUIRE(ldq == ldk && ldk == ldv, "attn_fwd_tokens: q, k, v share one row stride (got %d %d %d)", ldq, ldk,
+               ldv);
+  xtrl::AttnProblem pr{b, H, n, dh, lens, scale, 0.f, 0, 0, {}, {}, {}, {}};
+  pr.in = xtrl::attn_layout_tokens(n, ldq, dh);
+  pr.out = xtrl::attn_layout_tokens(n, ldo, dh);
+  pr.causal = causal;
+  // q, k, v are addressed from their own bases with the same layout
+  return xtrl::attn_fwd_ex(pr, q, k, v, o, lse, nullptr, nullptr, (hipStream_t)stream);
 }

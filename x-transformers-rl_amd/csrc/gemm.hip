@@ -539,6 +539,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
           float aux_o = 0.f;
           if constexpr (EPI == EPI_GELU) v = geluf_(v);
           if constexpr (EPI == EPI_SILU) v = siluf_(v);
+          if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
           if constexpr (EPI == EPI_GELU_DROP) {   // torch GELU (erf) and GeluBackward's factor
             const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
             const float pdf = 0.3989422804014327f * expf(v * v * -0.5f);
@@ -769,6 +770,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   XG(0, 0, EPI_GELU, true, false)
   XG(0, 0, EPI_GELU, false, false)
   XG(0, 0, EPI_SILU, false, false)
+  XG(0, 0, EPI_RELU, false, false)
   XG(0, 0, EPI_GELU_DROP, false, false)
   XG(0, 0, EPI_SILU_SAVE, false, false)
   // dgrad (B = weight used as [k][n]) with fused activation / dropout / gate backward
@@ -786,7 +788,8 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
 int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, int ldb, const float* bias,
             const float* ln_gamma, const float* R, int ldr, float* C, int ldc, const int32_t* t_dev,
             int64_t c_t_stride, int M, int N, int K, int act, float beta, hipStream_t s) {
-  XTRL_REQUIRE(act >= 0 && act <= 2, "gemm: bad activation %d", act);
+  XTRL_REQUIRE(act >= 0 && act <= 3, "gemm: bad activation %d", act);
+  if (act == 3) act = EPI_RELU;
   GemmArgs a;
   a.A = A; a.B = B; a.bias = bias; a.gamma = ln_gamma; a.R = R; a.C = C; a.t_dev = t_dev;
   a.c_t_stride = c_t_stride; a.lda = lda; a.ldb = ldb; a.ldr = ldr; a.ldc = ldc; a.M = M; a.N = N; a.K = K;

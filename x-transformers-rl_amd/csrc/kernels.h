@@ -20,6 +20,7 @@ enum GemmEpi : int {
   EPI_GELU_DROP = 3,   // C = drop(gelu(v)); aux_out = drop(gelu'(v))   (drop: keep ? x / (1 - p) : 0)
   EPI_SILU_SAVE = 4,   // n < act_cols: C = silu(v), aux_out = silu'(v);  else C = v, aux_out = 1
   EPI_MUL_AUX = 5,     // C = v * aux_in                                 (dgrad through a saved derivative)
+  EPI_RELU = 8,        // max(v, 0)   (fractal encoder final aggregation, fractal_rl.py:235-239)
   EPI_DGATE = 7,       // s = sigmoid(aux_in2): C = v * s; aux_out = v * aux_in * (1 - s) * s   (value gate)
 };
 
@@ -102,6 +103,7 @@ struct AttnProblem {
   uint32_t offset;
   AttnLayout in, out, grad;   // q/k/v; o/do (and og); dq/dk/dv
   AttnLayout gate;            // gate pre-activations (x-transformers attn_gate_values)
+  int causal = 1;             // 0: bidirectional (key-padding mask only; forward only)
 };
 
 // o (ungated) and lse; if gate != nullptr also og = o * sigmoid(gate) (og in the `out` layout)

@@ -13,12 +13,12 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
 
-ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU = 0, 1, 2, 3
 
 # stats[] slots of the fused loss (XTRL_LS_*)
 LS = dict(loss=0, actor=1, critic=2, autoreg=3, done=4, adv_mean=5, adv_den=6, L=7, Lc=8, nmask=9, nwm=10,
@@ -118,6 +118,12 @@ SIGNATURES = {
     'xtrl_ff_dropout_mask': (I32, [P, I32, I32, F32, U64, U32, P]),
     'xtrl_minibatch_gather': (I32, [C.POINTER(BatchDesc), P]),
     'xtrl_rsnorm_update': (I32, [P, P, P, I32, I32, P]),
+    'xtrl_attn_fwd_tokens': (I32, [P, I32, P, I32, P, I32, P, P, I32, P, I32, I32, I32, I32, F32, I32, P]),
+    'xtrl_rows_add': (I32, [P, I32, P, P, I32, I32, I32, P]),
+    'xtrl_add_layernorm': (I32, [P, I32, P, I32, I32, P, P, P, I32, I32, I32, F32, P]),
+    'xtrl_seq_mean': (I32, [P, I32, I32, I32, I32, P, I32, P]),
+    'xtrl_safe_embed': (I32, [P, I32, P, I32, P, I32, P]),
+    'xtrl_wm_post': (I32, [P, I32, I32, I32, P, P, I32, P, P]),
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
 }
