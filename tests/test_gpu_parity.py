@@ -93,6 +93,31 @@ def test_gemm_large_tile_split_bf16_accuracy(layout):
     assert err < 7 * 2.0 ** -24, f'{layout}: max error {err / 2.0 ** -24:.2f} x 2^-24 of sum |a b|'
 
 
+@pytest.mark.parametrize('K', [257, 18, 3])
+def test_gemm_ragged_extent_padded_rows(K):
+    """Operands whose contiguous extent is not a multiple of 4 but whose rows are padded to one
+    (the world-model head's d + 1 columns in a d + 4 row) take the float4 path: quads straddling
+    the extent read in-bounds padding that the tail mask zeroes (K) or the epilogue discards."""
+    from xtrl_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(K)
+    M, N, ld = 4100, 260, (K + 3) // 4 * 4 + 4
+    a = torch.randn(M, ld, generator=g)
+    a[:, K:] = 1e30                                   # garbage in the padding columns
+    b = torch.randn(K, N, generator=g)
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm_ex(a.to(DEV)[:, :K], b.to(DEV), 0, 1, M, N, K, out)   # dgrad layout, K ragged
+    ad, bd = a[:, :K].double(), b.double()
+    torch.cuda.synchronize()
+    assert float(((out.double().cpu() - ad @ bd).abs() / _dot_scale(ad, bd)).max()) < 1e-6
+    # weight gradient with a ragged output dimension N' = K: dW[K][N] = dY[:, :K]^T X
+    x = torch.randn(M, N, generator=g).double()
+    dw = torch.zeros(K, N, device=DEV)
+    ws = torch.empty(32 << 20, device=DEV)
+    ops.wgrad(a.to(DEV)[:, :K], x.float().to(DEV), dw, ws, beta=0.)
+    torch.cuda.synchronize()
+    assert float(((dw.double().cpu() - ad.t() @ x).abs() / _dot_scale(ad.t(), x)).max()) < 1e-6
+
+
 # ----------------------------------------------------------------------------------------------
 # training attention
 # ----------------------------------------------------------------------------------------------

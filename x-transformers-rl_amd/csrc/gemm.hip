@@ -188,7 +188,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
     const float* row = base + (int64_t)min(outer, outer_lim - 1) * ld;
     float4 f;
     if constexpr (VEC) {
-      f = *reinterpret_cast<const float4*>(row + min(inner, inner_lim - 4));
+      // quads are clamped into the row's 4-aligned extent (the leading dimension covers it, see
+      // gemm_run): a quad straddling the end of the contiguous extent reads in-bounds padding,
+      // zeroed by the tail mask when that extent is K and discarded by the epilogue otherwise
+      f = *reinterpret_cast<const float4*>(row + min(inner, ((inner_lim + 3) & ~3) - 4));
     } else {
       f.x = row[min(inner + 0, inner_lim - 1)];
       f.y = row[min(inner + 1, inner_lim - 1)];
@@ -739,6 +742,7 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+int round4(int x) { return (x + 3) & ~3; }
 
 }  // namespace
 
@@ -754,8 +758,11 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
                "gemm: epilogue %d needs aux_in", epi);
   XTRL_REQUIRE(!(epi == EPI_DGATE && !a.aux_in2), "gemm: gate epilogue needs aux_in2");
   if (a.M == 0 || a.N == 0) return XTRL_OK;
+  // float4 staging: 16-byte aligned operands whose leading dimensions are multiples of 4 and cover
+  // the contiguous extent rounded up to 4 (a ragged extent such as K = d + 1 then reads in-bounds
+  // padding of the row; see load4)
   const bool vec = aligned16(a.A) && aligned16(a.B) && (a.lda % 4 == 0) && (a.ldb % 4 == 0) &&
-                   ((trans_a ? a.M : a.K) % 4 == 0) && ((trans_b ? a.N : a.K) % 4 == 0);
+                   a.lda >= round4(trans_a ? a.M : a.K) && a.ldb >= round4(trans_b ? a.N : a.K);
   const bool ln = a.gamma != nullptr, res = a.R != nullptr;
 #define XG(TA_, TB_, E_, L_, R_)                                                                   \
   if (trans_a == TA_ && trans_b == TB_ && epi == E_ && ln == L_ && res == R_) {                    \
@@ -822,7 +829,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
     kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
     splits = (M + kspan - 1) / kspan;
   }
-  const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0) && (N % 4 == 0) && (K % 4 == 0);
+  const bool vec = aligned16(dY) && aligned16(X) && (ldy % 4 == 0) && (ldx % 4 == 0) && ldy >= round4(N) &&
+                   ldx >= round4(K);
   GemmArgs a;
   a.A = dY; a.B = X; a.C = dW; a.lda = ldy; a.ldb = ldx; a.ldc = ldw; a.M = N; a.N = K; a.K = M; a.beta = beta;
   a.rowsum = db;
