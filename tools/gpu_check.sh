@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out
 what=${1:-all}; shift || true
 run_tests() {
-  timeout -k 10 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout=300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
   rc=$?; tail -15 gpurun_out/gpu_tests.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 }
