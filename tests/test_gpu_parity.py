@@ -177,6 +177,43 @@ def test_attention_dropout_consistent():
     assert abs(float(o0.mean()) - 1.0) < 0.05
 
 
+def test_attention_dropout_mask_is_host_philox_stream():
+    """The kept attention probabilities are exactly the host Philox stream's (oracle/philox.py):
+    keep(b, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + b H + h, FIELD_DROPOUT << 24; seed)
+    >= p 2^32.  Forward against a double reference that applies that mask after the softmax, and
+    q / k / v gradients against its autograd (the backward kernels draw the same words, grouped
+    differently: one Philox block per 4 rows, dealt out by a quad transpose in dK / dV)."""
+    from xtrl_amd import ops
+    from oracle import philox as P
+    g = torch.Generator().manual_seed(9)
+    b, H, n, dh = 2, 2, 70, 16
+    q, k, v, do = (torch.randn(b, H, n, dh, generator=g) for _ in range(4))
+    lens = torch.tensor([70, 45], dtype=torch.int32)
+    p, seed, offset, scale = 0.25, 1234567, 5, dh ** -0.5
+    thresh = np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
+    i, j = np.arange(n)[:, None], np.arange(n)[None, :]
+    keep = np.zeros((b, H, n, n), dtype=bool)
+    for bb in range(b):
+        for hh in range(H):
+            words = P.philox4x32(i >> 2, j, offset + bb * H + hh, P._c3(P.FIELD_DROPOUT, 0), seed)
+            keep[bb, hh] = np.choose(np.broadcast_to(i & 3, (n, n)), [np.broadcast_to(w, (n, n)) for w in words]) >= thresh
+    keep_t = torch.from_numpy(keep).double() / (1 - p)
+    qd, kd, vd = (t.double().requires_grad_() for t in (q, k, v))
+    s = torch.einsum('bhid,bhjd->bhij', qd, kd) * scale
+    ii = torch.arange(n)
+    valid = (ii[None, :] <= ii[:, None])[None, None] & (ii[None, None, None, :] < lens.long()[:, None, None, None])
+    ref = torch.einsum('bhij,bhjd->bhid', s.masked_fill(~valid, float('-inf')).softmax(-1) * keep_t, vd)
+    (ref * do.double()).sum().backward()
+    qf, kf, vf = (t.to(DEV).requires_grad_() for t in (q, k, v))
+    out = ops.attention(qf, kf, vf, lens.to(DEV), scale, p, seed=seed, offset=offset)
+    (out * do.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    tol(out, ref, 1e-5, 1e-5)
+    tol(qf.grad, qd.grad, 1e-4, 1e-5)
+    tol(kf.grad, kd.grad, 1e-4, 1e-5)
+    tol(vf.grad, vd.grad, 1e-4, 1e-5)
+
+
 # ----------------------------------------------------------------------------------------------
 # rollout (decode step, sampling, synthetic Sim) vs the oracle's batch-1 reference loop
 # ----------------------------------------------------------------------------------------------

@@ -28,6 +28,9 @@ __device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, int i
   const int w = i & 3;
   return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
 }
+__device__ __forceinline__ uint32_t qword(const u32x4_t& u, int r) {
+  return r == 0 ? u.x : (r == 1 ? u.y : (r == 2 ? u.z : u.w));
+}
 
 struct AttnArgs {
   const float *Q, *K, *V, *O, *LSE, *dO, *Dl, *G;
@@ -90,6 +93,15 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) sacc[sub] = mfma16(qa[s], Ks[16 * sub + lr][4 * s + lg], sacc[sub]);
     }
+    // keep words: this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block per key column
+    // (word = row & 3), so one block per column instead of one per element
+    u32x4_t kws[4] = {};
+    if (a.thresh) {
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub)
+        kws[sub] = philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)(kt * TK + 16 * sub + lr), off,
+                                 rng_c3(FIELD_DROPOUT, 0), a.seed);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = q0 + 16 * w + 4 * lg + r;
@@ -112,10 +124,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
         const float p = (sv[sub] == -INFINITY) ? 0.f : expf(sv[sub] - mnew);
         rs += p;
         float pd = p;
-        if (a.thresh) {
-          const int j = kt * TK + 16 * sub + lr;
-          pd = (keep_word(a.seed, off, i, j) >= a.thresh) ? p * a.inv_keep : 0.f;
-        }
+        if (a.thresh) pd = (qword(kws[sub], r) >= a.thresh) ? p * a.inv_keep : 0.f;
         Ps[w][4 * lg + r][16 * sub + lr] = pd;
       }
 #pragma unroll
@@ -215,13 +224,26 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
           dpt = mfma16(va[s], dOs[16 * sub + lr][4 * s + lg], dpt);
         }
         const int il = 16 * sub + lr, i = qt * TQ + il;
+        // keep words of row i at key columns j0 + 16 w + 4 lg + 0..3: the four lanes of a quad hold
+        // rows 4 (i >> 2) + 0..3; lane c computes the block of column 4 lg + c (its four words are
+        // the quad's four rows) and a quad transpose hands every lane its row's word of each column
+        uint32_t kq[4] = {0u, 0u, 0u, 0u};
+        if (a.thresh) {
+          const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)(j0 + 16 * w + 4 * lg + (lr & 3)), off,
+                                           rng_c3(FIELD_DROPOUT, 0), a.seed);
+          kq[0] = kb.x;
+          kq[1] = kb.y;
+          kq[2] = kb.z;
+          kq[3] = kb.w;
+          quad_transpose(kq, lane);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = j0 + 16 * w + 4 * lg + r;
           const bool ok = (j <= i) && (j < len) && (i < n);
           const float p = ok ? expf(st[r] * a.scale - Ls[il]) : 0.f;
           float z = 1.f;
-          if (a.thresh && ok) z = (keep_word(a.seed, off, i, j) >= a.thresh) ? a.inv_keep : 0.f;
+          if (a.thresh && ok) z = (kq[r] >= a.thresh) ? a.inv_keep : 0.f;
           Ps[w][4 * lg + r][il] = p * z;
           Ds[w][4 * lg + r][il] = p * (dpt[r] * z - Dls[il]);
         }
@@ -303,13 +325,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
         dp = mfma16(da[s], Vs[16 * sub + lr][4 * s + lg], dp);
       }
       const int jl = 16 * sub + lr, j = kt * TK + jl;
+      // this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block (word = row & 3)
+      const u32x4_t kw = a.thresh ? philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)j, off,
+                                                  rng_c3(FIELD_DROPOUT, 0), a.seed)
+                                  : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = q0 + 16 * w + 4 * lg + r;
         const bool ok = (j <= i) && (j < len) && (i < n);
         const float p = ok ? expf(s_[r] * a.scale - lse[r]) : 0.f;
         float z = 1.f;
-        if (a.thresh && ok) z = (keep_word(a.seed, off, i, j) >= a.thresh) ? a.inv_keep : 0.f;
+        if (a.thresh && ok) z = (qword(kw, r) >= a.thresh) ? a.inv_keep : 0.f;
         Ds[w][4 * lg + r][jl] = p * (dp[r] * z - dl[r]);
       }
     }

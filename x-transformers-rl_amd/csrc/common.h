@@ -53,6 +53,35 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// 4 x 4 transpose across the four lanes of a quad (lanes with equal lane >> 2): on entry lane
+// c = lane & 3 holds column c of the block (x[q] = element (q, c)), on exit its row c
+// (x[k] = element (c, k)).  Two exchange stages: lane ^ 2 swaps the off-diagonal 2 x 2 blocks,
+// lane ^ 1 transposes each 2 x 2 block.
+template <typename T>
+__device__ __forceinline__ void quad_transpose(T (&x)[4], int lane) {
+  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+  T s0 = b1 ? x[0] : x[2], s1 = b1 ? x[1] : x[3];
+  T r0 = __shfl_xor(s0, 2, kWave), r1 = __shfl_xor(s1, 2, kWave);
+  if (b1) {
+    x[0] = r0;
+    x[1] = r1;
+  } else {
+    x[2] = r0;
+    x[3] = r1;
+  }
+  s0 = b0 ? x[0] : x[1];
+  s1 = b0 ? x[2] : x[3];
+  r0 = __shfl_xor(s0, 1, kWave);
+  r1 = __shfl_xor(s1, 1, kWave);
+  if (b0) {
+    x[0] = r0;
+    x[2] = r1;
+  } else {
+    x[1] = r0;
+    x[3] = r1;
+  }
+}
+
 // LDS hand-off between lanes of ONE wave (no workgroup barrier: waves of a block may have exited)
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -43,14 +43,256 @@ namespace {
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// x = hi + mid + lo exactly (round-to-nearest bf16 of the running remainder; exact subtractions)
+// x = hi + mid + lo exactly (round-to-nearest bf16 of the running remainder; exact subtractions).
+// Written on packed pairs: one v_cvt_pk_bf16_f32 per pair and level, the pieces widened back to
+// f32 by a shift (low half) / mask (high half) — 4.5 VALU per value instead of the ~7.7 the
+// vector-convert form compiled to.
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+}
+// (scalar v_sub_f32 in asm: left to itself the compiler pairs the subtractions into v_pk_add_f32
+// plus register moves, slower beside MFMAs)
+__device__ __forceinline__ float sub_f32(float a, float b) { return a - b; }
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pk_bf16(a, b);
+  const float ra = sub_f32(a, __builtin_bit_cast(float, h << 16));
+  const float rb = sub_f32(b, __builtin_bit_cast(float, h & 0xffff0000u));
+  m = pk_bf16(ra, rb);
+  const float sa = sub_f32(ra, __builtin_bit_cast(float, m << 16));
+  const float sb = sub_f32(rb, __builtin_bit_cast(float, m & 0xffff0000u));
+  l = pk_bf16(sa, sb);
+}
 __device__ __forceinline__ void split3(float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
-  const f32x4 x{v.x, v.y, v.z, v.w};
-  h = __builtin_convertvector(x, bf16x4);
-  const f32x4 r1 = x - __builtin_convertvector(h, f32x4);
-  m = __builtin_convertvector(r1, bf16x4);
-  const f32x4 r2 = r1 - __builtin_convertvector(m, f32x4);
-  l = __builtin_convertvector(r2, bf16x4);
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split3_pair(v.x, v.y, h0, m0, l0);
+  split3_pair(v.z, v.w, h1, m1, l1);
+  h = __builtin_bit_cast(bf16x4, make_uint2(h0, h1));
+  m = __builtin_bit_cast(bf16x4, make_uint2(m0, m1));
+  l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
+}
+
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+__device__ __forceinline__ float f4c(const float4& v, int k) {
+  return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+// the row-vector epilogue applies when every row segment it reads or writes is a 16-byte aligned float4
+template <int EPI, bool RES>
+__device__ __forceinline__ bool epi_v4_ok(const GemmArgs& a, const float* C) {
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE), AUX2 = (EPI == EPI_DGATE);
+  constexpr bool AOUT = (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE);
+  bool ok = (a.N & 3) == 0 && (a.ldc & 3) == 0 && al16(C);
+  if constexpr (RES) ok = ok && (a.ldr & 3) == 0 && al16(a.R);
+  if constexpr (AUX1) ok = ok && (a.ld_aux_in & 3) == 0 && al16(a.aux_in);
+  if constexpr (AUX2) ok = ok && (a.ld_aux_in2 & 3) == 0 && al16(a.aux_in2);
+  if constexpr (AOUT) ok = ok && (a.ld_aux_out & 3) == 0 && al16(a.aux_out);
+  return ok;
+}
+
+// Row-vector epilogue.  The element-wise stage that reads no operand (bias, activation, dropout,
+// saved derivative) runs in the MFMA layout — one Philox block still covers a column's four rows —
+// then a quad transpose gives every lane four consecutive columns of one row, so the operand reads
+// (saved derivative, gate, residual, old C) and the stores are float4: 4 store instructions per
+// 32 x 32 tile and output instead of 16 (the scalar tail was store-issue bound).  Per element the
+// same operations in the same order as the scalar form below.
+template <int TM, int TN, int EPI, bool RES>
+__device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc)[TM][TN], float* C, int m0, int n0,
+                                                 int wm, int wn, int lane) {
+  const int M = a.M, N = a.N;
+  const bool acc_c = a.beta != 0.f;
+  constexpr bool DROP = (EPI == EPI_GELU_DROP);
+  constexpr bool SAVE = (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE), AUX2 = (EPI == EPI_DGATE);
+  const int c4 = lane & 3;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);              // MFMA layout column
+    const int nv = n0 + wn * 32 * TN + 32 * j + 4 * ((lane & 31) >> 2);  // row-vector first column
+    const int nvc = nv < N ? nv : N - 4;
+    const bool nok = n < N;
+    const float bn = (a.bias && nok && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
+    const bool act = n < a.act_cols;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
+      float v[4][4], ax[4][4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x4_t kw{0u, 0u, 0u, 0u};
+        if (DROP && a.drop_thresh)
+          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
+                             a.seed);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float x = acc[i][j][4 * g + q] + bn;
+          float aux_o = 0.f;
+          const uint32_t word = q == 0 ? kw.x : (q == 1 ? kw.y : (q == 2 ? kw.z : kw.w));
+          if constexpr (EPI == EPI_GELU) x = geluf_(x);
+          if constexpr (EPI == EPI_SILU) x = siluf_(x);
+          if constexpr (EPI == EPI_RELU) x = fmaxf(x, 0.f);
+          if constexpr (EPI == EPI_GELU_DROP) {   // torch GELU (erf) and GeluBackward's factor
+            const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+            const float pdf = 0.3989422804014327f * expf(x * x * -0.5f);
+            aux_o = cdf + x * pdf;
+            x = (0.5f * x) * (1.0f + erff(x * 0.70710678118654752f));
+            if (a.drop_thresh) {
+              const bool keep = word >= a.drop_thresh;
+              x = keep ? x * a.inv_keep : 0.f;
+              aux_o = keep ? aux_o * a.inv_keep : 0.f;
+            }
+          }
+          if constexpr (EPI == EPI_SILU_SAVE) {
+            if (act) {
+              const float sg = 1.0f / (1.0f + expf(-x));
+              aux_o = sg * (1.0f + x * (1.0f - sg));
+              x = x / (1.0f + expf(-x));
+            } else {
+              aux_o = 1.0f;
+            }
+          }
+          v[g][q] = x;
+          ax[g][q] = aux_o;
+        }
+        quad_transpose(v[g], lane);
+        if constexpr (SAVE) quad_transpose(ax[g], lane);
+      }
+      // row-vector stage: this lane holds row mb + 8 g + (lane & 3), columns nv .. nv + 3; every
+      // operand read comes before the stores (which may alias them as far as the compiler knows)
+      float4 x1[4], x2[4], rr[4], old[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int m = mb + 8 * g + c4, mc = m < M ? m : M - 1;
+        if constexpr (AUX1) x1[g] = *reinterpret_cast<const float4*>(a.aux_in + (int64_t)mc * a.ld_aux_in + nvc);
+        if constexpr (AUX2) x2[g] = *reinterpret_cast<const float4*>(a.aux_in2 + (int64_t)mc * a.ld_aux_in2 + nvc);
+        if constexpr (RES) rr[g] = *reinterpret_cast<const float4*>(a.R + (int64_t)mc * a.ldr + nvc);
+        old[g] = acc_c ? *reinterpret_cast<const float4*>(C + (int64_t)mc * a.ldc + nvc)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int m = mb + 8 * g + c4;
+        float o[4], ao[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float x = v[g][k];
+          float aux_o = SAVE ? ax[g][k] : 0.f;
+          if constexpr (EPI == EPI_MUL_AUX) x = x * f4c(x1[g], k);
+          if constexpr (EPI == EPI_DGATE) {
+            const float sg = sigmoidf_(f4c(x2[g], k));
+            aux_o = (x * f4c(x1[g], k)) * (1.0f - sg) * sg;
+            x = x * sg;
+          }
+          if constexpr (RES) x = x + f4c(rr[g], k);
+          if (acc_c) x = a.beta * f4c(old[g], k) + x;
+          o[k] = x;
+          ao[k] = aux_o;
+        }
+        if (m < M && nv < N && (!a.row_mask || a.row_mask[m])) {
+          *reinterpret_cast<float4*>(C + (int64_t)m * a.ldc + nv) = make_float4(o[0], o[1], o[2], o[3]);
+          if constexpr (SAVE || EPI == EPI_DGATE)
+            *reinterpret_cast<float4*>(a.aux_out + (int64_t)m * a.ld_aux_out + nv) =
+                make_float4(ao[0], ao[1], ao[2], ao[3]);
+        }
+      }
+    }
+  }
+}
+
+// scalar epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 of the wave's 32 x 32
+// tile (i, j); bias / activation / saved derivative / gate / residual / beta, then the stores
+template <int TM, int TN, int EPI, bool RES>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
+                                              int wn, int lane, int bz) {
+  const int M = a.M, N = a.N;
+  float* C = a.C;
+  if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
+  if (a.kspan > 0) C += bz * a.c_split;
+  if (epi_v4_ok<EPI, RES>(a, C)) {
+    gemm_epilogue_v4<TM, TN, EPI, RES>(a, acc, C, m0, n0, wm, wn, lane);
+    return;
+  }
+  const bool acc_c = a.beta != 0.f;
+  constexpr bool DROP = (EPI == EPI_GELU_DROP);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE);
+  constexpr bool AUX2 = (EPI == EPI_DGATE);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);
+    const bool nok = n < N;
+    const int nc = nok ? n : N - 1;
+    const float bn = (a.bias && nok && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
+    const bool act = n < a.act_cols;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
+      // all reads of this lane's 16 elements first (aux inputs, residual, old C): the stores below
+      // may alias them as far as the compiler knows, so interleaving would serialise every access
+      float x1[16], x2[16], rr[16], old[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + (r & 3) + 8 * (r >> 2);
+        const int mc = m < M ? m : M - 1;
+        if constexpr (AUX1) x1[r] = a.aux_in[(int64_t)mc * a.ld_aux_in + nc];
+        if constexpr (AUX2) x2[r] = a.aux_in2[(int64_t)mc * a.ld_aux_in2 + nc];
+        if constexpr (RES) rr[r] = a.R[(int64_t)mc * a.ldr + nc];
+        old[r] = acc_c ? C[(int64_t)mc * a.ldc + nc] : 0.f;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        // rows mb + 8g + 0..3 (a 4-aligned group): one Philox block gives their four keep words
+        u32x4_t kw{0u, 0u, 0u, 0u};
+        if (DROP && a.drop_thresh)
+          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
+                             a.seed);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * g + q;
+          const int m = mb + 8 * g + q;
+          float v = acc[i][j][r] + bn;
+          const uint32_t word = q == 0 ? kw.x : (q == 1 ? kw.y : (q == 2 ? kw.z : kw.w));
+          float aux_o = 0.f;
+          if constexpr (EPI == EPI_GELU) v = geluf_(v);
+          if constexpr (EPI == EPI_SILU) v = siluf_(v);
+          if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+          if constexpr (EPI == EPI_GELU_DROP) {   // torch GELU (erf) and GeluBackward's factor
+            const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
+            const float pdf = 0.3989422804014327f * expf(v * v * -0.5f);
+            aux_o = cdf + v * pdf;
+            v = (0.5f * v) * (1.0f + erff(v * 0.70710678118654752f));
+            if (a.drop_thresh) {
+              const bool keep = word >= a.drop_thresh;
+              v = keep ? v * a.inv_keep : 0.f;
+              aux_o = keep ? aux_o * a.inv_keep : 0.f;
+            }
+          }
+          if constexpr (EPI == EPI_SILU_SAVE) {
+            if (act) {
+              const float sg = 1.0f / (1.0f + expf(-v));
+              aux_o = sg * (1.0f + v * (1.0f - sg));
+              v = v / (1.0f + expf(-v));
+            } else {
+              aux_o = 1.0f;
+            }
+          }
+          if constexpr (EPI == EPI_MUL_AUX) v = v * x1[r];
+          if constexpr (EPI == EPI_DGATE) {
+            const float sg = sigmoidf_(x2[r]);
+            aux_o = (v * x1[r]) * (1.0f - sg) * sg;
+            v = v * sg;
+          }
+          if constexpr (RES) v = v + rr[r];
+          if (acc_c) v = a.beta * old[r] + v;
+          if (nok && m < M && (!a.row_mask || a.row_mask[m])) {
+            C[(int64_t)m * a.ldc + n] = v;
+            if constexpr (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE)
+              a.aux_out[(int64_t)m * a.ld_aux_out + n] = aux_o;
+          }
+        }
+      }
+    }
+  }
 }
 
 template <int WM, int WN, int WK, int TM, int TN, bool TA, bool TB, int EPI, bool LN, bool RES, bool VEC,
@@ -358,16 +600,18 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
     // fragments double-buffered: the reads of k-step s + 1 fly across k-step s's MFMAs
     constexpr int FB = 2;
     bf16x8 av[FB][3][TM], bv[FB][3][TN];
-    auto rd = [&](int buf, int st) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
+    auto rd = [&](int buf, int st) {   // in the order the products consume them (see k_gemm_ws)
+      auto ra_ = [&](int p) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           av[buf][p][i] = *reinterpret_cast<const bf16x8*>(xa + (p * BM + xi + 32 * i) * XRS + 16 * st + xk);
+      };
+      auto rb_ = [&](int p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           bv[buf][p][j] = *reinterpret_cast<const bf16x8*>(xb + (p * BN + xj + 32 * j) * XRS + 16 * st + xk);
-      }
+      };
+      ra_(2); rb_(0); ra_(0); rb_(2); ra_(1); rb_(1);
     };
     if constexpr (FB == 2) rd(0, 0);
 #pragma unroll
@@ -496,90 +740,269 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
     }
   }
 
-  // ---- epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 -------------
-  float* C = a.C;
-  if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
-  if (a.kspan > 0) C += bz * a.c_split;
-  const bool acc_c = a.beta != 0.f;
-  constexpr bool DROP = (EPI == EPI_GELU_DROP);
-  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE);
-  constexpr bool AUX2 = (EPI == EPI_DGATE);
+  gemm_epilogue<TM, TN, EPI, RES>(a, acc, m0, n0, wm, wn, lane, bz);
+}
+
+#ifdef XTRL_WS_DIAG   // tools/ws_lab.hip: per-step s_memtime stamps of waves 0 and 4 of every workgroup
+__device__ uint64_t* g_ws_diag;
+__device__ int g_ws_mode;   // 1: consumers skip the MFMAs; 2: producers skip loads + splits; 3: skip splits
+#define WS_STAMP(step, k)                                                                         \
+  do {                                                                                            \
+    if ((tid & 255) == 0)                                                                         \
+      g_ws_diag[((int64_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 2 +   \
+                 (tid >> 8)) * 4096 + (step) * 4 + (k)] = __builtin_amdgcn_s_memtime();           \
+  } while (0)
+#else
+#define WS_STAMP(step, k) do {} while (0)
+#endif
+
+// ---- X6 warp-specialised GEMM (the 128 x 128 large-tile path) ----------------------------------
+// 8 waves per workgroup, one workgroup per CU.  Waves 0-3 (one per SIMD) are consumers: each owns
+// 64 x 64 of the tile and only reads piece fragments from LDS and issues bf16 MFMAs.  Waves 4-7
+// (their SIMD partners) are producers: they keep two fp32 slabs in flight global -> registers,
+// split each staged value into its hi / mid / lo pieces and write the piece images the consumers
+// read next.  Two piece images (double buffered), one barrier per 32-deep K slab: the consumers
+// never wait on global memory, and the producers' split arithmetic issues in the gaps of their
+// partner's MFMAs.  Requires K (and the split span) to be a multiple of 32 and float4 operands.
+template <bool TA, bool TB, int EPI, bool RES>
+__global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 32, XRS = BK + 8, NP = 256, TM = 2, TN = 2;
+  constexpr int A_F4 = BM * BK / 4 / NP, B_F4 = BN * BK / 4 / NP;   // float4 per producer thread per slab
+  constexpr int IMG = 3 * (BM + BN) * XRS;                           // bf16 per piece image
+  static_assert(A_F4 == 4 && B_F4 == 4, "one 4 x 4 transposed group per operand per producer thread");
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool producer = wave >= 4;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_remap) {   // as k_gemm: each XCD runs a contiguous range of tiles (column tile fastest)
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int total = nx * ny * gridDim.z;
+    const int lin = bx + nx * (by + ny * bz);
+    const int lg = (lin & 7) * (total >> 3) + (lin >> 3);
+    bx = lg % nx;
+    by = (lg / nx) % ny;
+    bz = lg / (nx * ny);
+  }
+  const int m0 = by * BM, n0 = bx * BN;
+  const int M = a.M, N = a.N;
+  int K = a.K;
+  const float* __restrict__ Ab = a.A;
+  const float* __restrict__ Bb = a.B;
+  if (a.kspan > 0) {
+    const int kb = bz * a.kspan;
+    K = min(a.kspan, a.K - kb);
+    Ab += TA ? (int64_t)kb * a.lda : kb;
+    Bb += TB ? (int64_t)kb * a.ldb : kb;
+  }
+  const int nk = K / BK;
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  // ---- producer state: two register sets of one slab each ----
+  const int p = tid - 256;
+  float4 ra[2][A_F4], rb[2][B_F4];
+  const bool do_rs = a.rowsum != nullptr && bx == 0;   // bias gradient (TA only, see gemm_run)
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  // operand element loads, clamped into the operand (rows / columns past M / N feed only outputs
+  // the epilogue discards; K is whole slabs)
+  auto ld_n = [&](const float* base, int64_t ld, int row, int row_lim, int k) -> float4 {   // [row][k]
+    return *reinterpret_cast<const float4*>(base + (int64_t)min(row, row_lim - 1) * ld + k);
+  };
+  auto ld_t = [&](const float* base, int64_t ld, int k, int col, int col_lim) -> float4 {   // [k][col]
+    return *reinterpret_cast<const float4*>(base + (int64_t)k * ld + min(col, ((col_lim + 3) & ~3) - 4));
+  };
+  auto load = [&](auto S, int kt) {
+    const int k0 = min(kt, nk - 1) * BK;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * 32 * TN + 32 * j + (lane & 31);
-    const bool nok = n < N;
-    const int nc = nok ? n : N - 1;
-    const float bn = (a.bias && nok && n >= a.bias_col0) ? a.bias[n - a.bias_col0] : 0.f;
-    const bool act = n < a.act_cols;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
-      // all reads of this lane's 16 elements first (aux inputs, residual, old C): the stores below
-      // may alias them as far as the compiler knows, so interleaving would serialise every access
-      float x1[16], x2[16], rr[16], old[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2);
-        const int mc = m < M ? m : M - 1;
-        if constexpr (AUX1) x1[r] = a.aux_in[(int64_t)mc * a.ld_aux_in + nc];
-        if constexpr (AUX2) x2[r] = a.aux_in2[(int64_t)mc * a.ld_aux_in2 + nc];
-        if constexpr (RES) rr[r] = a.R[(int64_t)mc * a.ldr + nc];
-        old[r] = acc_c ? C[(int64_t)mc * a.ldc + nc] : 0.f;
+    for (int i = 0; i < A_F4; ++i) {
+      if constexpr (!TA) {
+        const int e = p + i * NP, r = e / (BK / 4), q = e % (BK / 4);
+        ra[S][i] = ld_n(Ab, a.lda, m0 + r, M, k0 + 4 * q);
+      } else {   // 4 x 4 group: k rows 4 kq .. 4 kq + 3 of m quad q
+        const int kq = p % (BK / 4), q = p / (BK / 4);
+        ra[S][i] = ld_t(Ab, a.lda, k0 + 4 * kq + i, m0 + 4 * q, M);
       }
+    }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        // rows mb + 8g + 0..3 (a 4-aligned group): one Philox block gives their four keep words
-        u32x4_t kw{0u, 0u, 0u, 0u};
-        if (DROP && a.drop_thresh)
-          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
-                             a.seed);
+    for (int i = 0; i < B_F4; ++i) {
+      if constexpr (!TB) {
+        const int e = p + i * NP, r = e / (BK / 4), q = e % (BK / 4);
+        rb[S][i] = ld_n(Bb, a.ldb, n0 + r, N, k0 + 4 * q);
+      } else {
+        const int kq = p % (BK / 4), q = p / (BK / 4);
+        rb[S][i] = ld_t(Bb, a.ldb, k0 + 4 * kq + i, n0 + 4 * q, N);
+      }
+    }
+  };
+  auto put = [&](__bf16* img, int rows, int row, int k, float4 v) {
+    bf16x4 h, m, l;
+    split3(v, h, m, l);
+    __bf16* q = img + row * XRS + k;
+    *reinterpret_cast<bf16x4*>(q) = h;
+    *reinterpret_cast<bf16x4*>(q + rows * XRS) = m;
+    *reinterpret_cast<bf16x4*>(q + 2 * rows * XRS) = l;
+  };
+  auto convert = [&](auto S, __bf16* img, bool live) {   // live: a real slab (row sums count it)
+    __bf16* xa = img;
+    __bf16* xb = img + 3 * BM * XRS;
+    const int kq = p % (BK / 4), q = p / (BK / 4);
+    if constexpr (!TA) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 4 * g + q;
-          const int m = mb + 8 * g + q;
-          float v = acc[i][j][r] + bn;
-          const uint32_t word = q == 0 ? kw.x : (q == 1 ? kw.y : (q == 2 ? kw.z : kw.w));
-          float aux_o = 0.f;
-          if constexpr (EPI == EPI_GELU) v = geluf_(v);
-          if constexpr (EPI == EPI_SILU) v = siluf_(v);
-          if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
-          if constexpr (EPI == EPI_GELU_DROP) {   // torch GELU (erf) and GeluBackward's factor
-            const float cdf = 0.5f * (1.0f + erff(v * 0.70710678118654752f));
-            const float pdf = 0.3989422804014327f * expf(v * v * -0.5f);
-            aux_o = cdf + v * pdf;
-            v = (0.5f * v) * (1.0f + erff(v * 0.70710678118654752f));
-            if (a.drop_thresh) {
-              const bool keep = word >= a.drop_thresh;
-              v = keep ? v * a.inv_keep : 0.f;
-              aux_o = keep ? aux_o * a.inv_keep : 0.f;
-            }
-          }
-          if constexpr (EPI == EPI_SILU_SAVE) {
-            if (act) {
-              const float sg = 1.0f / (1.0f + expf(-v));
-              aux_o = sg * (1.0f + v * (1.0f - sg));
-              v = v / (1.0f + expf(-v));
-            } else {
-              aux_o = 1.0f;
-            }
-          }
-          if constexpr (EPI == EPI_MUL_AUX) v = v * x1[r];
-          if constexpr (EPI == EPI_DGATE) {
-            const float sg = sigmoidf_(x2[r]);
-            aux_o = (v * x1[r]) * (1.0f - sg) * sg;
-            v = v * sg;
-          }
-          if constexpr (RES) v = v + rr[r];
-          if (acc_c) v = a.beta * old[r] + v;
-          if (nok && m < M && (!a.row_mask || a.row_mask[m])) {
-            C[(int64_t)m * a.ldc + n] = v;
-            if constexpr (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE)
-              a.aux_out[(int64_t)m * a.ld_aux_out + n] = aux_o;
-          }
+      for (int i = 0; i < A_F4; ++i) {
+        const int e = p + i * NP, r = e / (BK / 4), qq = e % (BK / 4);
+        put(xa, BM, r, 4 * qq, ra[S][i]);
+      }
+    } else {
+      const float4 k0v = ra[S][0], k1v = ra[S][1], k2v = ra[S][2], k3v = ra[S][3];
+      put(xa, BM, 4 * q + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
+      put(xa, BM, 4 * q + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
+      put(xa, BM, 4 * q + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
+      put(xa, BM, 4 * q + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+      if (do_rs) {   // this slab's sums of rows 4 q .. 4 q + 3: own 4 k, then the 8 lanes of the m quad
+        float s4[4] = {(k0v.x + k1v.x) + (k2v.x + k3v.x), (k0v.y + k1v.y) + (k2v.y + k3v.y),
+                       (k0v.z + k1v.z) + (k2v.z + k3v.z), (k0v.w + k1v.w) + (k2v.w + k3v.w)};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+          for (int o = 1; o < BK / 4; o <<= 1) s4[c] += __shfl_xor(s4[c], o, kWave);
+          rs[c] += live ? s4[c] : 0.f;
         }
       }
     }
+    if constexpr (!TB) {
+#pragma unroll
+      for (int i = 0; i < B_F4; ++i) {
+        const int e = p + i * NP, r = e / (BK / 4), qq = e % (BK / 4);
+        put(xb, BN, r, 4 * qq, rb[S][i]);
+      }
+    } else {
+      const float4 k0v = rb[S][0], k1v = rb[S][1], k2v = rb[S][2], k3v = rb[S][3];
+      put(xb, BN, 4 * q + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
+      put(xb, BN, 4 * q + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
+      put(xb, BN, 4 * q + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
+      put(xb, BN, 4 * q + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+    }
+  };
+
+  // ---- consumer state ----
+  const int wm = (wave & 3) >> 1, wn = wave & 1;
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto compute = [&](const __bf16* img) {
+    const int xi = wm * 32 * TM + (lane & 31), xj = wn * 32 * TN + (lane & 31), xk = 8 * (lane >> 5);
+    const __bf16* xa = img;
+    const __bf16* xb = img + 3 * BM * XRS;
+    bf16x8 av[2][3][TM], bv[2][3][TN];
+    // fragments read in the order the products consume them (A lo, B hi, A hi, B lo, A mid, B mid),
+    // so the first MFMAs of a slab wait for three reads, not for all of them
+    auto rd = [&](int buf, int st) {
+      auto ra_ = [&](int pc) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[buf][pc][i] = *reinterpret_cast<const bf16x8*>(xa + (pc * BM + xi + 32 * i) * XRS + 16 * st + xk);
+      };
+      auto rb_ = [&](int pc) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[buf][pc][j] = *reinterpret_cast<const bf16x8*>(xb + (pc * BN + xj + 32 * j) * XRS + 16 * st + xk);
+      };
+      ra_(2); rb_(0); ra_(0); rb_(2); ra_(1); rb_(1);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) {
+      const int pb = st & 1;
+      if (st + 1 < BK / 16) rd(pb ^ 1, st + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // smallest products first: (A piece, B piece) = lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+      constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[pb][PA[t]][i], bv[pb][PB[t]][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- pipeline ----
+  // Slab t waits in register set t & 1 until it is split into piece image t & 1.  The two roles
+  // run separate loops (neither keeps the other's registers live) with the same barrier sequence:
+  // one after the prologue, then one per step, 2 * ceil(nk / 2) steps.  In step t the consumers
+  // multiply image t & 1 while the producers split slab t + 1 (set (t + 1) & 1) into image
+  // (t + 1) & 1 and refill that set with slab t + 3.  Loads past the last slab repeat it
+  // (clamped); their splits go to images no consumer reads.  (Three register sets with the loads
+  // issued ahead of the split measured 13 % slower: tools/ws_lab.hip.)
+  const int nsteps = 2 * ((nk + 1) / 2);
+  if (producer) {
+    load(I0{}, 0);
+    load(I1{}, 1);
+    convert(I0{}, smem, true);
+    load(I0{}, 2);
+    __syncthreads();
+#ifdef XTRL_WS_DIAG
+    const int mode = g_ws_mode;
+#else
+    constexpr int mode = 0;
+#endif
+    // straight-line body (no branch around a load: hipcc would wait for every load at the join);
+    // scheduling barriers keep each step's split inside its step (the scheduler would otherwise
+    // hoist the next step's split arithmetic above the workgroup barrier)
+    auto pstep = [&](auto C, int t) {
+      WS_STAMP(t, 0);
+      if (mode < 2) convert(C, smem + ((t + 1) & 1) * IMG, t + 1 < nk);
+      else if (mode == 3) {   // consume the loads without splitting
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s += ra[decltype(C)::value][i].x + rb[decltype(C)::value][i].y;
+        if (s == 12345.f) smem[tid] = (__bf16)s;
+      }
+      WS_STAMP(t, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (mode != 2) load(C, t + 3);
+      WS_STAMP(t, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    for (int t = 0; t < nsteps; t += 2) {
+      pstep(I1{}, t);
+      pstep(I0{}, t + 1);
+    }
+    if (TA && do_rs && (p % (BK / 4)) == 0) {
+      const int q = p / (BK / 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int m = m0 + 4 * q + c;
+        if (m < M && m >= a.rowsum_m0) {
+          if (a.kspan > 0) a.rowsum_ws[(int64_t)bz * M + m] = rs[c];
+          else a.rowsum[m - a.rowsum_m0] += rs[c];
+        }
+      }
+    }
+    return;
   }
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    WS_STAMP(t, 0);
+#ifdef XTRL_WS_DIAG
+    if (t < nk && g_ws_mode != 1) compute(smem + (t & 1) * IMG);
+#else
+    if (t < nk) compute(smem + (t & 1) * IMG);
+#endif
+    WS_STAMP(t, 1);
+    __syncthreads();
+  }
+  WS_STAMP(nsteps, 0);
+  gemm_epilogue<TM, TN, EPI, RES>(a, acc, m0, n0, wm, wn, lane, bz);
 }
 
 __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, const float* gamma, float* Y, int ldy,
@@ -691,6 +1114,35 @@ void launch(const GemmArgs& a, hipStream_t s) {
                      a);
 }
 
+bool use_ws() {   // XTRL_GEMM_WS=0: the register-staged X6 kernel instead of the warp-specialised one
+  static const bool on = [] {
+    const char* e = getenv("XTRL_GEMM_WS");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// the warp-specialised X6 kernel takes whole 32-deep slabs (K and the split span) and no LN prologue
+bool ws_ok(const GemmArgs& a, bool ta, bool ln) {
+  if (!(use_ws() && !ln && a.K % 32 == 0 && (a.kspan == 0 || a.kspan % 32 == 0) && (!a.rowsum || ta))) return false;
+  // one workgroup per CU: it wins only when the whole grid is one resident round and K is long
+  // (16384 x 256 x 1024: 59 vs 72 us); with several rounds or K = 256 the register-staged kernel's
+  // two workgroups per CU overlap one tile's prologue / epilogue with another's main loop
+  // (16384 x 1024 x 256: 94 vs 70 us; tools/gemm_bench.py, XTRL_GEMM_WS=0)
+  const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
+  const int64_t wgs = (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * splits;
+  return wgs <= 256 && (a.kspan > 0 ? a.kspan : a.K) >= 512;
+}
+
+template <bool TA, bool TB, int EPI, bool RES>
+void launch_ws(const GemmArgs& a, hipStream_t s) {
+  const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
+  dim3 grid((a.N + 127) / 128, (a.M + 127) / 128, splits);
+  GemmArgs r = a;
+  r.xcd_remap = (xcd_env() && (int64_t)grid.x * grid.y * grid.z % 8 == 0) ? 1 : 0;
+  hipLaunchKernelGGL((k_gemm_ws<TA, TB, EPI, RES>), grid, dim3(512), 0, s, r);
+}
+
 bool use_x6() {   // XTRL_GEMM_F32=1: native f32 MFMA products everywhere
   static const bool x6 = [] {
     const char* e = getenv("XTRL_GEMM_F32");
@@ -733,7 +1185,15 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   //  32x32/WK4 17.4; N=260 K=256 64x32/WK2 7.7 vs 8.2; N=256 K=1024 32x32/WK4 13.7 vs 64x64 24.7)
   if (!vec) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, false>(a, s);
   else if (tiles128 >= 192) {
-    if (use_x6()) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true, true>(a, s);
+    bool done = false;
+    if constexpr (EPI != EPI_DGATE && !LN) {   // (the gate epilogue needs more than 256 registers)
+      if (use_x6() && ws_ok(a, TA, LN)) {
+        launch_ws<TA, TB, EPI, RES>(a, s);
+        done = true;
+      }
+    }
+    if (done) {
+    } else if (use_x6()) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true, true>(a, s);
     else launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
   }
   else if (tiles64 >= 256 && a.K <= 512) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
@@ -819,7 +1279,11 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   const bool big = (int64_t)N * K >= 256 * 256;
   const int tm = big ? 128 : 64;
   const int64_t tiles = (int64_t)((N + tm - 1) / tm) * ((K + tm - 1) / tm);
-  const int64_t target = big ? 512 : 1024;
+  static const int64_t big_target = [] {   // XTRL_WGRAD_TARGET: workgroups of the 128 x 128 launch
+    const char* e = getenv("XTRL_WGRAD_TARGET");
+    return (int64_t)(e ? atoi(e) : 512);
+  }();
+  const int64_t target = big ? big_target : 1024;
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (M + 255) / 256));
   int kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
   splits = (M + kspan - 1) / kspan;
@@ -848,7 +1312,8 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   else if (big) {
     const bool timed = prof && prof->events && *prof->n < prof->cap;
     if (timed) (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n], s);
-    if (use_x6()) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true, true>(a, s);
+    if (use_x6() && ws_ok(a, true, false)) launch_ws<true, true, EPI_NONE, false>(a, s);
+    else if (use_x6()) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true, true>(a, s);
     else launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
     if (timed) {
       (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n + 1], s);

@@ -6,6 +6,8 @@
 // kernels, and everything else in the handful of small kernels below.  All reductions over tokens
 // (bias / LayerNorm-gain / embedding gradients) are two-phase with a fixed summation order, so the
 // step is deterministic run to run.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "philox.h"
 
@@ -430,6 +432,69 @@ struct Ctx {
   float* G(int64_t off) const { return off >= 0 ? D->grad + off : nullptr; }
 };
 
+// ---- weight gradients on a side stream ---------------------------------------------------------
+// The weight-gradient GEMMs (and their split-K reduces) are off the backward's critical path: only
+// the optimiser step reads dW.  They run on a low-priority side stream, each after an event on the
+// main stream marks its dY ready; the main stream waits for a specific side event before it
+// overwrites a buffer a pending weight gradient still reads (dx, dff, dproj), and for all of them
+// at the end of the backward.  The side stream and its event ring are created once per process
+// (one device per process) and hold no data.  XTRL_WGRAD_STREAM=0: everything on one stream.
+constexpr int kSideEvents = 160;
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[kSideEvents] = {};
+  bool ok = false;
+};
+SideStream& side_stream() {
+  static SideStream S = [] {
+    SideStream x;
+    const char* e = getenv("XTRL_WGRAD_STREAM");
+    if (e && atoi(e) == 0) return x;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least) == hipSuccess;
+    for (int i = 0; x.ok && i < kSideEvents; ++i)
+      x.ok = hipEventCreateWithFlags(&x.ev[i], hipEventDisableTiming) == hipSuccess;
+    return x;
+  }();
+  return S;
+}
+
+// fork / mark / wait helpers of one backward call (no-ops on a single stream)
+struct Fork {
+  hipStream_t main, side;
+  SideStream* S;
+  int next = 0;
+  bool on() const { return S != nullptr; }
+  hipEvent_t take() { return S->ev[next++]; }
+  // the side stream waits for everything issued on the main stream so far
+  int fork() {
+    if (!on()) return XTRL_OK;
+    hipEvent_t e = take();
+    if (hipEventRecord(e, main) != hipSuccess || hipStreamWaitEvent(side, e, 0) != hipSuccess) {
+      set_error("train: side-stream fork failed");
+      return XTRL_E_HIP;
+    }
+    return XTRL_OK;
+  }
+  // an event after everything issued on the side stream so far
+  hipEvent_t mark() {
+    if (!on()) return nullptr;
+    hipEvent_t e = take();
+    if (hipEventRecord(e, side) != hipSuccess) return nullptr;
+    return e;
+  }
+  // the main stream waits for a side event (nullptr: nothing to wait for)
+  int wait(hipEvent_t e) {
+    if (!on() || !e) return XTRL_OK;
+    if (hipStreamWaitEvent(main, e, 0) != hipSuccess) {
+      set_error("train: side-stream join failed");
+      return XTRL_E_HIP;
+    }
+    return XTRL_OK;
+  }
+};
+
 // C[M][N] = A[M][K] . W[N][K]^T (+ bias) with an epilogue
 int linear_fwd(const Ctx& c, const float* A, int lda, const float* W, const float* bias, float* C, int ldc, int M,
                int N, int K, int epi, const float* R = nullptr, float* aux_out = nullptr, int ld_aux = 0,
@@ -610,19 +675,26 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   const Ctx c{D, s, D->b * D->n};
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4, S1x2 = 2 * (D->S + 1);
   int rc;
+  SideStream& side = side_stream();
+  const bool two = side.ok && 4 * D->L + 24 <= kSideEvents;
+  Fork F{s, side.s, two ? &side : nullptr};
+  const Ctx cw{D, two ? side.s : s, T};   // weight gradients
   // ---- actor / critic heads
-  if ((rc = wgrad(c, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
-  if ((rc = wgrad(c, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d, c.G(D->b_c2)))) return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
+  if ((rc = wgrad(cw, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d, c.G(D->b_c2)))) return rc;
   if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_MUL_AUX, D->z1,
                          4 * d)))
     return rc;
   if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_MUL_AUX,
                          D->z1 + 2 * d, 4 * d)))
     return rc;
-  if ((rc = wgrad(c, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
   if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
   // state embedding and gene conditioning
-  if ((rc = wgrad(c, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
   if (D->evolutionary) {
     XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
     hipLaunchKernelGGL(k_latent_grad, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->dac, D->in_dim, 2 * d, D->b,
@@ -632,28 +704,41 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     XTRL_LAUNCHED("train latent grad");
   }
   // ---- world-model heads
-  if ((rc = wgrad(c, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
+  if ((rc = wgrad(cw, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
   if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_MUL_AUX, D->zp, ldp))) return rc;
   hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);
-  if ((rc = wgrad(c, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
   if ((rc = linear_dgrad(c, D->dzp, ldp, c.P(D->w_pd), D->dewa, 2 * d, T, d + 1, 2 * d, EPI_NONE))) return rc;
   // action-embedding gradient of the next-action input (and, below, of the previous action)
   // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
   if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
                    c.P(D->ln_final), nullptr, D->dx, c.G(D->ln_final))))
     return rc;
-  // ---- decoder blocks, last to first
+  // ---- decoder blocks, last to first.  Side events of the weight gradients whose dY buffer the
+  // main stream overwrites later: dx (FF2 / out-projection), dff (FF1, by the next layer's FF2
+  // input gradient), dproj (q|k|v projection, by the next layer's gate / attention backward).
+  hipEvent_t e_ff1 = nullptr, e_proj = nullptr;
   for (int li = D->L - 1; li >= 0; --li) {
     const XtrlTrainLayer& Ly = D->layers[li];
     // FF2 (+ residual): dx is the gradient w.r.t. the block output
-    if ((rc = wgrad(c, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
+    hipEvent_t e_ff2 = F.mark();
+    if ((rc = F.wait(e_ff1))) return rc;
     if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, ff, T, d, ff, EPI_MUL_AUX, Ly.u, ff))) return rc;
-    if ((rc = wgrad(c, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
+    e_ff1 = F.mark();
     if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+    if ((rc = F.wait(e_ff2))) return rc;
     if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
       return rc;
     // attention out-projection (+ residual) and the value gate
-    if ((rc = wgrad(c, D->dx, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dx, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
+    hipEvent_t e_out = F.mark();
+    if ((rc = F.wait(e_proj))) return rc;
     if (D->gate_values) {
       if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30,
                              Ly.proj + 3 * I, Ly.n_qkv, D->dproj + 3 * I, Ly.n_qkv)))
@@ -680,19 +765,23 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * 3 * I / 2, 256)), dim3(256), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
-    if ((rc = wgrad(c, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
       return rc;
+    e_proj = F.mark();
     if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
+    if ((rc = F.wait(e_out))) return rc;
     if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
                      c.G(Ly.ln_attn))))
       return rc;
   }
   // ---- embeddings: dx is d x0
-  if ((rc = wgrad(c, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
   if ((rc = colsum(c, D->dx, d, T, d, c.G(D->reward_embed), D->swr + D->S, D->S + 1, D->reward_keep))) return rc;
   if (D->continuous) {
-    if ((rc = wgrad(c, D->dx, d, D->prev_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
-    if ((rc = wgrad(c, D->dewa + d, 2 * d, D->next_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
+    if ((rc = wgrad(cw, D->dx, d, D->prev_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
+    if ((rc = wgrad(cw, D->dewa + d, 2 * d, D->next_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
     if ((rc = colsum(c, D->dx, d, T, d, c.G(D->act_emb_b)))) return rc;
     if ((rc = colsum(c, D->dewa + d, 2 * d, T, d, c.G(D->act_emb_b)))) return rc;
   } else {
@@ -706,6 +795,8 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
                        c.G(D->act_emb));
     XTRL_LAUNCHED("train embed grad");
   }
+  // every weight gradient is in before the caller's optimiser step
+  if ((rc = F.wait(F.mark()))) return rc;
   return XTRL_OK;
 }
 
