@@ -1114,6 +1114,16 @@ void launch(const GemmArgs& a, hipStream_t s) {
                      a);
 }
 
+// XTRL_GEMM_X6_SMALL=1: split-bf16 products on the 64 x 64 geometry too (off: the decode-sized
+// GEMMs are latency bound, C3 rollout 38.7 vs 38.1 ms with it on)
+bool use_x6_small() {
+  static const bool on = [] {
+    const char* e = getenv("XTRL_GEMM_X6_SMALL");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 bool use_ws() {   // XTRL_GEMM_WS=0: the register-staged X6 kernel instead of the warp-specialised one
   static const bool on = [] {
     const char* e = getenv("XTRL_GEMM_WS");
@@ -1196,7 +1206,18 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
     } else if (use_x6()) launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true, true>(a, s);
     else launch<2, 2, 1, 2, 2, TA, TB, EPI, LN, RES, true>(a, s);
   }
-  else if (tiles64 >= 256 && a.K <= 512) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (tiles64 >= 256 && a.K <= 512) {
+    bool done = false;
+    // 64 x 64 tiles with split-bf16 products (XTRL_GEMM_X6_SMALL=0: f32); "N" operands only (the
+    // transposed staging needs whole 4 x 4 groups per thread)
+    if constexpr (!TA && !TB && EPI != EPI_DGATE) {
+      if (use_x6() && use_x6_small()) {
+        launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true, true>(a, s);
+        done = true;
+      }
+    }
+    if (!done) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  }
   else if (a.K <= 256) launch<2, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
   else launch<1, 1, 4, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
 }
@@ -1273,15 +1294,16 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
   // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
   // 128 x 128 tiles (2 workgroups / CU by registers) when the weight is large, else 64 x 64 (4 / CU);
-  // split the tokens until one resident round of workgroups covers the chip, keeping at least 8
-  // K-slabs (256 tokens) per split so the pipeline reaches steady state (more splits would cost
-  // more partial-tile traffic in phase 2 than they save)
+  // split the tokens until 256 workgroups (half a resident round: the learn step runs these on a
+  // side stream beside the input-gradient chain, which fills the rest; C3 update 174.6 / 171.5 /
+  // 172.6 ms at 512 / 256 / 128) keeping at least 8 K-slabs (256 tokens) per split so the pipeline
+  // reaches steady state (more splits cost more partial-tile traffic in phase 2 than they save)
   const bool big = (int64_t)N * K >= 256 * 256;
   const int tm = big ? 128 : 64;
   const int64_t tiles = (int64_t)((N + tm - 1) / tm) * ((K + tm - 1) / tm);
   static const int64_t big_target = [] {   // XTRL_WGRAD_TARGET: workgroups of the 128 x 128 launch
     const char* e = getenv("XTRL_WGRAD_TARGET");
-    return (int64_t)(e ? atoi(e) : 512);
+    return (int64_t)(e ? atoi(e) : 256);
   }();
   const int64_t target = big ? big_target : 1024;
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (M + 255) / 256));
