@@ -137,7 +137,9 @@ class WgradGemmTimer:
     weight-gradient GEMM k_gemm<2,2,1,2,2,T,T,...> — inside xtrl_train_backward (XtrlTrainDesc
     prof_events / prof_flops), on the learn stream, over the timed region."""
 
-    KERNEL = 'k_gemm<2, 2, 1, 2, 2, true, true'
+    # the 128x128 weight-gradient launches: the warp-specialised kernel when the split grid is one
+    # resident round (the C3 shapes), the register-staged one otherwise
+    KERNELS = ('k_gemm_ws<true, true', 'k_gemm<2, 2, 1, 2, 2, true, true')
 
     def __init__(self, agent, cap=8192):
         import ctypes as C
@@ -173,17 +175,19 @@ class WgradGemmTimer:
         D.prof_events, D.prof_flops, D.prof_cap, D.prof_n = None, None, 0, None
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of ``kernel`` from the newest committed PMC summary
-    (profiles/rNN_pmc_traffic.json, written by tools/gpu_check.sh pmc from two rocprofv3 --pmc
-    passes of this bench: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of the MI355X guide)."""
+def pmc_traffic(*kernels):
+    """HBM bytes per launch of the kernels whose names contain one of ``kernels`` (dispatch-weighted
+    mean) from the newest committed PMC summary (profiles/rNN_pmc_traffic.json, written by
+    tools/gpu_check.sh pmc from two rocprofv3 --pmc passes of this bench: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of the MI355X guide)."""
     import glob
     files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_pmc_traffic.json')))
     if not files:
         return None
     data = json.load(open(files[-1]))
-    hits = [v for k, v in data.items() if kernel in k]
-    return round(hits[0]['traffic']) if hits else None
+    hits = [v for k, v in data.items() if any(x in k for x in kernels)]
+    n = sum(h['dispatches'] for h in hits)
+    return round(sum(h['traffic'] * h['dispatches'] for h in hits) / n) if n else None
 
 
 def cpu_baseline(cfg, seed, budget_s):
@@ -336,12 +340,13 @@ def main():
             achieved = flops / avg_s / 1e12
             x6 = os.environ.get('XTRL_GEMM_F32', '0') in ('', '0')
             peak = X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
-            roofline = dict(kernel='k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, 128x128 tiles, split-K; '
-                                   'the largest kernel of the update; fp32 products as ' +
+            roofline = dict(kernel='k_gemm_ws<T,T> / k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, '
+                                   '128x128 tiles, split-K over 256 workgroups, on the backward side stream beside '
+                                   'the input-gradient chain; the largest kernel of the update; fp32 products as ' +
                                    ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
                                     'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
                             peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
-                            traffic=pmc_traffic(WgradGemmTimer.KERNEL), avg_launch_us=round(avg_s * 1e6, 2),
+                            traffic=pmc_traffic(*WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
                             flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3

@@ -26,7 +26,7 @@ run_pmc() {
   cd /tmp && export TMPDIR=/tmp
   for c in FETCH_SIZE WRITE_SIZE; do
     # only the two roofline kernels (many more dispatches crash the counter-collection tool)
-    timeout -k 10 900 rocprofv3 --pmc $c --kernel-include-regex "k_attn_decode|k_gemm<2, 2, 1, 2, 2, true, true" -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$c -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-loss-delta "$@" > $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log 2>&1
+    timeout -k 10 900 rocprofv3 --pmc $c --kernel-include-regex "k_attn_decode|k_gemm<2, 2, 1, 2, 2, true, true|k_gemm_ws<true, true" -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$c -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-loss-delta "$@" > $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log 2>&1
     rc=$?; tail -2 $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log
     if [ $rc -ne 0 ]; then echo "pmc $c rc=$rc"; exit $rc; fi
   done

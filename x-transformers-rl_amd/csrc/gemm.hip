@@ -1334,7 +1334,11 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   else if (big) {
     const bool timed = prof && prof->events && *prof->n < prof->cap;
     if (timed) (void)hipEventRecord((hipEvent_t)prof->events[2 * *prof->n], s);
-    if (use_x6() && ws_ok(a, true, false)) launch_ws<true, true, EPI_NONE, false>(a, s);
+    static const bool wgrad_ws = [] {   // XTRL_WGRAD_WS=0: register-staged kernel for weight gradients
+      const char* e = getenv("XTRL_WGRAD_WS");
+      return !(e && atoi(e) == 0);
+    }();
+    if (use_x6() && wgrad_ws && ws_ok(a, true, false)) launch_ws<true, true, EPI_NONE, false>(a, s);
     else if (use_x6()) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true, true>(a, s);
     else launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
     if (timed) {
