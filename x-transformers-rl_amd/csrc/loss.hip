@@ -48,18 +48,33 @@ __device__ __forceinline__ float hl_cdf(const float* support, int k, float y, fl
   return erff((support[k] - y) * inv);
 }
 
-// cross entropy -sum_k t_k log_softmax(x)_k and (optionally) its gradient softmax * sum(t) - t
+// HL-Gauss target probabilities of bins lane and lane + 64 (B <= 127): each lane evaluates the
+// CDF at its two bin edges once and takes edge k + 1 from its neighbour, so every edge costs one
+// erff per token (the same value, bit for bit, as evaluating both edges of every bin)
+struct HlTargets {
+  float t0, t1;
+};
+
+__device__ HlTargets hl_targets(const float* support, int B, float y, float inv, int lane) {
+  const float e0 = lane <= B ? hl_cdf(support, lane, y, inv) : 0.f;
+  const float e1 = lane + 64 <= B ? hl_cdf(support, lane + 64, y, inv) : 0.f;
+  const int nb = (lane + 1) & 63;
+  const float n0s = __shfl(e0, nb, 64), n1 = __shfl(e1, nb, 64), e64 = __shfl(e1, 0, 64);
+  const float n0 = lane == 63 ? e64 : n0s;
+  const float cB = B < 64 ? __shfl(e0, B, 64) : __shfl(e1, B - 64, 64);
+  const float z = cB - __shfl(e0, 0, 64);
+  return {lane < B ? (n0 - e0) / z : 0.f, lane + 64 < B ? (n1 - e1) / z : 0.f};
+}
+
+// cross entropy -sum_k t_k log_softmax(x)_k
 __device__ float hl_ce(const XtrlLossDesc& D, const float* x, float lse, float y, int lane) {
   const int B = D.B;
   y = fminf(fmaxf(y, D.lo), D.hi);
   const float inv = 1.0f / (1.41421356237309505f * D.sigma);
-  const float c0 = hl_cdf(D.support, 0, y, inv), cB = hl_cdf(D.support, B, y, inv);
-  const float z = cB - c0;
+  const HlTargets t = hl_targets(D.support, B, y, inv, lane);
   float acc = 0.f;
-  for (int k = lane; k < B; k += 64) {
-    const float tk = (hl_cdf(D.support, k + 1, y, inv) - hl_cdf(D.support, k, y, inv)) / z;
-    acc += tk * (x[k] - lse);
-  }
+  if (lane < B) acc += t.t0 * (x[lane] - lse);
+  if (lane + 64 < B) acc += t.t1 * (x[lane + 64] - lse);
   return -wave_sum(acc);
 }
 
@@ -350,21 +365,27 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
     const float inv = 1.0f / (1.41421356237309505f * D.sigma);
     const float yu = fminf(fmaxf(D.returns[tk], D.lo), D.hi);
     const float yc = fminf(fmaxf(fminf(fmaxf(D.returns[tk], -D.value_clip), D.value_clip), D.lo), D.hi);
-    const float zu = hl_cdf(D.support, D.B, yu, inv) - hl_cdf(D.support, 0, yu, inv);
-    const float zc = hl_cdf(D.support, D.B, yc, inv) - hl_cdf(D.support, 0, yc, inv);
+    const HlTargets tu = hl_targets(D.support, D.B, yu, inv, lane);
+    const HlTargets tc = hl_targets(D.support, D.B, yc, inv, lane);
     // sum_k t_k (= 1 up to rounding) for the exact softmax * sum(t) - t gradient
     float su = 0.f, sc = 0.f;
-    for (int k = lane; k < D.B; k += 64) {
-      su += (hl_cdf(D.support, k + 1, yu, inv) - hl_cdf(D.support, k, yu, inv)) / zu;
-      sc += (hl_cdf(D.support, k + 1, yc, inv) - hl_cdf(D.support, k, yc, inv)) / zc;
+    if (lane < D.B) {
+      su += tu.t0;
+      sc += tc.t0;
+    }
+    if (lane + 64 < D.B) {
+      su += tu.t1;
+      sc += tc.t1;
     }
     su = wave_sum(su);
     sc = wave_sum(sc);
-    for (int k = lane; k < D.B; k += 64) {
-      const float p = expf(x[k] - rn.lse);
-      const float tu = (hl_cdf(D.support, k + 1, yu, inv) - hl_cdf(D.support, k, yu, inv)) / zu;
-      const float tc = (hl_cdf(D.support, k + 1, yc, inv) - hl_cdf(D.support, k, yc, inv)) / zc;
-      D.d_values[(int64_t)tk * D.B + k] = du * (p * su - tu) + dc * (p * sc - tc);
+    if (lane < D.B) {
+      const float p = expf(x[lane] - rn.lse);
+      D.d_values[(int64_t)tk * D.B + lane] = du * (p * su - tu.t0) + dc * (p * sc - tc.t0);
+    }
+    if (lane + 64 < D.B) {
+      const float p = expf(x[lane + 64] - rn.lse);
+      D.d_values[(int64_t)tk * D.B + lane + 64] = du * (p * su - tu.t1) + dc * (p * sc - tc.t1);
     }
   }
 
@@ -466,7 +487,8 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
 
 int check(const XtrlLossDesc* D) {
   XTRL_REQUIRE(D, "loss: null descriptor");
-  XTRL_REQUIRE(D->b > 0 && D->n > 0 && D->A > 0 && D->A <= 32 && D->B > 0 && D->S1 > 0, "loss: bad shape");
+  XTRL_REQUIRE(D->b > 0 && D->n > 0 && D->A > 0 && D->A <= 32 && D->B > 0 && D->B <= 127 && D->S1 > 0,
+               "loss: bad shape (A <= 32, B <= 127)");
   XTRL_REQUIRE(D->raw_actions && D->values && D->pred_raw && D->done_logit && D->old_logp && D->returns &&
                    D->old_values && D->dones && D->lens && D->real && D->support && D->centers && D->tok && D->stats,
                "loss: null operand");

@@ -14,6 +14,7 @@ namespace xtrl {
 namespace {
 
 constexpr int NB = 512;   // partial-sum blocks for the norm
+constexpr int ADOPT_U = 4;   // elements per thread in flight in the AdoptAtan2 passes
 
 __global__ __launch_bounds__(256) void k_sumsq(const float* g, int64_t n, double* ws) {
   double s = 0.0;
@@ -28,10 +29,13 @@ __global__ __launch_bounds__(256) void k_sumsq(const float* g, int64_t n, double
   if (threadIdx.x == 0) ws[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
+// 64 lanes: lane l sums partials l, l + 64, ... in order (loads in flight together), then a
+// fixed-order wave reduction
 __global__ void k_norm_final(const double* ws, int nb, float max_norm, float* out) {
-  if (threadIdx.x != 0) return;
   double s = 0.0;
-  for (int i = 0; i < nb; ++i) s += ws[i];
+  for (int i = threadIdx.x; i < nb; i += 64) s += ws[i];
+  s = wave_sum_d(s);
+  if (threadIdx.x != 0) return;
   const float norm = (float)sqrt(s);
   out[0] = norm;
   out[1] = fminf(max_norm / (norm + 1e-6f), 1.0f);
@@ -57,23 +61,40 @@ __global__ __launch_bounds__(256) void k_adopt_a(const AdoptArgs A) {
   const int sg = (int)A.chunks[3 * blockIdx.x + 2];
   const float coef = A.clip ? A.clip[1] : 1.f;
   int aligned = 0;
-  for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
-    const float g = A.g[i] * coef;
-    A.g[i] = g;
-    float p = A.p[i];
-    if (A.regen > 0.f && !A.first) p = lerpf_(p, A.p_init[i], A.lr / A.init_lr * A.regen);
-    if (A.wd > 0.f) p = p * (1.f - A.lr * A.wd);
-    A.p[i] = p;
-    if (A.first) {
-      A.m[i] = 0.f;
-      A.v[i] = g * g;
-      if (A.regen > 0.f) A.p_init[i] = p;
-      continue;
+  // ADOPT_U elements per thread per round, all loaded before the first store (the stores may alias
+  // the loads as far as the compiler knows): the round's loads are in flight together
+  for (int64_t i0 = c0 + threadIdx.x; i0 < c1; i0 += ADOPT_U * 256) {
+    float g[ADOPT_U], p[ADOPT_U], pi[ADOPT_U], v[ADOPT_U], m[ADOPT_U];
+#pragma unroll
+    for (int u = 0; u < ADOPT_U; ++u) {
+      const int64_t i = i0 + u * 256, ic = i < c1 ? i : c0;
+      g[u] = A.g[ic];
+      p[u] = A.p[ic];
+      pi[u] = (A.regen > 0.f && !A.first) ? A.p_init[ic] : 0.f;
+      v[u] = A.first ? 0.f : A.v[ic];
+      m[u] = A.first ? 0.f : A.m[ic];
     }
-    const float u = atan2f(g, A.b * sqrtf(A.v[i]));
-    const float m = lerpf_(A.m[i], u, 1.f - A.beta1);
-    A.m[i] = m;
-    aligned += (m * g > 0.f) ? 1 : 0;
+#pragma unroll
+    for (int u = 0; u < ADOPT_U; ++u) {
+      const int64_t i = i0 + u * 256;
+      if (i >= c1) break;
+      const float gg = g[u] * coef;
+      A.g[i] = gg;
+      float pp = p[u];
+      if (A.regen > 0.f && !A.first) pp = lerpf_(pp, pi[u], A.lr / A.init_lr * A.regen);
+      if (A.wd > 0.f) pp = pp * (1.f - A.lr * A.wd);
+      A.p[i] = pp;
+      if (A.first) {
+        A.m[i] = 0.f;
+        A.v[i] = gg * gg;
+        if (A.regen > 0.f) A.p_init[i] = pp;
+        continue;
+      }
+      const float uu = atan2f(gg, A.b * sqrtf(v[u]));
+      const float mm = lerpf_(m[u], uu, 1.f - A.beta1);
+      A.m[i] = mm;
+      aligned += (mm * gg > 0.f) ? 1 : 0;
+    }
   }
   if (A.first || A.cautious >= 1.f) return;
   __shared__ int sh[4];
@@ -97,12 +118,25 @@ __global__ __launch_bounds__(256) void k_adopt_b(const AdoptArgs A) {
     mean = (float)((k + (double)A.cautious * (len - k)) / len);
   }
   const float inv = 1.f / fmaxf(mean, 1e-5f);
-  for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
-    const float g = A.g[i], m = A.m[i];
-    float upd = m;
-    if (A.cautious < 1.f) upd = m * (((m * g > 0.f) ? 1.f : A.cautious) * inv);
-    A.p[i] = A.p[i] + (-A.lr) * (upd * A.a);
-    A.v[i] = lerpf_(A.v[i], g * g, 1.f - A.beta2);
+  for (int64_t i0 = c0 + threadIdx.x; i0 < c1; i0 += ADOPT_U * 256) {
+    float g[ADOPT_U], m[ADOPT_U], p[ADOPT_U], v[ADOPT_U];
+#pragma unroll
+    for (int u = 0; u < ADOPT_U; ++u) {
+      const int64_t i = i0 + u * 256, ic = i < c1 ? i : c0;
+      g[u] = A.g[ic];
+      m[u] = A.m[ic];
+      p[u] = A.p[ic];
+      v[u] = A.v[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < ADOPT_U; ++u) {
+      const int64_t i = i0 + u * 256;
+      if (i >= c1) break;
+      float upd = m[u];
+      if (A.cautious < 1.f) upd = m[u] * (((m[u] * g[u] > 0.f) ? 1.f : A.cautious) * inv);
+      A.p[i] = p[u] + (-A.lr) * (upd * A.a);
+      A.v[i] = lerpf_(v[u], g[u] * g[u], 1.f - A.beta2);
+    }
   }
 }
 

@@ -29,11 +29,12 @@ struct EmbedArgs {
   float keep;
 };
 
-constexpr int EMB_TOK = 32, EMB_MAXS = 32;
+constexpr int EMB_TOK = 4, EMB_MAXS = 32;
 // block: EMB_TOK tokens x all d columns; thread c keeps its project_in / to_state_embed rows in
-// registers (S <= EMB_MAXS) and walks the block's tokens
+// registers (S <= EMB_MAXS); every input of the block's tokens is loaded before the first store
+// (the stores may alias the inputs as far as the compiler knows), so the loads are in flight together
 __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
-  const int t0 = blockIdx.x * EMB_TOK, t1 = min(a.T, t0 + EMB_TOK);
+  const int t0 = blockIdx.x * EMB_TOK;
   for (int c = threadIdx.x; c < a.d; c += 256) {
     float wp[EMB_MAXS], ws[EMB_MAXS];
 #pragma unroll
@@ -43,39 +44,47 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
     }
     const float bse = a.b_se[c], re = a.reward_embed[c];
     const float bemb = a.continuous ? a.act_emb_b[c] : 0.f;
-    for (int t = t0; t < t1; ++t) {
+    float pin[EMB_TOK], se[EMB_TOK], rw[EMB_TOK], ap[EMB_TOK], an[EMB_TOK], le[EMB_TOK];
+#pragma unroll
+    for (int u = 0; u < EMB_TOK; ++u) {
+      const int t = min(t0 + u, a.T - 1);
       const float* st = a.swr + (int64_t)t * (a.S + 1);
-      float pin = 0.f, se = 0.f;
+      float sp = 0.f, ss = 0.f;
 #pragma unroll
       for (int s = 0; s < EMB_MAXS; ++s) {
         if (s < a.S) {
           const float x = st[s];
-          pin += x * wp[s];
-          se += x * ws[s];
+          sp += x * wp[s];
+          ss += x * ws[s];
         }
       }
-      se += bse;
-      float ap, an;
+      pin[u] = sp;
+      se[u] = ss + bse;
+      rw[u] = st[a.S];
       if (a.continuous) {
         const float* w = a.act_emb + (int64_t)c * a.A;
-        ap = 0.f;
-        an = 0.f;
+        float p = 0.f, q = 0.f;
         for (int k = 0; k < a.A; ++k) {
-          ap += a.prev_af[(int64_t)t * a.A + k] * w[k];
-          an += a.next_af[(int64_t)t * a.A + k] * w[k];
+          p += a.prev_af[(int64_t)t * a.A + k] * w[k];
+          q += a.next_af[(int64_t)t * a.A + k] * w[k];
         }
-        ap += bemb;
-        an += bemb;
+        ap[u] = p + bemb;
+        an[u] = q + bemb;
       } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
         const int p = a.prev_a[t], q = a.next_a[t];
-        ap = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
-        an = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
+        ap[u] = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
+        an[u] = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
       }
-      const float r = st[a.S];
-      a.x0[(int64_t)t * a.d + c] = pin + (ap + (r * re) * a.keep);
-      a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se;
-      a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an;
-      if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = a.lat_e[(int64_t)(t / a.n) * a.d + c];
+      le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < EMB_TOK; ++u) {
+      const int t = t0 + u;
+      if (t >= a.T) break;
+      a.x0[(int64_t)t * a.d + c] = pin[u] + (ap[u] + (rw[u] * re) * a.keep);
+      a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se[u];
+      a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an[u];
+      if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = le[u];
     }
   }
 }

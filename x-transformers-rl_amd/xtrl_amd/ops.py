@@ -239,7 +239,7 @@ def grad_norm(flat_grad, max_norm, ws, out):
                                    L.stream()), 'grad_norm')
 
 
-def adopt_chunks(seg, chunk=8192):
+def adopt_chunks(seg, chunk=2048):
     """[n_chunks][3] (start, end, tensor) pieces of the flat buffer, one workgroup each."""
     offs = seg.tolist()
     rows = []
