@@ -285,8 +285,14 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        # XTRL_BENCH_BACKEND=gloo: multi-rank rehearsal on fewer GPUs than ranks (ranks share devices)
+        backend = os.environ.get('XTRL_BENCH_BACKEND', 'nccl')
+        dev = local if backend == 'nccl' else local % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     cfg = CONFIGS[args.config]
@@ -359,7 +365,10 @@ def main():
 
     loss_delta = None
     cpu = None
-    if rank == 0:
+    # the loss-delta check runs one more update (its learn all-reduces gradients) and the CPU
+    # baseline is an N = 1 figure: both only in single-process runs, so no rank waits in a
+    # collective the others never enter
+    if world == 1:
         try:
             loss_delta = None if args.no_loss_delta else ppo_loss_delta(learner, env, cfg)
         except Exception as e:   # reported, never hidden

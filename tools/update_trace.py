@@ -58,6 +58,25 @@ def show(path):
                 a = agg[short(names[i])]; a[0] += 1; a[1] += dur[i]
             for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
                 print(f'  {us / 1e3:8.2f} ms {n:6d} {us / n:8.1f} us  {k}')
+        # GPU idle time in the learn phase (no kernel of any stream running) and where it falls
+        seg = learn
+        iv = sorted((int(rows[i]['Start_Timestamp']), int(rows[i]['End_Timestamp']), i) for i in seg)
+        idle, gaps, cur = 0, [], iv[0][1]
+        for s_, e_, i in iv[1:]:
+            if s_ > cur:
+                idle += s_ - cur
+                gaps.append(((s_ - cur) / 1e3, i))
+            cur = max(cur, e_)
+        gaps.sort(reverse=True)
+        print(f'\nlearn idle: {idle / 1e6:.2f} ms in {len(gaps)} gaps; largest:')
+        for g_us, i in gaps[:12]:
+            print(f'  {g_us:8.1f} us before {short(names[i])}  (after {short(names[i - 1])})')
+        by_next = defaultdict(float)
+        for g_us, i in gaps:
+            by_next[short(names[i])] += g_us
+        print('idle by the kernel that ends it:')
+        for k, v in sorted(by_next.items(), key=lambda kv: -kv[1])[:10]:
+            print(f'  {v / 1e3:8.2f} ms  {k}')
         # one minibatch: between the 2nd and 3rd gather
         if len(gathers) > 2:
             a, b = gathers[1], gathers[2]
