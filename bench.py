@@ -190,6 +190,19 @@ def pmc_traffic(*kernels):
     return round(sum(h['traffic'] * h['dispatches'] for h in hits) / n) if n else None
 
 
+def pmc_mfma_busy(*kernels):
+    """Matrix-core busy fraction of the kernels (dispatch-weighted mean of SQ_VALU_MFMA_BUSY_CYCLES /
+    (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), the third PMC pass of tools/gpu_check.sh pmc), or None."""
+    import glob
+    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_pmc_traffic.json')))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    hits = [v for k, v in data.items() if any(x in k for x in kernels) and 'mfma_busy' in v]
+    n = sum(h['dispatches'] for h in hits)
+    return round(sum(h['mfma_busy'] * h['dispatches'] for h in hits) / n, 4) if n else None
+
+
 def cpu_baseline(cfg, seed, budget_s):
     """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn), one
     update on a bounded number of episodes of the same workload."""
@@ -270,8 +283,8 @@ def ppo_loss_delta(learner, env, cfg):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=3)
-    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -352,7 +365,8 @@ def main():
                                    ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
                                     'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
                             peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
-                            traffic=pmc_traffic(*WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
+                            traffic=pmc_traffic(*WgradGemmTimer.KERNELS),
+                            mfma_busy=pmc_mfma_busy(*WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
                             flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3

@@ -24,10 +24,12 @@ run_prof() {
 run_pmc() {
   # HBM traffic counters, one counter group per pass (FETCH_SIZE and WRITE_SIZE do not fit together)
   cd /tmp && export TMPDIR=/tmp
-  for c in FETCH_SIZE WRITE_SIZE; do
+  # one counter group per pass: HBM read bytes, HBM write bytes, MFMA busy cycles + GPU clock
+  for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+    name=$(echo $c | cut -d' ' -f1)
     # only the two roofline kernels (many more dispatches crash the counter-collection tool)
-    timeout -k 10 900 rocprofv3 --pmc $c --kernel-include-regex "k_attn_decode|k_gemm<2, 2, 1, 2, 2, true, true|k_gemm_ws<true, true" -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$c -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-loss-delta "$@" > $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log 2>&1
-    rc=$?; tail -2 $GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log
+    timeout -k 10 900 rocprofv3 --pmc $c --kernel-include-regex "k_attn_decode|k_gemm<2, 2, 1, 2, 2, true, true|k_gemm_ws<true, true" -d $GRAFT_REPO_ROOT/gpurun_out/pmc_$name -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-loss-delta "$@" > $GRAFT_REPO_ROOT/gpurun_out/pmc_$name.log 2>&1
+    rc=$?; tail -2 $GRAFT_REPO_ROOT/gpurun_out/pmc_$name.log
     if [ $rc -ne 0 ]; then echo "pmc $c rc=$rc"; exit $rc; fi
   done
   cd $GRAFT_REPO_ROOT && python3 tools/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.txt; cat gpurun_out/pmc_summary.txt

@@ -175,7 +175,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
   constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
   __shared__ float Qs[TQ][KST], dOs[TQ][KST];
   __shared__ float Ls[TQ], Dls[TQ];
-  __shared__ float Ps[4][16][PST], Ds[4][16][PST];
+  // one per-wave tile image, used for P~ (dV) and then for dS (dK): 26.6 KB of LDS per workgroup,
+  // six resident per CU, so the C3 grid is one round
+  __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
   const int j0 = blockIdx.x * TK;
@@ -215,6 +217,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
         Dls[tid] = ii < n ? a.Dl[(int64_t)bh * n + ii] : 0.f;
       }
       __syncthreads();
+      float dsr[4][4];
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub) {
         f32x4v st = f32x4v{0.f, 0.f, 0.f, 0.f}, dpt = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -245,17 +248,24 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
           float z = 1.f;
           if (a.thresh && ok) z = (kq[r] >= a.thresh) ? a.inv_keep : 0.f;
           Ps[w][4 * lg + r][il] = p * z;
-          Ds[w][4 * lg + r][il] = p * (dpt[r] * z - Dls[il]);
+          dsr[sub][r] = p * (dpt[r] * z - Dls[il]);
         }
       }
       wave_sync();
 #pragma unroll
       for (int d = 0; d < ND; ++d)
 #pragma unroll
-        for (int s = 0; s < TQ / 4; ++s) {
-          dv[d] = mfma16(Ps[w][lr][4 * s + lg], dOs[4 * s + lg][16 * d + lr], dv[d]);
-          dk[d] = mfma16(Ds[w][lr][4 * s + lg], Qs[4 * s + lg][16 * d + lr], dk[d]);
-        }
+        for (int s = 0; s < TQ / 4; ++s) dv[d] = mfma16(Ps[w][lr][4 * s + lg], dOs[4 * s + lg][16 * d + lr], dv[d]);
+      wave_sync();
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ps[w][4 * lg + r][16 * sub + lr] = dsr[sub][r];
+      wave_sync();
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int s = 0; s < TQ / 4; ++s) dk[d] = mfma16(Ps[w][lr][4 * s + lg], Qs[4 * s + lg][16 * d + lr], dk[d]);
       wave_sync();
     }
   }
