@@ -161,7 +161,9 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
   }
   const int r0 = blockIdx.x * LN_ROWS;
   for (int rb = w * LN_R; rb < LN_ROWS; rb += LN_WAVES * LN_R) {
-    float g[LN_R][DPL], xv[LN_R][DPL], rs[LN_R], mu[LN_R];
+    // every operand of the wave's LN_R rows (incoming residual gradient included) is loaded
+    // before the first reduction: one memory round trip per row group
+    float g[LN_R][DPL], xv[LN_R][DPL], dr[LN_R][DPL], rs[LN_R], mu[LN_R];
 #pragma unroll
     for (int q = 0; q < LN_R; ++q) {
       const int t = r0 + rb + q;
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
         if (g2 && in) gv += g2[(int64_t)t * ldg2 + c];
         g[q][k] = gv;
         xv[q][k] = in ? x[(int64_t)t * d + c] : 0.f;
+        dr[q][k] = (dres && in) ? dres[(int64_t)t * d + c] : 0.f;
       }
     }
 #pragma unroll
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
           const int c = lane + 64 * k;
           if (c < d) {
             float v = rs[q] * (gm[k] - ma - xh[k] * mb);
-            if (dres) v += dres[(int64_t)t * d + c];
+            if (dres) v += dr[q][k];
             dx[(int64_t)t * d + c] = v;
           }
         }
@@ -341,24 +344,32 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, i
 
 // dst[c] += sum_k part[k][c]: 64 columns per block; wave w sums chunks w, w + 4, ... with four
 // interleaved accumulators; fixed combination order (deterministic)
-__global__ __launch_bounds__(256) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
-  __shared__ float red[4][64];
+// dst[c] += sum over chunks of part[chunk][c]: 16 waves per 64 columns, wave w sums chunks w,
+// w + 16, ... in four chains (loads in flight), then a fixed-order sum of the 16 wave totals
+constexpr int CS_WAVES = 16;
+__global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
+  __shared__ float red[CS_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < cols) {
     int k = w;
-    for (; k + 12 < chunks; k += 16) {
+    for (; k + 3 * CS_WAVES < chunks; k += 4 * CS_WAVES) {
       s0 += part[(int64_t)k * cols + c];
-      s1 += part[(int64_t)(k + 4) * cols + c];
-      s2 += part[(int64_t)(k + 8) * cols + c];
-      s3 += part[(int64_t)(k + 12) * cols + c];
+      s1 += part[(int64_t)(k + CS_WAVES) * cols + c];
+      s2 += part[(int64_t)(k + 2 * CS_WAVES) * cols + c];
+      s3 += part[(int64_t)(k + 3 * CS_WAVES) * cols + c];
     }
-    for (; k < chunks; k += 4) s0 += part[(int64_t)k * cols + c];
+    for (; k < chunks; k += CS_WAVES) s0 += part[(int64_t)k * cols + c];
   }
   red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (w == 0 && c < cols) dst[c] += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (w == 0 && c < cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < CS_WAVES; ++j) v += red[j][lane];
+    dst[c] += v;
+  }
 }
 
 // discrete action-embedding gradient: part[chunk][a][c] = sum over rows of the chunk with
@@ -549,7 +560,7 @@ int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* ds
   XTRL_REQUIRE((int64_t)chunks * cols <= c.D->part_floats, "train: partial-sum workspace too small");
   hipLaunchKernelGGL(k_colsum_part, dim3(blocks(cols, 256), chunks), dim3(256), 0, c.s, src, ld, rows, cols,
                      chunk_rows, rw, ld_rw, rw_scale, c.D->part);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 64)), dim3(256), 0, c.s, c.D->part, chunks, cols, dst);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 64)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, chunks, cols, dst);
   XTRL_LAUNCHED("train colsum");
   return XTRL_OK;
 }
@@ -570,7 +581,7 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
   else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
   else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
   else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 64)), dim3(256), 0, c.s, c.D->part, nb, d, dgamma);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 64)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
   XTRL_LAUNCHED("train ln_bwd");
   return XTRL_OK;
 }
@@ -800,7 +811,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");
     hipLaunchKernelGGL(k_embed_grad_part, dim3(blocks(d, 256), chunks), dim3(256), 0, s, D->dx, d, D->prev_action,
                        D->dewa + d, 2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
-    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 64)), dim3(256), 0, s, D->part, chunks, D->A * d,
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 64)), dim3(64 * CS_WAVES), 0, s, D->part, chunks, D->A * d,
                        c.G(D->act_emb));
     XTRL_LAUNCHED("train embed grad");
   }
