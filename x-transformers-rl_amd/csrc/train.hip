@@ -29,12 +29,11 @@ struct EmbedArgs {
   float keep;
 };
 
-constexpr int EMB_TOK = 4, EMB_MAXS = 32;
+constexpr int EMB_TOK = 32, EMB_U = 8, EMB_MAXS = 32;
 // block: EMB_TOK tokens x all d columns; thread c keeps its project_in / to_state_embed rows in
-// registers (S <= EMB_MAXS); every input of the block's tokens is loaded before the first store
-// (the stores may alias the inputs as far as the compiler knows), so the loads are in flight together
+// registers (S <= EMB_MAXS) and walks the block's tokens EMB_U at a time, every input of a batch
+// loaded before its first store (the stores may alias the inputs as far as the compiler knows)
 __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
-  const int t0 = blockIdx.x * EMB_TOK;
   for (int c = threadIdx.x; c < a.d; c += 256) {
     float wp[EMB_MAXS], ws[EMB_MAXS];
 #pragma unroll
@@ -44,47 +43,49 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
     }
     const float bse = a.b_se[c], re = a.reward_embed[c];
     const float bemb = a.continuous ? a.act_emb_b[c] : 0.f;
-    float pin[EMB_TOK], se[EMB_TOK], rw[EMB_TOK], ap[EMB_TOK], an[EMB_TOK], le[EMB_TOK];
+    for (int t0 = blockIdx.x * EMB_TOK; t0 < min(a.T, (int)(blockIdx.x + 1) * EMB_TOK); t0 += EMB_U) {
+      float pin[EMB_U], se[EMB_U], rw[EMB_U], ap[EMB_U], an[EMB_U], le[EMB_U];
 #pragma unroll
-    for (int u = 0; u < EMB_TOK; ++u) {
-      const int t = min(t0 + u, a.T - 1);
-      const float* st = a.swr + (int64_t)t * (a.S + 1);
-      float sp = 0.f, ss = 0.f;
+      for (int u = 0; u < EMB_U; ++u) {
+        const int t = min(t0 + u, a.T - 1);
+        const float* st = a.swr + (int64_t)t * (a.S + 1);
+        float sp = 0.f, ss = 0.f;
 #pragma unroll
-      for (int s = 0; s < EMB_MAXS; ++s) {
-        if (s < a.S) {
-          const float x = st[s];
-          sp += x * wp[s];
-          ss += x * ws[s];
+        for (int s = 0; s < EMB_MAXS; ++s) {
+          if (s < a.S) {
+            const float x = st[s];
+            sp += x * wp[s];
+            ss += x * ws[s];
+          }
         }
-      }
-      pin[u] = sp;
-      se[u] = ss + bse;
-      rw[u] = st[a.S];
-      if (a.continuous) {
-        const float* w = a.act_emb + (int64_t)c * a.A;
-        float p = 0.f, q = 0.f;
-        for (int k = 0; k < a.A; ++k) {
-          p += a.prev_af[(int64_t)t * a.A + k] * w[k];
-          q += a.next_af[(int64_t)t * a.A + k] * w[k];
+        pin[u] = sp;
+        se[u] = ss + bse;
+        rw[u] = st[a.S];
+        if (a.continuous) {
+          const float* w = a.act_emb + (int64_t)c * a.A;
+          float p = 0.f, q = 0.f;
+          for (int k = 0; k < a.A; ++k) {
+            p += a.prev_af[(int64_t)t * a.A + k] * w[k];
+            q += a.next_af[(int64_t)t * a.A + k] * w[k];
+          }
+          ap[u] = p + bemb;
+          an[u] = q + bemb;
+        } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
+          const int p = a.prev_a[t], q = a.next_a[t];
+          ap[u] = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
+          an[u] = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
         }
-        ap[u] = p + bemb;
-        an[u] = q + bemb;
-      } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
-        const int p = a.prev_a[t], q = a.next_a[t];
-        ap[u] = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
-        an[u] = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
+        le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + c] : 0.f;
       }
-      le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + c] : 0.f;
-    }
 #pragma unroll
-    for (int u = 0; u < EMB_TOK; ++u) {
-      const int t = t0 + u;
-      if (t >= a.T) break;
-      a.x0[(int64_t)t * a.d + c] = pin[u] + (ap[u] + (rw[u] * re) * a.keep);
-      a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se[u];
-      a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an[u];
-      if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = le[u];
+      for (int u = 0; u < EMB_U; ++u) {
+        const int t = t0 + u;
+        if (t >= a.T) break;
+        a.x0[(int64_t)t * a.d + c] = pin[u] + (ap[u] + (rw[u] * re) * a.keep);
+        a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se[u];
+        a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an[u];
+        if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = le[u];
+      }
     }
   }
 }
@@ -108,14 +109,16 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   const float* xr = x + (int64_t)t * d;
-  float v[kMaxDPerLane];
-  float s = 0.f;
+  float v[kMaxDPerLane], gm[kMaxDPerLane];   // gamma loaded with the row: one round trip
 #pragma unroll
   for (int k = 0; k < kMaxDPerLane; ++k) {
     const int c = lane + 64 * k;
     v[k] = c < d ? xr[c] : 0.f;
-    s += v[k];
+    gm[k] = c < d ? gamma[c] : 0.f;
   }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxDPerLane; ++k) s += v[k];
   const float mean = wave_sum(s) / (float)d;
   float q = 0.f;
 #pragma unroll
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
   for (int k = 0; k < kMaxDPerLane; ++k) {
     const int c = lane + 64 * k;
     if (c < d) {
-      const float y = ((v[k] - mean) * rstd) * gamma[c];
+      const float y = ((v[k] - mean) * rstd) * gm[k];
       y1[(int64_t)t * ld1 + c] = y;
       if (y2) y2[(int64_t)t * ld2 + c] = y;
     }
