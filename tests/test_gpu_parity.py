@@ -214,6 +214,30 @@ def test_attention_dropout_mask_is_host_philox_stream():
     tol(vf.grad, vd.grad, 1e-4, 1e-5)
 
 
+@pytest.mark.parametrize('p', [0.25, 0.1])
+def test_ff_dropout_mask_is_host_philox_stream(p):
+    """FF dropout keep mask (xtrl_ff_dropout_mask, the bits the GELU_DROP GEMM epilogue draws) equals
+    the host Philox stream (oracle/philox.py).  p a multiple of 1/256 (byte mode): keep(m, n) = byte
+    (m & 3) of word ((m >> 3) & 3) of philox4x32(n, 2 (m >> 5) + ((m >> 2) & 1), off, FIELD_FF_DROPOUT
+    sub 1; seed) >= 256 p; else (word mode): word (m & 3) of philox4x32(n, m >> 2, off, FIELD_FF_DROPOUT
+    sub 0; seed) >= p 2^32.  Keep fraction ~ 1 - p."""
+    from xtrl_amd.train import ff_dropout_mask
+    from oracle import philox as P
+    M, N, seed, off = 200, 70, 987654321, 11
+    got = ff_dropout_mask(M, N, p, seed, off, DEV).cpu().numpy().astype(bool)
+    m, n = np.arange(M)[:, None], np.arange(N)[None, :]
+    m, n = np.broadcast_to(m, (M, N)), np.broadcast_to(n, (M, N))
+    if float(p * 256).is_integer():
+        words = P.philox4x32(n, ((m >> 5) << 1) | ((m >> 2) & 1), off, P._c3(P.FIELD_FF_DROPOUT, 1), seed)
+        w = np.choose((m >> 3) & 3, words)
+        want = ((w >> (8 * (m & 3))) & 0xFF) >= int(p * 256)
+    else:
+        words = P.philox4x32(n, m >> 2, off, P._c3(P.FIELD_FF_DROPOUT, 0), seed)
+        want = np.choose(m & 3, words) >= np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
+    np.testing.assert_array_equal(got, want)
+    assert abs(got.mean() - (1 - p)) < 0.02
+
+
 # ----------------------------------------------------------------------------------------------
 # rollout (decode step, sampling, synthetic Sim) vs the oracle's batch-1 reference loop
 # ----------------------------------------------------------------------------------------------

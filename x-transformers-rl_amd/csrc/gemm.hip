@@ -91,6 +91,21 @@ __device__ __forceinline__ bool epi_v4_ok(const GemmArgs& a, const float* C) {
   return ok;
 }
 
+// FF dropout keep bits in byte mode (GemmArgs::drop_thresh8, p a multiple of 1/256): element (m, n)
+// keeps iff byte (m & 3) of word ((m >> 3) & 3) of philox(seed; n, 2 (m >> 5) + ((m >> 2) & 1),
+// drop_off, FIELD_FF_DROPOUT sub 1) is >= drop_thresh8 — the 16 rows of a 32-row MFMA tile one lane
+// holds (mb + 8 g + q, mb = 32-aligned base + 4 (lane >> 5)) share one block.  k_ff_mask (train.hip)
+// draws the same bits.
+__device__ __forceinline__ u32x4_t ff_block8(const GemmArgs& a, int n, int mb) {
+  return philox4x32_10((uint32_t)n, (uint32_t)(((mb >> 5) << 1) | ((mb >> 2) & 1)), a.drop_off,
+                       rng_c3(FIELD_FF_DROPOUT, 1), a.seed);
+}
+// the four bytes of word g (rows mb + 8 g + 0..3) as four "words" compared against drop_thresh8
+__device__ __forceinline__ u32x4_t ff_bytes8(const u32x4_t& kb, int g) {
+  const uint32_t w = g == 0 ? kb.x : (g == 1 ? kb.y : (g == 2 ? kb.z : kb.w));
+  return {w & 0xFFu, (w >> 8) & 0xFFu, (w >> 16) & 0xFFu, w >> 24};
+}
+
 // Row-vector epilogue.  The element-wise stage that reads no operand (bias, activation, dropout,
 // saved derivative) runs in the MFMA layout — one Philox block still covers a column's four rows —
 // then a quad transpose gives every lane four consecutive columns of one row, so the operand reads
@@ -118,12 +133,16 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
     for (int i = 0; i < TM; ++i) {
       const int mb = m0 + wm * 32 * TM + 32 * i + 4 * (lane >> 5);
       float v[4][4], ax[4][4];
+      // byte-mode keep bits (drop_thresh8): ONE Philox block covers this lane's 16 rows of column n
+      const u32x4_t kb = (DROP && a.drop_thresh8) ? ff_block8(a, n, mb) : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         u32x4_t kw{0u, 0u, 0u, 0u};
-        if (DROP && a.drop_thresh)
+        if (DROP && a.drop_thresh && !a.drop_thresh8)
           kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
                              a.seed);
+        else if (DROP && a.drop_thresh8)
+          kw = ff_bytes8(kb, g);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float x = acc[i][j][4 * g + q] + bn;
@@ -138,7 +157,7 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
             aux_o = cdf + x * pdf;
             x = (0.5f * x) * (1.0f + erff(x * 0.70710678118654752f));
             if (a.drop_thresh) {
-              const bool keep = word >= a.drop_thresh;
+              const bool keep = a.drop_thresh8 ? word >= a.drop_thresh8 : word >= a.drop_thresh;
               x = keep ? x * a.inv_keep : 0.f;
               aux_o = keep ? aux_o * a.inv_keep : 0.f;
             }
@@ -239,13 +258,17 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
         if constexpr (RES) rr[r] = a.R[(int64_t)mc * a.ldr + nc];
         old[r] = acc_c ? C[(int64_t)mc * a.ldc + nc] : 0.f;
       }
+      const u32x4_t kb = (DROP && a.drop_thresh8) ? ff_block8(a, n, mb) : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         // rows mb + 8g + 0..3 (a 4-aligned group): one Philox block gives their four keep words
+        // (byte mode: the lane's one block gives all 16)
         u32x4_t kw{0u, 0u, 0u, 0u};
-        if (DROP && a.drop_thresh)
+        if (DROP && a.drop_thresh && !a.drop_thresh8)
           kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
                              a.seed);
+        else if (DROP && a.drop_thresh8)
+          kw = ff_bytes8(kb, g);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = 4 * g + q;
@@ -262,7 +285,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
             aux_o = cdf + v * pdf;
             v = (0.5f * v) * (1.0f + erff(v * 0.70710678118654752f));
             if (a.drop_thresh) {
-              const bool keep = word >= a.drop_thresh;
+              const bool keep = a.drop_thresh8 ? word >= a.drop_thresh8 : word >= a.drop_thresh;
               v = keep ? v * a.inv_keep : 0.f;
               aux_o = keep ? aux_o * a.inv_keep : 0.f;
             }

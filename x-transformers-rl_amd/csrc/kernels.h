@@ -45,6 +45,7 @@ struct GemmArgs {
   uint64_t seed = 0;              // dropout (EPI_GELU_DROP): keep(m, n) =
   uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT) word (m & 3)
   uint32_t drop_thresh = 0;       //   >= drop_thresh (0: no dropout)
+  uint32_t drop_thresh8 = 0;      // != 0: byte-mode keep bits (p = drop_thresh8 / 256 exactly), see ff_block8
   float inv_keep = 1.f;
   const uint8_t* row_mask = nullptr;   // rows m with row_mask[m] == 0 are not stored (dead envs)
   float* rowsum = nullptr;        // += row sums of A (rows >= rowsum_m0, at rowsum[m - rowsum_m0]) —
@@ -73,6 +74,12 @@ int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias
 int layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, hipStream_t s);
 
 // dropout threshold of probability p on a uint32 word: keep iff word >= thresh
+// p * 256 when that is an integer in [1, 255] (byte-mode FF dropout keep bits), else 0
+inline uint32_t dropout_thresh8(float p) {
+  const double t = (double)p * 256.0;
+  return (t >= 1.0 && t <= 255.0 && t == (double)(int)t) ? (uint32_t)t : 0u;
+}
+
 inline uint32_t dropout_thresh(float p) {
   if (!(p > 0.f)) return 0u;
   const double th = (double)p * 4294967296.0;

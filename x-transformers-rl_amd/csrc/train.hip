@@ -434,10 +434,21 @@ __global__ void k_copy_col(const float* src, int ld, float* dst, int lddst, int 
   if (r < rows) dst[(int64_t)r * lddst] = src[(int64_t)r * ld];
 }
 
-__global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint64_t seed, uint32_t off) {
+// the FF dropout keep mask of the GELU_DROP epilogue (gemm.hip): word mode (one Philox block per
+// 4 rows of a column) or byte mode (thresh8 != 0: one block per 16 rows, see ff_block8)
+__global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint32_t thresh8, uint64_t seed,
+                          uint32_t off) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  if (thresh8) {
+    const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(((m >> 5) << 1) | ((m >> 2) & 1)), off,
+                                    rng_c3(FIELD_FF_DROPOUT, 1), seed);
+    const int g = (m >> 3) & 3;
+    const uint32_t w = g == 0 ? r.x : (g == 1 ? r.y : (g == 2 ? r.z : r.w));
+    mask[i] = (uint8_t)(((w >> (8 * (m & 3))) & 0xFFu) >= thresh8);
+    return;
+  }
   const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(m >> 2), off, rng_c3(FIELD_FF_DROPOUT, 0), seed);
   const int q = m & 3;
   const uint32_t w = q == 0 ? r.x : (q == 1 ? r.y : (q == 2 ? r.z : r.w));
@@ -529,6 +540,7 @@ int linear_fwd(const Ctx& c, const float* A, int lda, const float* W, const floa
     g.seed = c.D->seed;
     g.drop_off = drop_off;
     g.drop_thresh = dropout_thresh(c.D->dropout);
+    g.drop_thresh8 = dropout_thresh8(c.D->dropout);
     g.inv_keep = c.D->dropout > 0.f ? 1.f / (1.f - c.D->dropout) : 1.f;
   }
   return gemm_run(g, 0, 0, epi, c.s);
@@ -838,7 +850,7 @@ extern "C" int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64
   XTRL_REQUIRE(mask && M >= 0 && N >= 0 && p >= 0.f && p < 1.f, "ff_dropout_mask: bad arguments");
   if ((int64_t)M * N == 0) return XTRL_OK;
   hipLaunchKernelGGL(xtrl::k_ff_mask, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0,
-                     xtrl::as_stream(stream), mask, M, N, xtrl::dropout_thresh(p), seed, offset);
+                     xtrl::as_stream(stream), mask, M, N, xtrl::dropout_thresh(p), xtrl::dropout_thresh8(p), seed, offset);
   XTRL_LAUNCHED("ff_dropout_mask");
   return XTRL_OK;
 }
