@@ -360,7 +360,7 @@ def main():
             x6 = os.environ.get('XTRL_GEMM_F32', '0') in ('', '0')
             peak = X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
             roofline = dict(kernel='k_gemm_ws<T,T> / k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, '
-                                   '128x128 tiles, split-K over 256 workgroups, on the backward side stream beside '
+                                   '128x128 tiles, split-K over 192 workgroups, on the backward side stream beside '
                                    'the input-gradient chain; the largest kernel of the update; fp32 products as ' +
                                    ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
                                     'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),

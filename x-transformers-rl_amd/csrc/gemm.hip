@@ -1317,16 +1317,17 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
   // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
   // 128 x 128 tiles (2 workgroups / CU by registers) when the weight is large, else 64 x 64 (4 / CU);
-  // split the tokens until 256 workgroups (half a resident round: the learn step runs these on a
-  // side stream beside the input-gradient chain, which fills the rest; C3 update 174.6 / 171.5 /
-  // 172.6 ms at 512 / 256 / 128) keeping at least 8 K-slabs (256 tokens) per split so the pipeline
+  // split the tokens until 192 workgroups (three quarters of a resident round: the learn step runs
+  // these on a side stream beside the input-gradient chain, whose kernels take the free CUs; A/B on
+  // one box, learn ms: 256 / 224 / 192 / 160 / 128 workgroups = 130.0 / 129.5 / 128.6 / 128.6 / 130.1)
+  // keeping at least 8 K-slabs (256 tokens) per split so the pipeline
   // reaches steady state (more splits cost more partial-tile traffic in phase 2 than they save)
   const bool big = (int64_t)N * K >= 256 * 256;
   const int tm = big ? 128 : 64;
   const int64_t tiles = (int64_t)((N + tm - 1) / tm) * ((K + tm - 1) / tm);
   static const int64_t big_target = [] {   // XTRL_WGRAD_TARGET: workgroups of the 128 x 128 launch
     const char* e = getenv("XTRL_WGRAD_TARGET");
-    return (int64_t)(e ? atoi(e) : 256);
+    return (int64_t)(e ? atoi(e) : 192);
   }();
   const int64_t target = big ? big_target : 1024;
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (M + 255) / 256));
