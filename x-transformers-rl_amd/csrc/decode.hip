@@ -32,7 +32,9 @@ constexpr float F32_EPS = 1.1920928955078125e-07f;
 // ---------------------------------------------------------------------------------------------
 // embeddings (one wave per env)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_embed(const XtrlDecodeDesc D, int t) {
+// ln_gamma != NULL (d <= 256): the row is also layer-normalised into xn with the first layer's
+// pre-norm gamma, in k_layernorm's order of operations (bit-identical; one launch less per step)
+__global__ __launch_bounds__(256) void k_embed(const XtrlDecodeDesc D, int t, const float* ln_gamma) {
   const int lane = threadIdx.x & 63;
   const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= D.E) return;
@@ -50,7 +52,8 @@ __global__ __launch_bounds__(256) void k_embed(const XtrlDecodeDesc D, int t) {
   wave_sync();
   const float nr = ns[S];
   const int a = D.continuous ? 0 : D.prev_action[e];
-  for (int c = lane; c < d; c += 64) {
+  float xs[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = lane, k = 0; c < d; c += 64, ++k) {
     float p = 0.f, se = 0.f;
     for (int s = 0; s < S; ++s) {
       p += ns[s] * D.w_pin[c * S + s];
@@ -66,8 +69,31 @@ __global__ __launch_bounds__(256) void k_embed(const XtrlDecodeDesc D, int t) {
       act = a >= 0 ? D.act_emb[a * d + c] : 0.f;
     }
     const float rew = D.no_reward_cond ? 0.f : nr * D.reward_embed[c];
-    D.x[(int64_t)e * d + c] = p + (act + rew);
+    const float xv = p + (act + rew);
+    D.x[(int64_t)e * d + c] = xv;
+    if (k < 4) xs[k] = xv;
     D.ac_in[(int64_t)e * D.in_dim + d + c] = se + D.b_se[c];
+  }
+  if (ln_gamma) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < d) s += xs[k];
+    const float mean = wave_sum(s) / (float)d;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (lane + 64 * k < d) {
+        const float dlt = xs[k] - mean;
+        q += dlt * dlt;
+      }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d) D.xn[(int64_t)e * d + c] = ((xs[k] - mean) * rstd) * ln_gamma[c];
+    }
   }
 }
 
@@ -322,12 +348,14 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode: t=%d outside [0, %d)", t, D->Tmax);
   const int E = D->E, d = D->d, I = D->H * D->dh;
-  hipLaunchKernelGGL(k_embed, dim3((E + 3) / 4), dim3(256), 0, s, *D, t);
+  const bool embed_ln = d <= 256;   // layer 0's pre-norm inside the embedding kernel
+  hipLaunchKernelGGL(k_embed, dim3((E + 3) / 4), dim3(256), 0, s, *D, t,
+                     embed_ln ? D->layers[0].ln_attn : (const float*)nullptr);
   XTRL_LAUNCHED("embed");
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
     // pre-norm once per row (a LN prologue inside the GEMM would be recomputed by every column tile)
-    int rc = layernorm_f32(D->x, d, Ly.ln_attn, D->xn, d, E, d, s);
+    int rc = (l == 0 && embed_ln) ? XTRL_OK : layernorm_f32(D->x, d, Ly.ln_attn, D->xn, d, E, d, s);
     if (rc) return rc;
     if ((rc = gemm_f32(D->xn, d, Ly.w_qkv, d, Ly.b_qkv, nullptr, nullptr, 0, D->qkv, D->n_qkv, nullptr, 0, E,
                        D->n_qkv, d, XTRL_ACT_NONE, s)))
