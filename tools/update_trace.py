@@ -71,6 +71,14 @@ def show(path):
         print(f'\nlearn idle: {idle / 1e6:.2f} ms in {len(gaps)} gaps; largest:')
         for g_us, i in gaps[:12]:
             print(f'  {g_us:8.1f} us before {short(names[i])}  (after {short(names[i - 1])})')
+        # per queue / stream: busy time in the learn phase (the input-gradient chain vs the side stream)
+        qkey = 'Stream_Id' if 'Stream_Id' in rows[0] else 'Queue_Id'
+        per_q = defaultdict(float)
+        for i in seg:
+            per_q[rows[i].get(qkey)] += dur[i]
+        lw = (int(rows[seg[-1]]['End_Timestamp']) - int(rows[seg[0]]['Start_Timestamp'])) / 1e3
+        print(f'learn busy per {qkey} (wall {lw / 1e3:.2f} ms): ' +
+              ', '.join(f'{q}: {us / 1e3:.2f} ms' for q, us in sorted(per_q.items(), key=lambda kv: -kv[1])))
         by_next = defaultdict(float)
         for g_us, i in gaps:
             by_next[short(names[i])] += g_us
