@@ -9,9 +9,12 @@
 //   compute_done_loss    :406-411   (sigmoid + F.binary_cross_entropy, log clamped at -100)
 //   combination          :939-978   ((w_a actor + w_c critic)[mask].mean() + (wm.mean() + done.mean()) w_ar)
 //
-// k_loss_tokens (one wave per token, lanes over the value bins) -> k_loss_reduce (one workgroup:
-// deterministic masked statistics + the per-token actor / critic terms + final scalars) ->
-// k_loss_bwd (one wave per token) writes d/draw_actions, d/dvalues, d/dpred_raw, d/ddone_logit.
+// k_loss_tokens (one wave per token, lanes over the value bins; each block of 4 tokens leaves the
+// partial sums of the masked statistics in its tokens' spare slots) -> k_loss_stats (one workgroup:
+// fixed-order sum of the block partials -> advantage mean / unbiased variance, critic means,
+// gradient coefficients) -> k_loss_actor (thread per token: actor / critic terms, block partials)
+// -> k_loss_final (the loss scalars) -> k_loss_bwd (one wave per token) writes d/draw_actions,
+// d/dvalues, d/dpred_raw, d/ddone_logit.  Every sum is in double in a fixed order (deterministic).
 // Gradients follow PyTorch's autograd rules for min (ties split), clamp (inclusive bounds),
 // gaussian_nll_loss (straight-through var clamp) and binary_cross_entropy (eps 1e-12).
 #include "common.h"
@@ -21,7 +24,16 @@ namespace {
 
 constexpr float F32_EPS = 1.1920928955078125e-07f;
 constexpr int NT = XTRL_LOSS_TOK;
-enum Tok { T_ADV = 0, T_V = 1, T_VOLD = 2, T_CEU = 3, T_CEC = 4, T_LP = 5, T_ENT = 6, T_WM = 7, T_BCE = 8, T_ACT = 9 };
+enum Tok { T_ADV = 0, T_V = 1, T_VOLD = 2, T_CEU = 3, T_CEC = 4, T_LP = 5, T_ENT = 6, T_WM = 7, T_BCE = 8, T_ACT = 9,
+           T_SPARE = 10 };
+// partial sums of a block: doubles in the spare slots of the block's first token
+__device__ __forceinline__ double* part_slot(float* tok, int64_t first, int k) {
+  return reinterpret_cast<double*>(tok + first * NT + T_SPARE + 2 * k);
+}
+// pass-1 statistics
+enum Part { P_NMASK = 0, P_ADV, P_ADV2, P_CEU, P_CEC, P_WM, P_NWM, P_BCE, P_KCRIT, P_N1 };
+enum Part2 { Q_ACTOR = 0, Q_CRITIC, Q_AC, Q_N };
+static_assert(T_SPARE + 2 * P_N1 <= NT && T_SPARE % 2 == 0, "partial sums must fit a token's spare slots");
 
 // softmax statistics of a B-bin logit row held by a wave (lanes strided over bins)
 struct RowStats {
@@ -124,11 +136,18 @@ __device__ void cont_terms(const float* raw, float x, int i, int squash, ContTer
 }
 
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool critic_zeroed(float v, float ret, float vold, float clip) {
+  const float lo = vold - clip, hi = vold + clip;
+  return ((ret < v) && (v < lo)) || ((hi < v) && (v < ret));
+}
+
 __global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
-  const int lane = threadIdx.x & 63;
-  const int tk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ double shp[4][P_N1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = D.b * D.n;
-  if (tk >= N) return;
+  const int tk0 = blockIdx.x * 4 + w;
+  const bool valid = tk0 < N;   // (waves past N evaluate the last token and store nothing)
+  const int tk = valid ? tk0 : N - 1;
   const int bi = tk / D.n, ti = tk - bi * D.n;
   const bool mask = ti < D.lens[bi];
   float* tok = D.tok + (int64_t)tk * NT;
@@ -140,8 +159,9 @@ __global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
   const float ceu = hl_ce(D, vals, rn.lse, ret, lane);
   const float cec = hl_ce(D, vals, rn.lse, fminf(fmaxf(ret, -D.value_clip), D.value_clip), lane);
   // world model: predictions at t predict the normalised state-with-reward at t + 1
+  const bool wm_on = mask && ti < D.n - 1;
   float wm = 0.f;
-  if (mask && ti < D.n - 1) {
+  if (wm_on) {
     for (int c = lane; c < D.S1; c += 64) {
       const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
       const float mean = pr[2 * c];
@@ -153,22 +173,43 @@ __global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
     wm = wave_sum(wm);
   }
   if (lane == 0) {
-    tok[T_ADV] = ret - ro.dot_centers;
-    tok[T_V] = rn.dot_centers;
-    tok[T_VOLD] = ro.dot_centers;
-    tok[T_CEU] = ceu;
-    tok[T_CEC] = cec;
-    if (!D.continuous) {
-      DiscreteTerms T;
-      discrete_terms(D.raw_actions + (int64_t)tk * D.A, D.A, D.actions[tk], T);
-      tok[T_LP] = T.lp;
-      tok[T_ENT] = T.ent;
-    }
-    tok[T_WM] = wm;
+    const float adv = ret - ro.dot_centers;
     const float pd = sigmoidf_(D.done_logit[tk]);
     const float y = D.dones[tk] ? 1.f : 0.f;
     const float l1 = fmaxf(logf(pd), -100.f), l0 = fmaxf(logf(1.f - pd), -100.f);
-    tok[T_BCE] = -(y * l1 + (1.f - y) * l0);
+    const float bce = -(y * l1 + (1.f - y) * l0);
+    if (valid) {
+      tok[T_ADV] = adv;
+      tok[T_V] = rn.dot_centers;
+      tok[T_VOLD] = ro.dot_centers;
+      tok[T_CEU] = ceu;
+      tok[T_CEC] = cec;
+      if (!D.continuous) {
+        DiscreteTerms T;
+        discrete_terms(D.raw_actions + (int64_t)tk * D.A, D.A, D.actions[tk], T);
+        tok[T_LP] = T.lp;
+        tok[T_ENT] = T.ent;
+      }
+      tok[T_WM] = wm;
+      tok[T_BCE] = bce;
+    }
+    // this token's share of the masked statistics (k_loss_stats)
+    const bool m = valid && mask;
+    double* sp = shp[w];
+    sp[P_NMASK] = m ? 1.0 : 0.0;
+    sp[P_ADV] = m ? (double)adv : 0.0;
+    sp[P_ADV2] = m ? (double)adv * (double)adv : 0.0;
+    sp[P_CEU] = valid ? (double)ceu : 0.0;
+    sp[P_CEC] = valid ? (double)cec : 0.0;
+    sp[P_WM] = (valid && wm_on) ? (double)wm : 0.0;
+    sp[P_NWM] = (valid && wm_on) ? (double)D.S1 : 0.0;
+    sp[P_BCE] = m ? (double)bce : 0.0;
+    sp[P_KCRIT] = (m && !critic_zeroed(rn.dot_centers, ret, ro.dot_centers, D.value_clip)) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < P_N1) {
+    const int k = threadIdx.x;
+    *part_slot(D.tok, (int64_t)blockIdx.x * 4, k) = ((shp[0][k] + shp[1][k]) + shp[2][k]) + shp[3][k];
   }
 }
 
@@ -200,136 +241,110 @@ __device__ __forceinline__ float dmin_dr(float r, float adv, float lo, float hi)
   return 0.5f * adv + 0.5f * adv * inr;
 }
 
-__device__ __forceinline__ bool critic_zeroed(float v, float ret, float vold, float clip) {
-  const float lo = vold - clip, hi = vold + clip;
-  return ((ret < v) && (v < lo)) || ((hi < v) && (v < ret));
-}
-
-__global__ __launch_bounds__(1024) void k_loss_reduce(const XtrlLossDesc D) {
+// the block partials of k_loss_tokens summed in a fixed order -> masked statistics, advantage mean
+// and unbiased variance (sum of squares about zero, in double), critic means and the gradient
+// coefficients of the mean-reduced HL-Gauss critic
+__global__ __launch_bounds__(1024) void k_loss_stats(const XtrlLossDesc D) {
   __shared__ double sh[16];
-  const int N = D.b * D.n;
-  // pass 1: masked counts and sums (4 tokens per thread in flight)
-  double n_mask = 0, s_adv = 0, s_ceu = 0, s_cec = 0, s_wm = 0, n_wm = 0, s_bce = 0;
-#pragma unroll 4
-  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
-    const int bi = tk / D.n, ti = tk - bi * D.n;
-    const float* tok = D.tok + (int64_t)tk * NT;
-    const bool mask = ti < D.lens[bi];
-    s_ceu += tok[T_CEU];
-    s_cec += tok[T_CEC];
-    if (mask) {
-      n_mask += 1;
-      s_adv += tok[T_ADV];
-      s_bce += tok[T_BCE];
-      if (ti < D.n - 1) {
-        s_wm += tok[T_WM];
-        n_wm += D.S1;
-      }
-    }
+  const int N = D.b * D.n, P = (N + 3) / 4;
+  double acc[P_N1];
+#pragma unroll
+  for (int k = 0; k < P_N1; ++k) acc[k] = 0.0;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < P_N1; ++k) acc[k] += *part_slot(D.tok, (int64_t)p * 4, k);
   }
-  n_mask = block_sum(n_mask, sh);
-  s_adv = block_sum(s_adv, sh);
-  s_ceu = block_sum(s_ceu, sh);
-  s_cec = block_sum(s_cec, sh);
-  s_wm = block_sum(s_wm, sh);
-  n_wm = block_sum(n_wm, sh);
-  s_bce = block_sum(s_bce, sh);
+#pragma unroll
+  for (int k = 0; k < P_N1; ++k) acc[k] = block_sum(acc[k], sh);
+  if (threadIdx.x != 0) return;
+  const double n_mask = acc[P_NMASK], s_adv = acc[P_ADV], n_wm = acc[P_NWM], k_crit = acc[P_KCRIT];
   const float adv_mean = (float)(s_adv / n_mask);
-  // pass 2: unbiased variance of the masked advantages
-  double s_var = 0;
-#pragma unroll 4
-  for (int tk = threadIdx.x; tk < N; tk += blockDim.x) {
-    const int bi = tk / D.n, ti = tk - bi * D.n;
-    if (ti < D.lens[bi]) {
-      const float dlt = D.tok[(int64_t)tk * NT + T_ADV] - adv_mean;
-      s_var += (double)dlt * dlt;
-    }
-  }
-  s_var = block_sum(s_var, sh);
+  const double s_var = acc[P_ADV2] - s_adv * (s_adv / n_mask);
   const float var = n_mask > 1 ? (float)(s_var / (n_mask - 1)) : NAN;
   const float den = sqrtf(fmaxf(var, 1e-5f));
-  const float L = (float)(s_ceu / N), Lc = (float)(s_cec / N);
+  const float L = (float)(acc[P_CEU] / N), Lc = (float)(acc[P_CEC] / N);
+  float* st = D.stats;
+  st[XTRL_LS_AUTOREG] = (float)(acc[P_WM] / n_wm);
+  st[XTRL_LS_DONE] = (float)(acc[P_BCE] / n_mask);
+  st[XTRL_LS_ADV_MEAN] = adv_mean;
+  st[XTRL_LS_ADV_DEN] = den;
+  st[XTRL_LS_L] = L;
+  st[XTRL_LS_LC] = Lc;
+  st[XTRL_LS_NMASK] = (float)n_mask;
+  st[XTRL_LS_NWM] = (float)n_wm;
+  st[XTRL_LS_KCRIT] = (float)k_crit;
+  const float dmin = D.w_critic * (float)(k_crit / n_mask);
+  st[XTRL_LS_DL] = L < Lc ? dmin : (L > Lc ? 0.f : 0.5f * dmin);
+  st[XTRL_LS_DLC] = Lc < L ? dmin : (Lc > L ? 0.f : 0.5f * dmin);
+}
+
+// per-token actor / critic terms (thread per token) with the normalised advantage; T_ACT and the
+// block partials of sum actor, sum critic (all b*n tokens) and the masked weighted sum
+__global__ __launch_bounds__(256) void k_loss_actor(const XtrlLossDesc D) {
+  __shared__ double sh[4][Q_N];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int N = D.b * D.n;
+  const int tk0 = blockIdx.x * 256 + threadIdx.x;
+  const bool valid = tk0 < N;
+  const int tk = valid ? tk0 : N - 1;
+  const int bi = tk / D.n, ti = tk - bi * D.n;
+  const bool mask = ti < D.lens[bi];
+  const float* st = D.stats;
+  const float* tok = D.tok + (int64_t)tk * NT;
+  const float advn = (tok[T_ADV] - st[XTRL_LS_ADV_MEAN]) / st[XTRL_LS_ADV_DEN];
   const float lo = 1.f - D.eps_clip, hi = 1.f + D.eps_clip;
-  // pass 3: per-token actor / critic terms; the inputs of four tokens are read before their T_ACT
-  // stores (which the compiler cannot prove disjoint), so four tokens' loads are in flight
-  double s_actor_all = 0, s_critic_all = 0, s_ac = 0, k_crit = 0;
-  constexpr int U = 4;
-  for (int base = 0; base < N; base += U * blockDim.x) {
-    float adv[U], lp[U], ent[U], v[U], vold[U], ceu[U], cec[U], olp[U], ret[U];
-    bool mask[U], ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tk = base + u * blockDim.x + threadIdx.x;
-      ok[u] = tk < N;
-      const int tc = ok[u] ? tk : 0;
-      const int bi = tc / D.n, ti = tc - bi * D.n;
-      const float* tok = D.tok + (int64_t)tc * NT;
-      mask[u] = ti < D.lens[bi];
-      adv[u] = tok[T_ADV];
-      lp[u] = tok[T_LP];
-      ent[u] = tok[T_ENT];
-      v[u] = tok[T_V];
-      vold[u] = tok[T_VOLD];
-      ceu[u] = tok[T_CEU];
-      cec[u] = tok[T_CEC];
-      olp[u] = D.continuous ? 0.f : D.old_logp[tc];
-      ret[u] = D.returns[tc];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;
-      const int tk = base + u * blockDim.x + threadIdx.x;
-      const float advn = (adv[u] - adv_mean) / den;
-      float actor = 0.f;
-      if (!D.continuous) {
-        const float r = expf(lp[u] - olp[u]);
-        const float rc = fminf(fmaxf(r, lo), hi);
-        actor = -fminf(r * advn, rc * advn) - D.entropy_weight * ent[u];
-      } else {
-        for (int i = 0; i < D.A; ++i) {
-          ContTerms C;
-          cont_terms(D.raw_actions + (int64_t)tk * 2 * D.A, D.actions_f[(int64_t)tk * D.A + i], i, D.squash, C);
-          const float r = expf(C.lp - D.old_logp[(int64_t)tk * D.A + i]);
-          const float rc = fminf(fmaxf(r, lo), hi);
-          actor += -fminf(r * advn, rc * advn) - D.entropy_weight * C.ent;
-        }
-      }
-      const bool zero = critic_zeroed(v[u], ret[u], vold[u], D.value_clip);
-      float critic;
-      if (D.hl_reduction_mean) critic = zero ? 0.f : fminf(L, Lc);
-      else critic = zero ? 0.f : fminf(ceu[u], cec[u]);
-      D.tok[(int64_t)tk * NT + T_ACT] = actor;
-      s_actor_all += actor;
-      s_critic_all += critic;
-      if (mask[u]) {
-        s_ac += actor * D.w_actor + critic * D.w_critic;
-        if (!zero) k_crit += 1;
-      }
+  float actor = 0.f;
+  if (!D.continuous) {
+    const float r = expf(tok[T_LP] - D.old_logp[tk]);
+    const float rc = fminf(fmaxf(r, lo), hi);
+    actor = -fminf(r * advn, rc * advn) - D.entropy_weight * tok[T_ENT];
+  } else {
+    for (int i = 0; i < D.A; ++i) {
+      ContTerms C;
+      cont_terms(D.raw_actions + (int64_t)tk * 2 * D.A, D.actions_f[(int64_t)tk * D.A + i], i, D.squash, C);
+      const float r = expf(C.lp - D.old_logp[(int64_t)tk * D.A + i]);
+      const float rc = fminf(fmaxf(r, lo), hi);
+      actor += -fminf(r * advn, rc * advn) - D.entropy_weight * C.ent;
     }
   }
-  s_actor_all = block_sum(s_actor_all, sh);
-  s_critic_all = block_sum(s_critic_all, sh);
-  s_ac = block_sum(s_ac, sh);
-  k_crit = block_sum(k_crit, sh);
-  if (threadIdx.x == 0) {
-    const float wm_mean = (float)(s_wm / n_wm), done_mean = (float)(s_bce / n_mask);
-    float* st = D.stats;
-    st[XTRL_LS_LOSS] = (float)(s_ac / n_mask) + (wm_mean + done_mean) * D.w_autoreg;
-    st[XTRL_LS_ACTOR] = (float)(s_actor_all / N);
-    st[XTRL_LS_CRITIC] = (float)(s_critic_all / N);
-    st[XTRL_LS_AUTOREG] = wm_mean;
-    st[XTRL_LS_DONE] = done_mean;
-    st[XTRL_LS_ADV_MEAN] = adv_mean;
-    st[XTRL_LS_ADV_DEN] = den;
-    st[XTRL_LS_L] = L;
-    st[XTRL_LS_LC] = Lc;
-    st[XTRL_LS_NMASK] = (float)n_mask;
-    st[XTRL_LS_NWM] = (float)n_wm;
-    st[XTRL_LS_KCRIT] = (float)k_crit;
-    const float dmin = D.w_critic * (float)(k_crit / n_mask);
-    st[XTRL_LS_DL] = L < Lc ? dmin : (L > Lc ? 0.f : 0.5f * dmin);
-    st[XTRL_LS_DLC] = Lc < L ? dmin : (Lc > L ? 0.f : 0.5f * dmin);
+  const bool zero = critic_zeroed(tok[T_V], D.returns[tk], tok[T_VOLD], D.value_clip);
+  float critic;
+  if (D.hl_reduction_mean) critic = zero ? 0.f : fminf(st[XTRL_LS_L], st[XTRL_LS_LC]);
+  else critic = zero ? 0.f : fminf(tok[T_CEU], tok[T_CEC]);
+  if (valid) D.tok[(int64_t)tk * NT + T_ACT] = actor;
+  double q[Q_N];
+  q[Q_ACTOR] = valid ? (double)actor : 0.0;
+  q[Q_CRITIC] = valid ? (double)critic : 0.0;
+  q[Q_AC] = (valid && mask) ? (double)(actor * D.w_actor + critic * D.w_critic) : 0.0;
+#pragma unroll
+  for (int k = 0; k < Q_N; ++k) {
+    const double v = wave_sum_d(q[k]);
+    if (lane == 0) sh[w][k] = v;
   }
+  __syncthreads();
+  if (threadIdx.x < Q_N) {
+    const int k = threadIdx.x;
+    *part_slot(D.tok, (int64_t)blockIdx.x * 256, k) = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
+  }
+}
+
+// the loss scalars from the k_loss_actor block partials (fixed order)
+__global__ __launch_bounds__(256) void k_loss_final(const XtrlLossDesc D) {
+  __shared__ double sh[16];
+  const int N = D.b * D.n, P = (N + 255) / 256;
+  double acc[Q_N] = {0.0, 0.0, 0.0};
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < Q_N; ++k) acc[k] += *part_slot(D.tok, (int64_t)p * 256, k);
+  }
+#pragma unroll
+  for (int k = 0; k < Q_N; ++k) acc[k] = block_sum(acc[k], sh);
+  if (threadIdx.x != 0) return;
+  float* st = D.stats;
+  const double n_mask = st[XTRL_LS_NMASK];
+  st[XTRL_LS_LOSS] = (float)(acc[Q_AC] / n_mask) + (st[XTRL_LS_AUTOREG] + st[XTRL_LS_DONE]) * D.w_autoreg;
+  st[XTRL_LS_ACTOR] = (float)(acc[Q_ACTOR] / N);
+  st[XTRL_LS_CRITIC] = (float)(acc[Q_CRITIC] / N);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -503,8 +518,12 @@ int loss_fwd(const XtrlLossDesc* D, hipStream_t s) {
   const int N = D->b * D->n;
   hipLaunchKernelGGL(k_loss_tokens, dim3((N + 3) / 4), dim3(256), 0, s, *D);
   XTRL_LAUNCHED("loss_tokens");
-  hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(1024), 0, s, *D);
-  XTRL_LAUNCHED("loss_reduce");
+  hipLaunchKernelGGL(k_loss_stats, dim3(1), dim3(1024), 0, s, *D);
+  XTRL_LAUNCHED("loss_stats");
+  hipLaunchKernelGGL(k_loss_actor, dim3((N + 255) / 256), dim3(256), 0, s, *D);
+  XTRL_LAUNCHED("loss_actor");
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(256), 0, s, *D);
+  XTRL_LAUNCHED("loss_final");
   return XTRL_OK;
 }
 
