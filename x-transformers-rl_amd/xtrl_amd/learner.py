@@ -107,7 +107,8 @@ class Agent(nn.Module):
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
         self.model = WorldModelActorCritic(c).to(dev)
-        self.flat = FlatParams(self.model, dev, order=self.model.flat_order())
+        # the minibatch RSNorm mean (xtrl_minibatch_gather) rides behind the gradient: one all-reduce
+        self.flat = FlatParams(self.model, dev, order=self.model.flat_order(), extra=state_dim + 1)
         dist_.broadcast_(self.flat.flat)          # identical initial weights on every rank (DDP semantics)
         if self.gene_pool is not None:
             dist_.broadcast_(self.gene_pool.genes)
@@ -334,14 +335,16 @@ class Agent(nn.Module):
                 else:
                     loss, stats = ops.fused_loss(raw, values, pred_raw, done_logit, K)
                     loss.backward()
-                dist_.mean_(self.flat.grad)
+                # DDP gradient mean (xtrl.py:981); the fused path's RSNorm batch mean (xtrl.py:601) is in
+                # the same buffer, so one collective per optimiser step
+                dist_.mean_(self.flat.grad_ext if fused else self.flat.grad)
                 if probe is not None:
                     probe(epoch, mbi, idx, loss, stats)
                 self.optimizer_step()
                 # RSNorm copy update with the normalised masked rows (xtrl.py:1005, 598-610)
                 with torch.no_grad():
                     if fused:
-                        m = dist_.mean_(g['rs_m'])
+                        m = g['rs_m']   # (averaged over ranks with the gradient above)
                         rsnorm_update(rs_mean, rs_var, m, rs_step)
                     else:
                         mask = (torch.arange(n, device=dev)[None, :] < mb_lens[:, None]).float()
@@ -365,7 +368,7 @@ class Agent(nn.Module):
         bg = getattr(self, '_batch_gather', None)
         if bg is None or bg.n_max < Tmax:
             from .train import BatchGather
-            self._batch_gather = bg = BatchGather(self.cfg, self.batch_size, Tmax, self.device)
+            self._batch_gather = bg = BatchGather(self.cfg, self.batch_size, Tmax, self.device, rs_m=self.flat.extra)
         return bg
 
     def train_step(self, b, n):

@@ -10,7 +10,9 @@ from torch import nn
 
 
 class FlatParams:
-    def __init__(self, module: nn.Module, device, order=None):
+    def __init__(self, module: nn.Module, device, order=None, extra=0):
+        """``extra`` floats follow the gradient buffer (``grad_ext = grad | extra``): per-step
+        statistics stored there ride along in the same data-parallel all-reduce."""
         named = dict(module.named_parameters())
         order = list(order) if order is not None else list(named)
         assert sorted(order) == sorted(named), 'flat order must list every parameter exactly once'
@@ -19,7 +21,9 @@ class FlatParams:
         sizes = [p.numel() for p in self.params]
         self.n = sum(sizes)
         self.flat = torch.empty(self.n, device=device, dtype=torch.float32)
-        self.grad = torch.zeros(self.n, device=device, dtype=torch.float32)
+        self.grad_ext = torch.zeros(self.n + extra, device=device, dtype=torch.float32)
+        self.grad = self.grad_ext[:self.n]
+        self.extra = self.grad_ext[self.n:]
         offs = [0]
         for s in sizes:
             offs.append(offs[-1] + s)

@@ -192,7 +192,9 @@ def ff_dropout_mask(M, N, p, seed, offset, device):
 class BatchGather:
     """Device minibatch assembly (xtrl_minibatch_gather) into persistent [b_max][n_max] buffers."""
 
-    def __init__(self, cfg, b_max, n_max, device):
+    def __init__(self, cfg, b_max, n_max, device, rs_m=None):
+        """``rs_m``: optional [S+1] output buffer of the minibatch RSNorm mean (the tail of the
+        learner's extended gradient buffer, so the DP all-reduce carries it)."""
         c = cfg
         self.c, self.b_max, self.n_max = c, b_max, n_max
         S, A, B = c.state_dim, c.num_actions, c.num_bins
@@ -202,7 +204,9 @@ class BatchGather:
         self.buf = dict(swr=torch.empty(T * (S + 1), **f32), old_logp=torch.empty(T * (A if c.continuous else 1), **f32),
                         mb_returns=torch.empty(T, **f32), old_values=torch.empty(T * B, **f32),
                         dones=torch.empty(T, **u8), mb_lens=torch.empty(b_max, **i32),
-                        rs_part=torch.empty(64 * (S + 2), **f32), rs_m=torch.empty(S + 1, **f32))
+                        rs_part=torch.empty(64 * (S + 2), **f32),
+                        rs_m=rs_m if rs_m is not None else torch.empty(S + 1, **f32))
+        assert self.buf['rs_m'].numel() == S + 1 and self.buf['rs_m'].is_contiguous()
         if c.continuous:
             self.buf.update(prev_action_f=torch.empty(T * A, **f32), action_f=torch.empty(T * A, **f32))
         else:
