@@ -310,6 +310,16 @@ def test_rollout_matches_oracle(depth, gates, evo):
         tol(learner.fitness(cum, torch.tensor([g for _, g in learner.episode_genes])), fitness, 1e-5, 1e-5)
 
 
+def test_rollout_d256_matches_oracle():
+    """The C3 width (d = 256, 4 x 16 heads; the decode embedding kernel's fused layer-0 pre-norm, the
+    decode GEMM geometries of that shape) reproduces the oracle's batch-1 rollout."""
+    learner, env, oracle = make_learner(depth=2, gates=True, dim=256, episodes=20)
+    traj, lens, _, _ = learner.rollout_device(env, 0, 12)
+    torch.cuda.synchronize()
+    episodes, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes)
+
+
 def test_rollout_continuous_matches_oracle():
     learner, env, oracle = make_learner(cont=True, gates=True)
     traj, lens, _, _ = learner.rollout_device(env, 0, 12)
