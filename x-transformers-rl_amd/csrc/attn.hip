@@ -158,17 +158,6 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
   }
 }
 
-// D_i = rowsum(dO_i * O_i)
-__global__ void k_attn_delta(const AttnArgs a, int rows, int DH) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= rows) return;
-  const int bh = r / a.n, i = r - bh * a.n, b = bh / a.H, h = bh - b * a.H;
-  const int64_t at = b * a.out.sb + h * a.out.sh + (int64_t)i * a.out.si;
-  float s = 0.f;
-  for (int c = 0; c < DH; ++c) s += a.dO[at + c] * a.O[at + c];
-  a.Dout[r] = s;
-}
-
 // ---------------------------------------------------------------------------------------------
 template <int DH>
 __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
@@ -211,10 +200,24 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
         Qs[i][c] = ii < n ? a.Q[ib + (int64_t)ii * isi + c] : 0.f;
         dOs[i][c] = ii < n ? a.dO[ob + (int64_t)ii * osi + c] : 0.f;
       }
+      // D_i = rowsum(dO_i * O_i) of the tile's query rows, computed here (the O row in registers
+      // while the tile stages) in the order of a sequential sum over the head dimension; the
+      // key-tile-0 workgroup, which visits every query tile, stores it for k_attn_bwd_dq
+      float orow[DH];
       if (tid < TQ) {
         const int ii = qt * TQ + tid;
         Ls[tid] = ii < n ? a.LSE[(int64_t)bh * n + ii] : 0.f;
-        Dls[tid] = ii < n ? a.Dl[(int64_t)bh * n + ii] : 0.f;
+#pragma unroll
+        for (int c = 0; c < DH; ++c) orow[c] = ii < n ? a.O[ob + (int64_t)ii * osi + c] : 0.f;
+      }
+      __syncthreads();
+      if (tid < TQ) {
+        const int ii = qt * TQ + tid;
+        float dsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < DH; ++c) dsum += dOs[tid][c] * orow[c];
+        Dls[tid] = dsum;
+        if (j0 == 0 && ii < n) a.Dout[(int64_t)bh * n + ii] = dsum;
       }
       __syncthreads();
       float dsr[4][4];
@@ -427,9 +430,7 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
   a.dQ = dq;
   a.dK = dk;
   a.dV = dv;
-  const int rows = p.b * p.H * p.n;
-  hipLaunchKernelGGL(k_attn_delta, dim3((rows + 255) / 256), dim3(256), 0, s, a, rows, p.dh);
-  XTRL_LAUNCHED("attn_delta");
+  // (D = rowsum(dO * O) is formed inside k_attn_bwd_dkdv, whose key-tile-0 workgroups store it for dq)
   dim3 grid((p.n + TQ - 1) / TQ, p.b * p.H);
   if (p.dh == 16) {
     hipLaunchKernelGGL(k_attn_bwd_dkdv<16>, grid, dim3(256), 0, s, a);
