@@ -245,8 +245,9 @@ __device__ __forceinline__ float dmin_dr(float r, float adv, float lo, float hi)
 // and unbiased variance (sum of squares about zero, in double), critic means and the gradient
 // coefficients of the mean-reduced HL-Gauss critic
 __global__ __launch_bounds__(1024) void k_loss_stats(const XtrlLossDesc D) {
-  __shared__ double sh[16];
+  __shared__ double sh[16][P_N1];
   const int N = D.b * D.n, P = (N + 3) / 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double acc[P_N1];
 #pragma unroll
   for (int k = 0; k < P_N1; ++k) acc[k] = 0.0;
@@ -254,9 +255,21 @@ __global__ __launch_bounds__(1024) void k_loss_stats(const XtrlLossDesc D) {
 #pragma unroll
     for (int k = 0; k < P_N1; ++k) acc[k] += *part_slot(D.tok, (int64_t)p * 4, k);
   }
+  // all nine sums in one pass: butterfly per wave, one barrier, wave totals in a fixed order
 #pragma unroll
-  for (int k = 0; k < P_N1; ++k) acc[k] = block_sum(acc[k], sh);
+  for (int k = 0; k < P_N1; ++k) {
+    const double v = wave_sum_d(acc[k]);
+    if (lane == 0) sh[w][k] = v;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
+  const int nw = (int)(blockDim.x >> 6);
+#pragma unroll
+  for (int k = 0; k < P_N1; ++k) {
+    double t = 0.0;
+    for (int j = 0; j < nw; ++j) t += sh[j][k];
+    acc[k] = t;
+  }
   const double n_mask = acc[P_NMASK], s_adv = acc[P_ADV], n_wm = acc[P_NWM], k_crit = acc[P_KCRIT];
   const float adv_mean = (float)(s_adv / n_mask);
   const double s_var = acc[P_ADV2] - s_adv * (s_adv / n_mask);

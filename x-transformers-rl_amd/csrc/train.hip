@@ -33,13 +33,17 @@ constexpr int EMB_TOK = 32, EMB_U = 8, EMB_MAXS = 32;
 // block: EMB_TOK tokens x all d columns; thread c keeps its project_in / to_state_embed rows in
 // registers (S <= EMB_MAXS) and walks the block's tokens EMB_U at a time, every input of a batch
 // loaded before its first store (the stores may alias the inputs as far as the compiler knows)
+// S_ > 0: the state width at compile time (the lander's 8: no per-element guards in the S loops)
+template <int S_>
 __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
+  constexpr int MS = S_ > 0 ? S_ : EMB_MAXS;
+  const int S = S_ > 0 ? S_ : a.S;
   for (int c = threadIdx.x; c < a.d; c += 256) {
-    float wp[EMB_MAXS], ws[EMB_MAXS];
+    float wp[MS], ws[MS];
 #pragma unroll
-    for (int s = 0; s < EMB_MAXS; ++s) {
-      wp[s] = s < a.S ? a.w_pin[(int64_t)c * a.S + s] : 0.f;
-      ws[s] = s < a.S ? a.w_se[(int64_t)c * a.S + s] : 0.f;
+    for (int s = 0; s < MS; ++s) {
+      wp[s] = s < S ? a.w_pin[(int64_t)c * S + s] : 0.f;
+      ws[s] = s < S ? a.w_se[(int64_t)c * S + s] : 0.f;
     }
     const float bse = a.b_se[c], re = a.reward_embed[c];
     const float bemb = a.continuous ? a.act_emb_b[c] : 0.f;
@@ -48,11 +52,11 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
 #pragma unroll
       for (int u = 0; u < EMB_U; ++u) {
         const int t = min(t0 + u, a.T - 1);
-        const float* st = a.swr + (int64_t)t * (a.S + 1);
+        const float* st = a.swr + (int64_t)t * (S + 1);
         float sp = 0.f, ss = 0.f;
 #pragma unroll
-        for (int s = 0; s < EMB_MAXS; ++s) {
-          if (s < a.S) {
+        for (int s = 0; s < MS; ++s) {
+          if (s < S) {
             const float x = st[s];
             sp += x * wp[s];
             ss += x * ws[s];
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
         }
         pin[u] = sp;
         se[u] = ss + bse;
-        rw[u] = st[a.S];
+        rw[u] = st[S];
         if (a.continuous) {
           const float* w = a.act_emb + (int64_t)c * a.A;
           float p = 0.f, q = 0.f;
@@ -338,8 +342,10 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, i
   const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
   float s = 0.f;
   if (rw) {
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) s += src[(int64_t)r * ld + c] * (rw[(int64_t)r * ld_rw] * rw_scale);
   } else {
+#pragma unroll 8
     for (int r = r0; r < r1; ++r) s += src[(int64_t)r * ld + c];
   }
   part[(int64_t)blockIdx.y * cols + c] = s;
@@ -378,20 +384,22 @@ __global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* par
 // discrete action-embedding gradient: part[chunk][a][c] = sum over rows of the chunk with
 // prev[r] == a of g1[r][c]  +  rows with next[r] == a of g2[r][c]   (A <= EMB_MAXA, registers)
 constexpr int EMB_MAXA = 32;
+template <int MAXA>   // a compile-time bound on A (4 / 8 / 32): the per-row select chain is MAXA long
 __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld1, const int32_t* prev,
                                                          const float* g2, int ld2, const int32_t* next, int rows,
                                                          int d, int A, int chunk_rows, float* part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= d) return;
   const int r0 = blockIdx.y * chunk_rows, r1 = min(rows, r0 + chunk_rows);
-  float acc[EMB_MAXA];
+  float acc[MAXA];
 #pragma unroll
-  for (int a = 0; a < EMB_MAXA; ++a) acc[a] = 0.f;
+  for (int a = 0; a < MAXA; ++a) acc[a] = 0.f;
+#pragma unroll 4
   for (int r = r0; r < r1; ++r) {
     const int p = prev[r], q = next[r];
     const float x = g1[(int64_t)r * ld1 + c], y = g2[(int64_t)r * ld2 + c];
 #pragma unroll
-    for (int a = 0; a < EMB_MAXA; ++a) {
+    for (int a = 0; a < MAXA; ++a) {
       if (a < A) {
         acc[a] += p == a ? x : 0.f;
         acc[a] += q == a ? y : 0.f;
@@ -400,7 +408,7 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld
   }
   float* out = part + (int64_t)blockIdx.y * A * d;
 #pragma unroll
-  for (int a = 0; a < EMB_MAXA; ++a)
+  for (int a = 0; a < MAXA; ++a)
     if (a < A) out[(int64_t)a * d + c] = acc[a];
 }
 
@@ -569,7 +577,7 @@ int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float
 int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* dst, const float* rw = nullptr,
            int ld_rw = 0, float rw_scale = 1.f) {
   if (!dst || cols <= 0) return XTRL_OK;
-  int chunks = std::min(256, std::max(1, rows / 32));
+  int chunks = std::min(1024, std::max(1, rows / 16));   // 16 rows per partial (loads in flight)
   const int chunk_rows = (rows + chunks - 1) / chunks;
   chunks = (rows + chunk_rows - 1) / chunk_rows;
   XTRL_REQUIRE((int64_t)chunks * cols <= c.D->part_floats, "train: partial-sum workspace too small");
@@ -652,7 +660,8 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
                c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
                D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
                D->evolutionary, D->reward_keep};
-  hipLaunchKernelGGL(k_embed, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+  if (D->S == 8) hipLaunchKernelGGL(k_embed<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+  else hipLaunchKernelGGL(k_embed<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
   XTRL_LAUNCHED("train embed");
   // decoder blocks
   for (int li = 0; li < D->L; ++li) {
@@ -824,8 +833,16 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     const int chunk_rows = (T + chunks - 1) / chunks;
     chunks = (T + chunk_rows - 1) / chunk_rows;
     XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");
-    hipLaunchKernelGGL(k_embed_grad_part, dim3(blocks(d, 256), chunks), dim3(256), 0, s, D->dx, d, D->prev_action,
-                       D->dewa + d, 2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
+    const dim3 eg(blocks(d, 256), chunks);
+    if (D->A <= 4)
+      hipLaunchKernelGGL(k_embed_grad_part<4>, eg, dim3(256), 0, s, D->dx, d, D->prev_action, D->dewa + d, 2 * d,
+                         D->next_action, T, d, D->A, chunk_rows, D->part);
+    else if (D->A <= 8)
+      hipLaunchKernelGGL(k_embed_grad_part<8>, eg, dim3(256), 0, s, D->dx, d, D->prev_action, D->dewa + d, 2 * d,
+                         D->next_action, T, d, D->A, chunk_rows, D->part);
+    else
+      hipLaunchKernelGGL(k_embed_grad_part<EMB_MAXA>, eg, dim3(256), 0, s, D->dx, d, D->prev_action, D->dewa + d,
+                         2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
     hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 64)), dim3(64 * CS_WAVES), 0, s, D->part, chunks, D->A * d,
                        c.G(D->act_emb));
     XTRL_LAUNCHED("train embed grad");
