@@ -239,18 +239,22 @@ struct PrepArgs {
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col;   // mix_col < 0: no mix
 };
 
-__global__ __launch_bounds__(256) void k_qkv_prep(const PrepArgs a) {
+// grid (pair blocks, n steps, b episodes), PREP_T threads: token and position come from the grid
+// (no 64-bit division per element); one sincosf per rotated pair
+constexpr int PREP_T = 128;
+__global__ __launch_bounds__(PREP_T) void k_qkv_prep(const PrepArgs a) {
   const int P = 3 * a.I / 2;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)a.T * P) return;
-  const int t = (int)(i / P), col = 2 * (int)(i - (int64_t)t * P);
+  const int pair = blockIdx.x * PREP_T + threadIdx.x;
+  if (pair >= P) return;
+  const int pos = blockIdx.y, t = blockIdx.z * a.n + pos, col = 2 * pair;
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
   const float2 x = *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col);
   float2 y;
   if (seg < 2) {
     if (j < a.rot_dim) {
-      const float f = (float)(t % a.n) * a.inv_freq[j >> 1];
-      const float cs = cosf(f), sn = sinf(f);
+      const float f = (float)pos * a.inv_freq[j >> 1];
+      float sn, cs;
+      sincosf(f, &sn, &cs);
       y.x = x.x * cs + (-x.y) * sn;
       y.y = x.y * cs + x.x * sn;
     } else {
@@ -280,12 +284,12 @@ struct PrepBwdArgs {
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col, first_layer, accumulate;
 };
 
-__global__ __launch_bounds__(256) void k_qkv_prep_bwd(const PrepBwdArgs a) {
+__global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
   const int P = 3 * a.I / 2;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = i < (int64_t)a.T * P;
-  const int64_t ic = valid ? i : 0;
-  const int t = (int)(ic / P), col = 2 * (int)(ic - (int64_t)t * P);
+  const int pair0 = blockIdx.x * PREP_T + threadIdx.x;
+  const bool valid = pair0 < P;
+  const int pair = valid ? pair0 : 0;
+  const int pos = blockIdx.y, t = blockIdx.z * a.n + pos, col = 2 * pair;
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
   float* g = a.dproj + (int64_t)t * a.n_qkv + col;
   float dm = 0.f, m = 0.f;
@@ -293,8 +297,9 @@ __global__ __launch_bounds__(256) void k_qkv_prep_bwd(const PrepBwdArgs a) {
     float2 gv = *reinterpret_cast<float2*>(g);
     if (seg < 2) {
       if (j < a.rot_dim) {
-        const float f = (float)(t % a.n) * a.inv_freq[j >> 1];
-        const float cs = cosf(f), sn = sinf(f);
+        const float f = (float)pos * a.inv_freq[j >> 1];
+        float sn, cs;
+        sincosf(f, &sn, &cs);
         const float g0 = gv.x, g1 = gv.y;
         gv.x = g0 * cs + g1 * sn;
         gv.y = g1 * cs + (-g0) * sn;
@@ -673,7 +678,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
     const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
     PrepArgs pa{Ly.proj, D->layers[0].proj, Ly.qkv, D->inv_freq, T, D->n, D->H, D->dh, I, Ly.n_qkv,
                 D->layers[0].n_qkv, D->rot_dim, mix_col};
-    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks((int64_t)T * 3 * I / 2, 256)), dim3(256), 0, s, pa);
+    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pa);
     XTRL_LAUNCHED("train qkv_prep");
     const AttnProblem ap = attn_problem(c, Ly, li);
     if ((rc = attn_fwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse,
@@ -806,7 +811,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     PrepBwdArgs pb{D->dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
                    Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
                    (li == 0 ? any_mix : deeper_mix) ? 1 : 0};
-    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks((int64_t)T * 3 * I / 2, 256)), dim3(256), 0, s, pb);
+    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
     if ((rc = F.fork())) return rc;
