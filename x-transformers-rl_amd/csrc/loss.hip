@@ -9,7 +9,7 @@
 //   compute_done_loss    :406-411   (sigmoid + F.binary_cross_entropy, log clamped at -100)
 //   combination          :939-978   ((w_a actor + w_c critic)[mask].mean() + (wm.mean() + done.mean()) w_ar)
 //
-// k_loss_tokens (one wave per token, lanes over the value bins; each block of 4 tokens leaves the
+// k_loss_tokens (one wave per token, lanes over the value bins; each block of 16 tokens leaves the
 // partial sums of the masked statistics in its tokens' spare slots) -> k_loss_stats (one workgroup:
 // fixed-order sum of the block partials -> advantage mean / unbiased variance, critic means,
 // gradient coefficients) -> k_loss_actor (thread per token: actor / critic terms, block partials)
@@ -141,11 +141,13 @@ __device__ __forceinline__ bool critic_zeroed(float v, float ret, float vold, fl
   return ((ret < v) && (v < lo)) || ((hi < v) && (v < ret));
 }
 
-__global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
-  __shared__ double shp[4][P_N1];
+// LT_W waves (tokens) per block: the block partials number N / LT_W for k_loss_stats
+constexpr int LT_W = 16;
+__global__ __launch_bounds__(64 * LT_W) void k_loss_tokens(const XtrlLossDesc D) {
+  __shared__ double shp[LT_W][P_N1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int N = D.b * D.n;
-  const int tk0 = blockIdx.x * 4 + w;
+  const int tk0 = blockIdx.x * LT_W + w;
   const bool valid = tk0 < N;   // (waves past N evaluate the last token and store nothing)
   const int tk = valid ? tk0 : N - 1;
   const int bi = tk / D.n, ti = tk - bi * D.n;
@@ -209,7 +211,10 @@ __global__ __launch_bounds__(256) void k_loss_tokens(const XtrlLossDesc D) {
   __syncthreads();
   if (threadIdx.x < P_N1) {
     const int k = threadIdx.x;
-    *part_slot(D.tok, (int64_t)blockIdx.x * 4, k) = ((shp[0][k] + shp[1][k]) + shp[2][k]) + shp[3][k];
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < LT_W; ++j) v += shp[j][k];
+    *part_slot(D.tok, (int64_t)blockIdx.x * LT_W, k) = v;
   }
 }
 
@@ -246,14 +251,14 @@ __device__ __forceinline__ float dmin_dr(float r, float adv, float lo, float hi)
 // coefficients of the mean-reduced HL-Gauss critic
 __global__ __launch_bounds__(1024) void k_loss_stats(const XtrlLossDesc D) {
   __shared__ double sh[16][P_N1];
-  const int N = D.b * D.n, P = (N + 3) / 4;
+  const int N = D.b * D.n, P = (N + LT_W - 1) / LT_W;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double acc[P_N1];
 #pragma unroll
   for (int k = 0; k < P_N1; ++k) acc[k] = 0.0;
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
 #pragma unroll
-    for (int k = 0; k < P_N1; ++k) acc[k] += *part_slot(D.tok, (int64_t)p * 4, k);
+    for (int k = 0; k < P_N1; ++k) acc[k] += *part_slot(D.tok, (int64_t)p * LT_W, k);
   }
   // all nine sums in one pass: butterfly per wave, one barrier, wave totals in a fixed order
 #pragma unroll
@@ -529,7 +534,7 @@ int check(const XtrlLossDesc* D) {
 int loss_fwd(const XtrlLossDesc* D, hipStream_t s) {
   if (int rc = check(D)) return rc;
   const int N = D->b * D->n;
-  hipLaunchKernelGGL(k_loss_tokens, dim3((N + 3) / 4), dim3(256), 0, s, *D);
+  hipLaunchKernelGGL(k_loss_tokens, dim3((N + LT_W - 1) / LT_W), dim3(64 * LT_W), 0, s, *D);
   XTRL_LAUNCHED("loss_tokens");
   hipLaunchKernelGGL(k_loss_stats, dim3(1), dim3(1024), 0, s, *D);
   XTRL_LAUNCHED("loss_stats");

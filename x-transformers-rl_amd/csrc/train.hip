@@ -834,7 +834,9 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = colsum(c, D->dx, d, T, d, c.G(D->act_emb_b)))) return rc;
     if ((rc = colsum(c, D->dewa + d, 2 * d, T, d, c.G(D->act_emb_b)))) return rc;
   } else {
-    int chunks = std::min(512, std::max(1, T / 32));
+    // 16-row partials (loads in flight), as many as the partial workspace holds
+    int chunks = std::min<int64_t>(std::min(1024, std::max(1, T / 16)),
+                                   std::max<int64_t>(1, D->part_floats / ((int64_t)D->A * d)));
     const int chunk_rows = (T + chunks - 1) / chunks;
     chunks = (T + chunk_rows - 1) / chunk_rows;
     XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "train: partial-sum workspace too small");

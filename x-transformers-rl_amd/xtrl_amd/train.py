@@ -78,8 +78,7 @@ class FusedTrainStep:
                         dx=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
-        part = max(256 * max(ff, 4 * d, B, max_qkv), (T // 64 + 1) * d, 512 * max(A, 1) * d, b_max * d,
-                   1024 * d)
+        part = max(256 * max(ff, 4 * d, B, max_qkv), (T // 64 + 1) * d, 1024 * max(A, 1) * d, b_max * d)
         self.buf['part'] = E(part)
         self.tok = torch.empty(b_max, n_max, L.LOSS_TOK, **f32)
         self.stats = torch.zeros(L.LOSS_STATS, **f32)
