@@ -1,0 +1,14 @@
+import sys
+sys.path[:0] = ['.', 'x-transformers-rl_amd']
+import torch
+from xtrl_amd import ops
+def timeit(fn, iters=50):
+    fn(); torch.cuda.synchronize()
+    s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+    s.record()
+    for _ in range(iters): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+for tag, M, N, K in [('ff2', 1024, 256, 1024), ('ff1', 1024, 1024, 256), ('qkv', 1024, 324, 256), ('head1', 1024, 1024, 512), ('a2', 1024, 4, 512), ('c2', 1024, 100, 512)]:
+    A = torch.randn(M, K, device='cuda'); B = torch.randn(N, K, device='cuda'); C = torch.empty(M, N, device='cuda')
+    print(tag, f'{timeit(lambda: ops.gemm_ex(A, B, 0, 0, M, N, K, C)):.1f}')

@@ -221,15 +221,24 @@ __device__ __forceinline__ void sim_step_env(const XtrlDecodeDesc& D, int e, int
   D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
   D.prev_reward[e] = reward;
   D.cum_reward[e] += (double)reward;
-  D.lens[e] = t + 1;
-  for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
+  D.lens[e] = t + 1;   // (the next state was written by the env's lanes in k_sample)
   if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
 }
 
+// SAMPLE_L lanes per env (one wave holds whole envs): lane 0 samples the action and steps the Sim;
+// the next state's S normals are spread over the env's lanes (they do not depend on the action)
+constexpr int SAMPLE_L = 8;
 __global__ void k_sample(const XtrlDecodeDesc D, int t) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D.E || !D.alive[e]) return;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gid / SAMPLE_L, sub = gid % SAMPLE_L;
+  if (e >= D.E || !D.alive[e]) return;   // (every lane of the env reads alive before lane 0 clears it)
   const XtrlRngState R = *D.rng;
+  if (D.sim_mode >= 0) {
+    const uint32_t ep = (uint32_t)D.episode_of_slot[e];
+    for (int i = sub; i < D.S; i += SAMPLE_L)
+      D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
+  }
+  if (sub != 0) return;
   const uint32_t slot = R.slot_offset + e;
   const int A = D.A;
   const float* lg = D.logits + (int64_t)e * (D.continuous ? 2 * A : A);
@@ -391,7 +400,7 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
     g.row_mask = D->alive;
     if ((rc = gemm_run(g, 0, 0, EPI_NONE, s))) return rc;
   }
-  hipLaunchKernelGGL(k_sample, dim3((E + 255) / 256), dim3(256), 0, s, *D, t);
+  hipLaunchKernelGGL(k_sample, dim3((E * SAMPLE_L + 255) / 256), dim3(256), 0, s, *D, t);
   XTRL_LAUNCHED("sample");
   return XTRL_OK;
 }
