@@ -9,6 +9,11 @@ def timeit(fn, iters=50):
     for _ in range(iters): fn()
     e.record(); torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1e3
-for tag, M, N, K in [('ff2', 1024, 256, 1024), ('ff1', 1024, 1024, 256), ('qkv', 1024, 324, 256), ('head1', 1024, 1024, 512), ('a2', 1024, 4, 512), ('c2', 1024, 100, 512)]:
+SHAPES = [('ff2', 1024, 256, 1024), ('ff1', 1024, 1024, 256), ('qkv', 1024, 324, 256), ('head1', 1024, 1024, 512),
+          ('a2', 1024, 4, 512), ('c2', 1024, 100, 512)]
+if len(sys.argv) > 1 and sys.argv[1] == 'learn':   # learn-step forward shapes (16384 tokens)
+    SHAPES = [('out', 16384, 256, 64), ('qkv', 16384, 324, 256), ('pred2', 16384, 18, 256), ('vals', 16384, 100, 512),
+              ('a2', 16384, 4, 512), ('pd', 16384, 257, 512)]
+for tag, M, N, K in SHAPES:
     A = torch.randn(M, K, device='cuda'); B = torch.randn(N, K, device='cuda'); C = torch.empty(M, N, device='cuda')
     print(tag, f'{timeit(lambda: ops.gemm_ex(A, B, 0, 0, M, N, K, C)):.1f}')

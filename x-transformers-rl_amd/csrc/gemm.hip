@@ -1216,8 +1216,11 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   }
   // (decode-sized M measured on MI355X, graph-timed: M=1024 N=1024 K=256 64x64 11.6 us vs
   //  32x32/WK4 17.4; N=260 K=256 64x32/WK2 7.7 vs 8.2; N=256 K=1024 32x32/WK4 13.7 vs 64x64 24.7)
+  // (learn shapes, tools/geom_probe.py learn: N <= 32 outputs over 16384 rows 64x32/WK2 9.8-10.8 us vs
+  //  64x64 13.3 / 32x32-WK4 14.9; K = 64 64x64 12.3 vs 128x128 14.0)
   if (!vec) launch<2, 2, 1, 1, 1, TA, TB, EPI, LN, RES, false>(a, s);
-  else if (tiles128 >= 192) {
+  else if (!TA && a.N <= 32 && a.M >= 4096) launch<2, 1, 2, 1, 1, TA, TB, EPI, LN, RES, true>(a, s);
+  else if (tiles128 >= 192 && a.K > 64) {
     bool done = false;
     if constexpr (EPI != EPI_DGATE && !LN) {   // (the gate epilogue needs more than 256 registers)
       if (use_x6() && ws_ok(a, TA, LN)) {
