@@ -358,7 +358,7 @@ typedef struct XtrlLossDesc {
   float* d_raw_actions; float* d_values; float* d_pred_raw; float* d_done_logit;
 } XtrlLossDesc;
 
-#define XTRL_LOSS_TOK 28       /* 10 per-token terms + 18 floats: per-block partial sums (doubles) */
+#define XTRL_LOSS_TOK 30       /* 11 per-token terms (+1 pad) + 18 floats: per-block partial sums (doubles) */
 #define XTRL_LOSS_STATS 32
 /* stats[] slots */
 #define XTRL_LS_LOSS 0         /* total loss (xtrl.py:975-978) */

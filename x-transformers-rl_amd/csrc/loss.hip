@@ -25,7 +25,7 @@ namespace {
 constexpr float F32_EPS = 1.1920928955078125e-07f;
 constexpr int NT = XTRL_LOSS_TOK;
 enum Tok { T_ADV = 0, T_V = 1, T_VOLD = 2, T_CEU = 3, T_CEC = 4, T_LP = 5, T_ENT = 6, T_WM = 7, T_BCE = 8, T_ACT = 9,
-           T_SPARE = 10 };
+           T_LSE = 10, T_SPARE = 12 };   // T_LSE: log-sum-exp of the value logits (the backward reuses it)
 // partial sums of a block: doubles in the spare slots of the block's first token
 __device__ __forceinline__ double* part_slot(float* tok, int64_t first, int k) {
   return reinterpret_cast<double*>(tok + first * NT + T_SPARE + 2 * k);
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(64 * LT_W) void k_loss_tokens(const XtrlLossDesc D)
     if (valid) {
       tok[T_ADV] = adv;
       tok[T_V] = rn.dot_centers;
+      tok[T_LSE] = rn.lse;
       tok[T_VOLD] = ro.dot_centers;
       tok[T_CEU] = ceu;
       tok[T_CEC] = cec;
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
       du = a < b ? w : (a > b ? 0.f : 0.5f * w);
       dc = b < a ? w : (b > a ? 0.f : 0.5f * w);
     }
-    const RowStats rn = row_stats(x, D.centers, D.B, lane);
+    const float lse = tok[T_LSE];   // the forward's softmax statistics of this token's value logits
     const float inv = 1.0f / (1.41421356237309505f * D.sigma);
     const float yu = fminf(fmaxf(D.returns[tk], D.lo), D.hi);
     const float yc = fminf(fmaxf(fminf(fmaxf(D.returns[tk], -D.value_clip), D.value_clip), D.lo), D.hi);
@@ -413,11 +414,11 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
     su = wave_sum(su);
     sc = wave_sum(sc);
     if (lane < D.B) {
-      const float p = expf(x[lane] - rn.lse);
+      const float p = expf(x[lane] - lse);
       D.d_values[(int64_t)tk * D.B + lane] = du * (p * su - tu.t0) + dc * (p * sc - tc.t0);
     }
     if (lane + 64 < D.B) {
-      const float p = expf(x[lane + 64] - rn.lse);
+      const float p = expf(x[lane + 64] - lse);
       D.d_values[(int64_t)tk * D.B + lane + 64] = du * (p * su - tu.t1) + dc * (p * sc - tc.t1);
     }
   }

@@ -23,7 +23,7 @@ ACT_NONE, ACT_GELU, ACT_SILU, ACT_RELU = 0, 1, 2, 3
 # stats[] slots of the fused loss (XTRL_LS_*)
 LS = dict(loss=0, actor=1, critic=2, autoreg=3, done=4, adv_mean=5, adv_den=6, L=7, Lc=8, nmask=9, nwm=10,
           kcrit=11, dL=12, dLc=13)
-LOSS_TOK, LOSS_STATS = 28, 32
+LOSS_TOK, LOSS_STATS = 30, 32
 
 
 class DecodeLayer(C.Structure):
