@@ -357,33 +357,36 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, i
   part[(int64_t)blockIdx.y * cols + c] = s;
 }
 
-// dst[c] += sum_k part[k][c]: 64 columns per block; wave w sums chunks w, w + 4, ... with four
-// interleaved accumulators; fixed combination order (deterministic)
-// dst[c] += sum over chunks of part[chunk][c]: 16 waves per 64 columns, wave w sums chunks w,
-// w + 16, ... in four chains (loads in flight), then a fixed-order sum of the 16 wave totals
-constexpr int CS_WAVES = 16;
+// dst[c] += sum over chunks of part[chunk][c]: CS_COLS columns per block of CS_WAVES waves; each
+// lane owns (column lane % CS_COLS, chunk group) and sums its chunks in four chains (loads in flight),
+// then the CS_G group totals of a column are added in a fixed order (deterministic)
+constexpr int CS_WAVES = 16, CS_COLS = 16, CS_G = 64 * CS_WAVES / CS_COLS;
 __global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
-  __shared__ float red[CS_WAVES][64];
+  __shared__ float red[CS_G][CS_COLS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int cl = lane % CS_COLS, g = w * (64 / CS_COLS) + lane / CS_COLS;
+  const int c = blockIdx.x * CS_COLS + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < cols) {
-    int k = w;
-    for (; k + 3 * CS_WAVES < chunks; k += 4 * CS_WAVES) {
+    int k = g;
+    for (; k + 3 * CS_G < chunks; k += 4 * CS_G) {
       s0 += part[(int64_t)k * cols + c];
-      s1 += part[(int64_t)(k + CS_WAVES) * cols + c];
-      s2 += part[(int64_t)(k + 2 * CS_WAVES) * cols + c];
-      s3 += part[(int64_t)(k + 3 * CS_WAVES) * cols + c];
+      s1 += part[(int64_t)(k + CS_G) * cols + c];
+      s2 += part[(int64_t)(k + 2 * CS_G) * cols + c];
+      s3 += part[(int64_t)(k + 3 * CS_G) * cols + c];
     }
-    for (; k < chunks; k += CS_WAVES) s0 += part[(int64_t)k * cols + c];
+    for (; k < chunks; k += CS_G) s0 += part[(int64_t)k * cols + c];
   }
-  red[w][lane] = (s0 + s1) + (s2 + s3);
+  red[g][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (w == 0 && c < cols) {
-    float v = 0.f;
-#pragma unroll
-    for (int j = 0; j < CS_WAVES; ++j) v += red[j][lane];
-    dst[c] += v;
+  if (threadIdx.x < CS_COLS) {
+    const int cc = blockIdx.x * CS_COLS + threadIdx.x;
+    if (cc < cols) {
+      float v = 0.f;
+#pragma unroll 8
+      for (int j2 = 0; j2 < CS_G; ++j2) v += red[j2][threadIdx.x];
+      dst[cc] += v;
+    }
   }
 }
 
@@ -589,7 +592,7 @@ int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* ds
   XTRL_REQUIRE((int64_t)chunks * cols <= c.D->part_floats, "train: partial-sum workspace too small");
   hipLaunchKernelGGL(k_colsum_part, dim3(blocks(cols, 256), chunks), dim3(256), 0, c.s, src, ld, rows, cols,
                      chunk_rows, rw, ld_rw, rw_scale, c.D->part);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, 64)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, chunks, cols, dst);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(cols, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, chunks, cols, dst);
   XTRL_LAUNCHED("train colsum");
   return XTRL_OK;
 }
@@ -610,7 +613,7 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
   else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
   else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
   else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, 64)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
   XTRL_LAUNCHED("train ln_bwd");
   return XTRL_OK;
 }
@@ -851,7 +854,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     else
       hipLaunchKernelGGL(k_embed_grad_part<EMB_MAXA>, eg, dim3(256), 0, s, D->dx, d, D->prev_action, D->dewa + d,
                          2 * d, D->next_action, T, d, D->A, chunk_rows, D->part);
-    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, 64)), dim3(64 * CS_WAVES), 0, s, D->part, chunks, D->A * d,
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, CS_COLS)), dim3(64 * CS_WAVES), 0, s, D->part, chunks, D->A * d,
                        c.G(D->act_emb));
     XTRL_LAUNCHED("train embed grad");
   }
