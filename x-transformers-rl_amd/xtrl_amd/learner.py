@@ -286,6 +286,10 @@ class Agent(nn.Module):
         if fused:
             returns = returns.contiguous()
             gather = self.batch_gather(traj['rewards'].shape[1])
+        # one stats row per minibatch, written in place by the fused loss (no per-minibatch clone)
+        n_mb = self.epochs * ((N + self.batch_size - 1) // self.batch_size)
+        stats_rows = torch.zeros(n_mb, L.LOSS_STATS, device=dev) if fused else None
+        logs0 = len(self.logs)
         for epoch in range(self.epochs):
             for mbi, k in enumerate(range(0, N, self.batch_size)):
                 idx = perms[epoch, k:k + self.batch_size]
@@ -329,7 +333,7 @@ class Agent(nn.Module):
                                    sigma=float(model.hl_sigma))
                 self.flat.zero_grad()
                 if self.fused_learn:
-                    stats = step.loss(K)
+                    stats = step.loss(K, stats_rows[len(self.logs) - logs0])
                     step.backward()
                     loss = stats[L.LS['loss']]
                 else:

@@ -147,7 +147,7 @@ class FusedTrainStep:
         return (bf['raw'][:T].view(b, n, -1), bf['values'][:T].view(b, n, -1), bf['pred'][:T].view(b, n, -1),
                 bf['done'][:T].view(b, n))
 
-    def loss(self, K):
+    def loss(self, K, stats=None):
         """Fused loss forward + backward (upstream gradient 1) into the d_* buffers.
         Returns the stats tensor (XTRL_LS_* slots)."""
         c, D = self.cfg, self.D
@@ -156,7 +156,12 @@ class FusedTrainStep:
         bf = self.buf
         S1 = c.state_dim + 1
         A = c.num_actions
-        self.stats.zero_()
+        # ``stats``: a caller-owned row (every XTRL_LS_* slot is written by the loss kernels), else
+        # the step's own buffer, cloned on return since the next minibatch reuses it
+        own = stats is None
+        if own:
+            self.stats.zero_()
+            stats = self.stats
         d = L.LossDesc(b=b, n=n, A=A, B=c.num_bins, S1=S1, continuous=int(K.continuous), squash=int(K.squash),
                        hl_reduction_mean=int(K.hl_mean), eps_clip=K.eps_clip, value_clip=K.value_clip,
                        entropy_weight=K.entropy_weight, w_actor=K.w_actor, w_critic=K.w_critic,
@@ -164,7 +169,7 @@ class FusedTrainStep:
         fields = dict(raw_actions=bf['raw'], values=bf['values'], pred_raw=bf['pred'], done_logit=bf['done'],
                       actions=None if K.continuous else K.actions, actions_f=K.actions if K.continuous else None,
                       old_logp=K.old_logp, returns=K.returns, old_values=K.old_values, dones=K.dones, lens=K.lens,
-                      real=K.real, support=K.support, centers=K.centers, tok=self.tok, stats=self.stats,
+                      real=K.real, support=K.support, centers=K.centers, tok=self.tok, stats=stats,
                       d_raw_actions=bf['d_raw'], d_values=bf['d_values'], d_pred_raw=bf['d_pred'],
                       d_done_logit=bf['d_done'])
         for name, t in fields.items():
@@ -175,7 +180,7 @@ class FusedTrainStep:
         L.check(lib.xtrl_loss_fwd(C.byref(d), L.stream()), 'loss_fwd')
         L.check(lib.xtrl_loss_bwd(C.byref(d), 1.0, L.stream()), 'loss_bwd')
         del T
-        return self.stats.clone()   # the stats buffer is reused by the next minibatch
+        return stats.clone() if own else stats
 
     def backward(self):
         L.check(L.lib().xtrl_train_backward(C.byref(self.D), L.stream()), 'train_backward')
