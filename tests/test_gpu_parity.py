@@ -27,7 +27,10 @@ def tol(a, b, rtol=1e-4, atol=1e-5):
 
 
 @pytest.mark.parametrize('M,N,K', [(1, 5, 8), (37, 100, 96), (64, 64, 64), (130, 257, 48), (1024, 1024, 256),
-                                   (515, 4, 512)])
+                                   (515, 4, 512),
+                                   # learn-step geometry rules: narrow outputs over many rows (64x32/WK2),
+                                   # K = 64 over 16384 rows (64x64 instead of 128x128)
+                                   (4100, 18, 256), (4096, 4, 512), (16384, 256, 64)])
 @pytest.mark.parametrize('mode', ['plain', 'ln_gelu', 'silu', 'residual', 'ln'])
 def test_gemm_f32(M, N, K, mode):
     from xtrl_amd import _lib as L, ops
