@@ -27,9 +27,11 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 4
+#define XTRL_ABI_VERSION 5
 
 int xtrl_abi_version(void);
+/* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
+int64_t xtrl_struct_size(const char* name);
 const char* xtrl_last_error(void);
 
 /* ---------------------------------------------------------------------------------------------
@@ -124,6 +126,8 @@ typedef struct XtrlDecodeDesc {
   int32_t* lens;           /* [E] episode length so far */
   double* cum_reward;      /* [E] cumulative reward (fitness, xtrl.py:1310, 1345-1346) */
   const int32_t* episode_of_slot;  /* [E] episode index keying the Sim stream */
+  const int32_t* slot_of_row;      /* [E] global (episode, gene) pair index keying the sampling stream, or
+                                      NULL: rng->slot_offset + row (contiguous shards) */
   const XtrlRngState* rng;
   /* trajectory (device), row e = one episode, padded with zeros past its length */
   float* traj_states;      /* [E][Tmax][S] */
@@ -178,12 +182,15 @@ int xtrl_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, 
  * Training attention (x-transformers Attend with causal + key-padding mask, post-softmax dropout)
  *   q, k, v: [b][H][n][dh]; lens[b] valid keys per row; out o [b][H][n][dh]; lse [b][H][n]
  * ------------------------------------------------------------------------------------------- */
+/* dropout keep(b, h, i, j) = word (i & 3) of philox(seed; i >> 2, j, offset + b * H + h,
+ * (6 << 24) | sub) >= p * 2^32; sub (< 2^24) names the decoder layer */
 int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o, float* lse,
                   int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset,
-                  void* stream);
+                  uint32_t sub, void* stream);
 int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
                   const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b,
-                  int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset, void* stream);
+                  int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset, uint32_t sub,
+                  void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Learn-step forward / backward of WorldModelActorCritic on one minibatch, hand-scheduled (no
@@ -194,8 +201,13 @@ int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t*
  *   (accumulated: the caller zeroes `grad`).  Offsets are in floats, -1 = absent.
  * Forward writes raw / values / pred / done (the inputs of xtrl_loss_fwd) and saves what the
  * backward needs; backward consumes d_raw / d_values / d_pred / d_done (xtrl_loss_bwd).
- * Feed-forward dropout keep(m, n) = philox(seed; n, m >> 2, ff_offset + layer, (7 << 24)) word
- * (m & 3) >= p * 2^32; attention dropout as xtrl_attn_fwd with offset attn_offset + layer * 65536.
+ * Dropout streams (Philox counter (c0, c1, c2, c3), c3 = field << 24 | sub):
+ *   feed-forward  keep(m, n) = word (m & 3) of philox(seed; n, m >> 2, ff_offset, (7 << 24) | 2 layer)
+ *                 >= p * 2^32; when 256 p is an integer, byte (m & 3) of word ((m >> 3) & 3) of
+ *                 philox(seed; n, 2 (m >> 5) + ((m >> 2) & 1), ff_offset, (7 << 24) | (2 layer + 1)) >= 256 p;
+ *   attention     as xtrl_attn_fwd with offset attn_offset and sub = layer.
+ * The caller gives every minibatch its own ff_offset and a disjoint [attn_offset, attn_offset + b H)
+ * range (xtrl_amd/learner.py: minibatch ordinal and ordinal * batch_size * H).
  * ------------------------------------------------------------------------------------------- */
 typedef struct XtrlTrainLayer {
   int64_t ln_attn, w_proj, b_proj, w_out, ln_ff, w_ff1, b_ff1, w_ff2, b_ff2;
@@ -285,7 +297,11 @@ typedef struct XtrlTrainDesc {
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
 int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream);
 /* the feed-forward dropout keep mask of layer `layer` as uint8 [M][N] (tests / reference mode) */
-int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, void* stream);
+int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, uint32_t layer,
+                         void* stream);
+/* floats of XtrlTrainDesc.part (the partial-sum workspace) a learn step of T = b * n tokens needs;
+ * host-only, no device call */
+int64_t xtrl_train_part_floats(int T, int b, int d, int A);
 
 /* ---------------------------------------------------------------------------------------------
  * Minibatch assembly for the learn step (Agent.learn data prep, xtrl.py:816-924): gathers the

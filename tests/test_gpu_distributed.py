@@ -1,9 +1,20 @@
-"""Two data-parallel ranks on one GPU (gloo carries the collectives; the 8-GPU bench uses RCCL):
-both ranks run two full learning updates of the device Learner on their halves of the (episode,
-gene) pairs.  After every optimiser step the flat gradient was all-reduced, so the weights, the
-EMA copy, the RSNorm statistics and the gene pool must be bitwise identical on the two ranks, and
-the rollouts must reproduce a single-process rollout of the same pairs (world-size-invariant
-sampling streams)."""
+"""Two data-parallel ranks on one GPU (gloo carries the collectives; the 8-GPU bench uses RCCL).
+
+* lockstep: both ranks run two full learning updates of the device Learner on their halves of
+  the (episode, gene) pairs.  After every optimiser step the flat gradient was all-reduced, so the
+  weights, the EMA copy, the RSNorm statistics and the gene pool must be bitwise identical on the
+  two ranks, and the rollouts must reproduce a single-process rollout of the same pairs
+  (world-size-invariant sampling streams).
+* DP gradient: the all-reduced gradient of every optimiser step of one update equals the mean of
+  the gradients a single process computes on each rank's minibatch separately (the DDP semantics
+  of the reference, xtrl.py:885/981: every rank normalises advantages and averages its loss over
+  its own minibatch, DDP averages the rank gradients).  The learning rate is 0 so every minibatch
+  sees the same weights on both sides; the gradient buffer's tail (the minibatch RSNorm mean,
+  xtrl.py:601) is compared too.
+* gene-sharded EPO (C5 partition): with ``shard_by_gene`` rank r rolls out every
+  episode of genes g = r (mod world); the rank rollouts reassembled in pair order equal the
+  single-process rollout, the fitness sums over ranks equal the single-process fitness, and the
+  ranks stay in lockstep through evolve_."""
 import os
 import socket
 import sys
@@ -24,20 +35,26 @@ def _free_port():
     return port
 
 
-def _make(world):
+def _make(world, shard_by_gene=False, genes=3, episodes=4):
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(3)
     wm = dict(attn_dim_head=16, heads=4, depth=2, attn_gate_values=True, add_value_residual=True,
               learned_value_residual_mix=True)
-    learner = Learner(8, 4, (-2., 2.), world_model=wm, max_timesteps=20, batch_size=2, num_episodes_per_update=4,
-                      evolutionary=True, evolve_every=1, evolve_after_step=0,
-                      latent_gene_pool=dict(dim=8, num_genes_per_island=3, num_selected=2, tournament_size=2),
+    learner = Learner(8, 4, (-2., 2.), world_model=wm, max_timesteps=20, batch_size=2,
+                      num_episodes_per_update=episodes, evolutionary=True, evolve_every=1, evolve_after_step=0,
+                      latent_gene_pool=dict(dim=8, num_genes_per_island=genes, num_selected=2, tournament_size=2),
                       agent_kwargs=dict(dropout=0.1, seed=7, hidden_dim=48, save_path='/tmp/xtrl_dp_test.pt'),
-                      use_graph=False)
+                      use_graph=False, shard_by_gene=shard_by_gene)
     return learner, SynthVecSim(8, 4, 'lander', hazard_log2=3)
 
 
-def _worker(rank, world, port, out_dir):
+def _grad_probe(agent, out):
+    def probe(epoch, mbi, idx, loss, stats):
+        out.append(agent.flat.grad_ext.detach().cpu().clone())
+    return probe
+
+
+def _worker(rank, world, port, out_dir, mode):
     sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
@@ -45,31 +62,96 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        learner, env = _make(world)
-        traj, lens, _, _ = learner.rollout_device(env, 0, 20)
-        first = dict(actions=traj['actions'].cpu().clone(), lens=lens.cpu().clone())
-        learner(env, 2)
+        gene_mode = mode == 'genes'
+        learner, env = _make(world, shard_by_gene=gene_mode, genes=4 if gene_mode else 3)
         a = learner.agent
+        traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+        first = dict(actions=traj['actions'].cpu().clone(), lens=lens.cpu().clone(), fit=learner.fitness(cum, genes))
+        grads = []
+        if mode == 'grad':
+            a.opt_cfg['lr'] = 0.     # weights fixed: every minibatch gradient at the same point
+            a.learn(traj, lens, genes, first['fit'], update=0, probe=_grad_probe(a, grads))
+        else:
+            learner(env, 2)
         torch.save(dict(flat=a.flat.flat.cpu(), ema=a.ema_flat.cpu(), rs_mean=a.rs_mean.cpu(), rs_var=a.rs_var.cpu(),
-                        genes=a.gene_pool.genes.clone(), first=first, pairs=learner.episode_genes_for_process),
+                        genes=a.gene_pool.genes.clone(), first=first, pairs=learner.episode_genes_for_process,
+                        slots=learner.pair_slots, grads=grads),
                    os.path.join(out_dir, f'rank{rank}.pt'))
     finally:
         dist.destroy_process_group()
 
 
+def _run(tmp_path, mode, world=2):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, start_method='spawn')
+    sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
+    return [torch.load(tmp_path / f'rank{i}.pt', weights_only=True) for i in range(world)]
+
+
 @pytest.mark.gpu
 def test_two_ranks_one_gpu_stay_in_lockstep(tmp_path):
-    world, port = 2, _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method='spawn')
-    r = [torch.load(tmp_path / f'rank{i}.pt', weights_only=True) for i in range(world)]
+    r = _run(tmp_path, 'lockstep')
     for k in ('flat', 'ema', 'rs_mean', 'rs_var', 'genes'):
         assert torch.equal(r[0][k], r[1][k]), k
     assert torch.isfinite(r[0]['flat']).all()
     # the concatenated rank rollouts == a single-process rollout of all pairs
-    sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
     learner, env = _make(1)
     traj, lens, _, _ = learner.rollout_device(env, 0, 20)
     n0 = len(r[0]['pairs'])
     assert torch.equal(torch.cat([r[0]['first']['lens'], r[1]['first']['lens']]), lens.cpu())
     assert torch.equal(torch.cat([r[0]['first']['actions'], r[1]['first']['actions']]), traj['actions'].cpu())
     assert n0 * 2 == lens.numel()
+
+
+@pytest.mark.gpu
+def test_dp_gradient_equals_mean_of_rank_minibatch_gradients(tmp_path):
+    r = _run(tmp_path, 'grad')
+    assert len(r[0]['grads']) == len(r[1]['grads']) > 0
+    for g0, g1 in zip(r[0]['grads'], r[1]['grads']):
+        assert torch.equal(g0, g1)          # every rank holds the same all-reduced gradient
+    # single process: each rank's half of the pairs learned on its own, from the same weights
+    learner, env = _make(1)
+    a = learner.agent
+    a.opt_cfg['lr'] = 0.
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    fit = learner.fitness(cum, genes)
+    n0 = len(r[0]['pairs'])
+    flat0 = a.flat.flat.clone()
+    rs0 = (a.rs_mean.clone(), a.rs_var.clone(), a.rs_step)
+    per_rank = []
+    for rank in range(2):
+        a.rs_mean, a.rs_var, a.rs_step = rs0[0].clone(), rs0[1].clone(), rs0[2]
+        a.step = 0
+        rows = slice(rank * n0, (rank + 1) * n0)
+        sub = {k: (v[rows].contiguous() if v is not None else None) for k, v in traj.items()}
+        grads = []
+        a.learn(sub, lens[rows].contiguous(), genes[rows].contiguous(), fit, update=0, probe=_grad_probe(a, grads))
+        assert torch.equal(a.flat.flat, flat0)     # lr 0: the weights did not move
+        per_rank.append(grads)
+    steps = len(r[0]['grads'])
+    assert len(per_rank[0]) == len(per_rank[1]) == steps
+    for i in range(steps):
+        want = (per_rank[0][i] + per_rank[1][i]) / 2
+        got = r[0]['grads'][i]
+        scale = float(want.abs().max())
+        err = float((got - want).abs().max())
+        assert err <= 1e-6 * scale + 1e-9, (i, err, scale)
+
+
+@pytest.mark.gpu
+def test_gene_sharded_epo_partition(tmp_path):
+    r = _run(tmp_path, 'genes')
+    # gene g on rank g (mod 2), every episode of the gene
+    for rank in range(2):
+        assert {g for _, g in r[rank]['pairs']} == {rank, rank + 2}
+        assert len(r[rank]['pairs']) == 4 * 2
+    for k in ('flat', 'ema', 'rs_mean', 'rs_var', 'genes'):
+        assert torch.equal(r[0][k], r[1][k]), k
+    # single process, all pairs: the rank rows reassembled by global pair index match
+    learner, env = _make(1, genes=4)
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    fit = learner.fitness(cum, genes)
+    for rank in range(2):
+        slots = torch.tensor(r[rank]['slots'])
+        assert torch.equal(r[rank]['first']['lens'], lens.cpu()[slots])
+        assert torch.equal(r[rank]['first']['actions'], traj['actions'].cpu()[slots])
+        torch.testing.assert_close(r[rank]['first']['fit'], fit, rtol=1e-6, atol=1e-6)

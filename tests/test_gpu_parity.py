@@ -182,8 +182,8 @@ def test_attention_dropout_consistent():
 
 def test_attention_dropout_mask_is_host_philox_stream():
     """The kept attention probabilities are exactly the host Philox stream's (oracle/philox.py):
-    keep(b, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + b H + h, FIELD_DROPOUT << 24; seed)
-    >= p 2^32.  Forward against a double reference that applies that mask after the softmax, and
+    keep(b, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + b H + h, FIELD_DROPOUT << 24 | layer;
+    seed) >= p 2^32.  Forward against a double reference that applies that mask after the softmax, and
     q / k / v gradients against its autograd (the backward kernels draw the same words, grouped
     differently: one Philox block per 4 rows, dealt out by a quad transpose in dK / dV)."""
     from xtrl_amd import ops
@@ -192,13 +192,13 @@ def test_attention_dropout_mask_is_host_philox_stream():
     b, H, n, dh = 2, 2, 70, 16
     q, k, v, do = (torch.randn(b, H, n, dh, generator=g) for _ in range(4))
     lens = torch.tensor([70, 45], dtype=torch.int32)
-    p, seed, offset, scale = 0.25, 1234567, 5, dh ** -0.5
+    p, seed, offset, scale, layer = 0.25, 1234567, 5, dh ** -0.5, 3
     thresh = np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
     i, j = np.arange(n)[:, None], np.arange(n)[None, :]
     keep = np.zeros((b, H, n, n), dtype=bool)
     for bb in range(b):
         for hh in range(H):
-            words = P.philox4x32(i >> 2, j, offset + bb * H + hh, P._c3(P.FIELD_DROPOUT, 0), seed)
+            words = P.philox4x32(i >> 2, j, offset + bb * H + hh, P._c3(P.FIELD_DROPOUT, layer), seed)
             keep[bb, hh] = np.choose(np.broadcast_to(i & 3, (n, n)), [np.broadcast_to(w, (n, n)) for w in words]) >= thresh
     keep_t = torch.from_numpy(keep).double() / (1 - p)
     qd, kd, vd = (t.double().requires_grad_() for t in (q, k, v))
@@ -208,7 +208,7 @@ def test_attention_dropout_mask_is_host_philox_stream():
     ref = torch.einsum('bhij,bhjd->bhid', s.masked_fill(~valid, float('-inf')).softmax(-1) * keep_t, vd)
     (ref * do.double()).sum().backward()
     qf, kf, vf = (t.to(DEV).requires_grad_() for t in (q, k, v))
-    out = ops.attention(qf, kf, vf, lens.to(DEV), scale, p, seed=seed, offset=offset)
+    out = ops.attention(qf, kf, vf, lens.to(DEV), scale, p, seed=seed, offset=offset, sub=layer)
     (out * do.to(DEV)).sum().backward()
     torch.cuda.synchronize()
     tol(out, ref, 1e-5, 1e-5)
@@ -217,25 +217,25 @@ def test_attention_dropout_mask_is_host_philox_stream():
     tol(vf.grad, vd.grad, 1e-4, 1e-5)
 
 
-@pytest.mark.parametrize('p', [0.25, 0.1])
-def test_ff_dropout_mask_is_host_philox_stream(p):
+@pytest.mark.parametrize('p,layer', [(0.25, 0), (0.1, 0), (0.25, 5), (0.1, 2)])
+def test_ff_dropout_mask_is_host_philox_stream(p, layer):
     """FF dropout keep mask (xtrl_ff_dropout_mask, the bits the GELU_DROP GEMM epilogue draws) equals
     the host Philox stream (oracle/philox.py).  p a multiple of 1/256 (byte mode): keep(m, n) = byte
     (m & 3) of word ((m >> 3) & 3) of philox4x32(n, 2 (m >> 5) + ((m >> 2) & 1), off, FIELD_FF_DROPOUT
-    sub 1; seed) >= 256 p; else (word mode): word (m & 3) of philox4x32(n, m >> 2, off, FIELD_FF_DROPOUT
-    sub 0; seed) >= p 2^32.  Keep fraction ~ 1 - p."""
+    sub 2 layer + 1; seed) >= 256 p; else (word mode): word (m & 3) of philox4x32(n, m >> 2, off,
+    FIELD_FF_DROPOUT sub 2 layer; seed) >= p 2^32.  Keep fraction ~ 1 - p."""
     from xtrl_amd.train import ff_dropout_mask
     from oracle import philox as P
     M, N, seed, off = 200, 70, 987654321, 11
-    got = ff_dropout_mask(M, N, p, seed, off, DEV).cpu().numpy().astype(bool)
+    got = ff_dropout_mask(M, N, p, seed, off, DEV, layer=layer).cpu().numpy().astype(bool)
     m, n = np.arange(M)[:, None], np.arange(N)[None, :]
     m, n = np.broadcast_to(m, (M, N)), np.broadcast_to(n, (M, N))
     if float(p * 256).is_integer():
-        words = P.philox4x32(n, ((m >> 5) << 1) | ((m >> 2) & 1), off, P._c3(P.FIELD_FF_DROPOUT, 1), seed)
+        words = P.philox4x32(n, ((m >> 5) << 1) | ((m >> 2) & 1), off, P._c3(P.FIELD_FF_DROPOUT, 2 * layer + 1), seed)
         w = np.choose((m >> 3) & 3, words)
         want = ((w >> (8 * (m & 3))) & 0xFF) >= int(p * 256)
     else:
-        words = P.philox4x32(n, m >> 2, off, P._c3(P.FIELD_FF_DROPOUT, 0), seed)
+        words = P.philox4x32(n, m >> 2, off, P._c3(P.FIELD_FF_DROPOUT, 2 * layer), seed)
         want = np.choose(m & 3, words) >= np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
     np.testing.assert_array_equal(got, want)
     assert abs(got.mean() - (1 - p)) < 0.02
@@ -247,18 +247,19 @@ def test_ff_dropout_mask_is_host_philox_stream(p):
 
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
-                 hazard=3, mode='lander', dim=48, reward_dropout=0.5):
+                 hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None):
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(seed)
     wm = dict(attn_dim_head=16, heads=4, depth=depth)
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
-    gp = dict(dim=8, num_genes_per_island=3, num_selected=2, tournament_size=2)
+    gp = dict(dim=gene_dim, num_genes_per_island=3, num_selected=2, tournament_size=2)
     learner = Learner(state_dim=S, num_actions=A, reward_range=(-2., 2.), world_model=wm, max_timesteps=T,
                       batch_size=batch, num_episodes_per_update=episodes, evolutionary=evo, evolve_every=1,
                       evolve_after_step=0, latent_gene_pool=gp, continuous_actions=cont,
                       continuous_actions_clamp=(-1., 1.) if cont else None,
-                      agent_kwargs=dict(dropout=0., seed=seed, hidden_dim=dim, reward_dropout=reward_dropout),
+                      agent_kwargs=dict(dropout=0., seed=seed, hidden_dim=dim, reward_dropout=reward_dropout,
+                                        **(agent_extra or {})),
                       use_graph=False)
     with torch.no_grad():   # non-trivial gate / mix weights (their init is constant)
         g = torch.Generator().manual_seed(seed + 1)
@@ -470,6 +471,19 @@ def test_adopt_atan2_and_clip_match_oracle():
 # ----------------------------------------------------------------------------------------------
 
 
+def gpu_episodes(traj, lens, genes, cont=False):
+    """The device trajectory as the reference's per-episode Memory lists (xtrl.py:67-81)."""
+    out = []
+    lens_c = lens.cpu()
+    for i, gene in enumerate(genes):
+        n = int(lens_c[i])
+        acts = traj['actions_f'][i, :n].cpu() if cont else traj['actions'][i, :n].cpu().long()
+        mem = list(zip(traj['states'][i, :n].cpu(), acts, traj['logp'][i, :n].cpu(), traj['rewards'][i, :n].cpu(),
+                       traj['bounds'][i, :n].cpu().bool(), traj['values'][i, :n].cpu()))
+        out.append(dict(mem=mem, len=n, gene=gene))
+    return out
+
+
 def oracle_minibatch_tensors(episodes):
     """Agent.learn's data preparation (xtrl.py:822-852) on the oracle side."""
     from torch.nn.utils.rnn import pad_sequence
@@ -519,7 +533,7 @@ def test_ppo_loss_and_grads_identical_weights(evo, gates, cont):
             keep = R.reward_coin(c.seed, u, epoch, mbi, c.reward_dropout)
             ref_loss, _, _, _ = R.minibatch_loss(oracle.model, rs, mb, latent, c.weights, keep)
             ref_loss.backward()
-            l_gpu, l_ref = float(loss), float(ref_loss)
+            l_gpu, l_ref = float(loss.detach()), float(ref_loss.detach())
             assert abs(l_gpu - l_ref) <= 1e-4 * abs(l_ref) + 1e-6, (u, epoch, mbi, l_gpu, l_ref)
             gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
             scale = max(float(p.grad.abs().max()) for p in oracle.model.parameters() if p.grad is not None)
@@ -669,3 +683,118 @@ def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, d
     for name, (s, e) in agent.flat.index.items():
         err = float((a['grad'][s:e] - b['grad'][s:e]).abs().max())
         assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
+
+
+# ----------------------------------------------------------------------------------------------
+# BASELINE configurations (C2, C3) against the oracle: rollout, then the learn step's loss and
+# every gradient on identical weights, at the configs' model shapes and sequence lengths
+# ----------------------------------------------------------------------------------------------
+
+
+def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_minibatches=2):
+    """Rollout of the device Learner vs the oracle's batch-1 loop (actions / lengths / rewards /
+    done masks bit-exact, log-probs and critic logits within 1e-4), then the first
+    ``max_minibatches`` minibatches of Agent.learn: loss within 1e-4 relative and every gradient
+    within 1e-4 of the gradient scale against the oracle on the GPU's weights and minibatch."""
+    learner, env, oracle = make_learner(depth=depth, gates=True, evo=evo, T=T, episodes=episodes, batch=batch, seed=4,
+                                        hazard=hazard, dim=dim, gene_dim=gene_dim)
+    agent = learner.agent
+    c = oracle.c
+    traj, lens, genes, cum = learner.rollout_device(env, 0, T)
+    torch.cuda.synchronize()
+    episodes_o, fitness = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    fit = learner.fitness(cum, genes)
+    if evo:
+        tol(fit, fitness, 1e-5, 1e-5)
+    states, actions, old_lp, rewards, bounds, values, elens, egenes = oracle_minibatch_tensors(
+        gpu_episodes(traj, lens, [ep['gene'] for ep in episodes_o]))
+    returns = R.calc_gae(rewards, oracle.model.hl(values), (~bounds).float(), c.gamma, c.lam)
+    rs = R.RSNormState(c.state_dim + 1)
+    rs.mean, rs.var = agent.rs_mean.cpu().clone(), agent.rs_var.cpu().clone()
+    seen = []
+
+    def probe(epoch, mbi, idx, loss, stats):
+        idx = idx.cpu()
+        oracle.model.load_state_dict({k: v.detach().cpu() for k, v in agent.model.state_dict().items()})
+        oracle.model.train()
+        oracle.model.zero_grad()
+        mb = R.Minibatch(states[idx], actions[idx], rewards[idx], old_lp[idx], returns[idx], values[idx], bounds[idx],
+                         egenes[idx], elens[idx])
+        latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if evo else None
+        keep = R.reward_coin(c.seed, 0, epoch, mbi, c.reward_dropout)
+        ref_loss, _, _, _ = R.minibatch_loss(oracle.model, rs, mb, latent, c.weights, keep)
+        ref_loss.backward()
+        l_gpu, l_ref = float(loss.detach()), float(ref_loss.detach())
+        assert abs(l_gpu - l_ref) <= 1e-4 * abs(l_ref) + 1e-6, (epoch, mbi, l_gpu, l_ref)
+        gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
+        scale = max(float(p.grad.abs().max()) for p in oracle.model.parameters() if p.grad is not None)
+        for name, p in oracle.model.named_parameters():
+            if p.grad is not None:
+                err = float((gpu_g[name] - p.grad).abs().max())
+                assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
+        seen.append((int(elens[idx].max()), l_gpu))
+        if len(seen) >= max_minibatches:
+            raise _Captured()
+
+    with pytest.raises(_Captured):
+        agent.learn(traj, lens, genes, fit, update=0, probe=probe)
+    return seen, lens
+
+
+def test_c3_shape_rollout_and_learn_match_oracle():
+    """C3 model (depth 4, d 256, 4 x 16 heads, gated values + learned value-residual mix) at its
+    sequence length (T = 128, termination hazard 1/64), 16 episodes in minibatches of 8."""
+    seen, lens = _config_parity(depth=4, dim=256, T=128, hazard=6, evo=False, episodes=16, batch=8)
+    assert len(seen) == 2 and int(lens.max()) > 64     # multi-tile training attention
+
+
+def test_c2_shape_rollout_and_learn_match_oracle():
+    """C2 model (train_lander defaults: depth 2, d 128, 3-gene EPO with 32-dim genes) at T = 500:
+    the decode attention over caches up to 500 keys and the training attention over 8 key tiles
+    (hazard 2^-9 so most episodes run long)."""
+    seen, lens = _config_parity(depth=2, dim=128, T=500, hazard=9, evo=True, episodes=2, batch=2, gene_dim=32)
+    assert int(lens.max()) > 256
+
+
+def test_c3_full_minibatch_fused_matches_reference_mode():
+    """The C3 learn step at its real minibatch (128 episodes x 128 steps = 16384 tokens, dropout
+    0.25): the fused step — X6 large-tile GEMMs, the warp-specialised kernel, split-K weight
+    gradients over 192 workgroups on the side stream — against the reference-mode autograd step on
+    identical weights, minibatch and dropout masks."""
+    _fused_vs_autograd(False, False, True, 0.25, 128, depth=4, episodes=128, batch=128, hazard=6, dim=256)
+
+
+def test_ema_schedule_and_model_copy_back_match_oracle():
+    """Agent EMA (xtrl.py:747-753, ema-pytorch restated) against oracle/thirdparty.EMA fed the same
+    online weights: copies before ``update_after_step``, the lerp with the warm-up decay after it
+    (k_ema on the flat buffer), and the online-model copy-back every ``update_model_with_ema_every``
+    steps — with ema_kwargs small enough that 40 optimiser steps cover all three."""
+    ek = dict(update_after_step=6, update_every=2, update_model_with_ema_every=14)
+    learner, _, _ = make_learner(depth=1, gates=False, agent_extra=dict(ema_kwargs=ek))
+    agent = learner.agent
+    online = torch.nn.Module()
+    online.p = torch.nn.Parameter(agent.flat.flat.detach().cpu().clone())
+    ema = tp.EMA(online, beta=agent.ema_beta, **ek)
+    snaps = []
+    orig = agent._ema_update
+
+    def hooked():
+        snaps.append(agent.flat.flat.detach().cpu().clone())
+        orig()
+
+    agent._ema_update = hooked
+    g = torch.Generator().manual_seed(21)
+    lerped = copied_back = 0
+    for i in range(40):
+        agent.flat.grad.copy_(torch.randn(agent.flat.n, generator=g).to(DEV) * 0.1)
+        agent.optimizer_step()
+        with torch.no_grad():
+            online.p.copy_(snaps[-1])
+        before = ema.ema_model.p.detach().clone()
+        ema.update()
+        lerped += int(ema.initted.item() and not torch.equal(before, ema.ema_model.p))
+        tol(agent.ema_flat, ema.ema_model.p, 1e-6, 1e-7)
+        tol(agent.flat.flat, online.p, 1e-6, 1e-7)
+        copied_back += int(torch.equal(online.p.detach(), ema.ema_model.p.detach()) and ema.initted.item())
+    assert agent.ema_step == 40 and lerped >= 10 and copied_back >= 2

@@ -17,12 +17,24 @@ def test_library_exports_every_declared_symbol():
     from xtrl_amd import _lib
     lib = _lib.load()
     header = (REPO / 'include' / 'xtrl_hip.h').read_text()
-    declared = set(re.findall(r'^\s*(?:int|float|const char\*)\s+(xtrl_\w+)\s*\(', header, re.M))
+    declared = set(re.findall(r'^\s*(?:int|int64_t|float|const char\*)\s+(xtrl_\w+)\s*\(', header, re.M))
     assert len(declared) >= 18
     for name in declared:
         assert hasattr(lib, name), name
     assert set(_lib.SIGNATURES) <= declared | {'xtrl_last_error'}
     assert lib.xtrl_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize('T,b,d,A', [(64 * 500, 64, 128, 1), (16384, 128, 256, 4), (10, 2, 48, 2), (17, 1, 8, 16)])
+def test_train_partial_workspace_covers_every_reduction(T, b, d, A):
+    """xtrl_train_part_floats (host-only) states the partial-sum floats a learn step needs: the
+    LayerNorm backward's 16-row blocks (ceil(T / 16) d), the column sums (min(1024, T / 16) d), the
+    latent gradient (b d) and one embedding chunk (A d) — the Python side sizes from it, so a
+    1-action env at 64 x 500 tokens (beyond the old (T / 64 + 1) d sizing) fits."""
+    from xtrl_amd import _lib
+    need = _lib.load().xtrl_train_part_floats(T, b, d, A)
+    assert need >= -(-T // 16) * d
+    assert need >= min(1024, max(1, T // 16)) * d and need >= b * d and need >= A * d
 
 
 def test_struct_layouts_match_header():

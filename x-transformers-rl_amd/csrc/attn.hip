@@ -8,7 +8,8 @@
 // Geometry: 64-row tiles, 4 waves x 16 rows; K/V (or Q/dO) tiles staged in LDS with a 2-float
 // row pad; the probability tile crosses LDS once per wave to turn the MFMA C layout (rows on
 // lane groups) into the A layout (rows on lanes), in a 66-float-stride image (conflict-free read).
-// Dropout keep bits: philox(seed; c0 = i >> 2, c1 = j, c2 = offset + b*H + h) word (i & 3).
+// Dropout keep bits: philox(seed; c0 = i >> 2, c1 = j, c2 = offset + b*H + h,
+// c3 = FIELD_DROPOUT << 24 | sub) word (i & 3); sub = the decoder layer.
 #include "kernels.h"
 #include "philox.h"
 
@@ -23,8 +24,8 @@ __device__ __forceinline__ f32x4v mfma16(float a, float b, f32x4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, int i, int j) {
-  const u32x4_t r = philox4x32_10((uint32_t)(i >> 2), (uint32_t)j, off, rng_c3(FIELD_DROPOUT, 0), seed);
+__device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, uint32_t c3, int i, int j) {
+  const u32x4_t r = philox4x32_10((uint32_t)(i >> 2), (uint32_t)j, off, c3, seed);
   const int w = i & 3;
   return w == 0 ? r.x : (w == 1 ? r.y : (w == 2 ? r.z : r.w));
 }
@@ -42,6 +43,7 @@ struct AttnArgs {
   uint32_t thresh;    // keep iff word >= thresh (thresh = 0: no dropout)
   uint64_t seed;
   uint32_t offset;
+  uint32_t c3;        // rng_c3(FIELD_DROPOUT, layer)
   int causal;
 };
 
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub)
         kws[sub] = philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)(kt * TK + 16 * sub + lr), off,
-                                 rng_c3(FIELD_DROPOUT, 0), a.seed);
+                                 a.c3, a.seed);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
         uint32_t kq[4] = {0u, 0u, 0u, 0u};
         if (a.thresh) {
           const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)(j0 + 16 * w + 4 * lg + (lr & 3)), off,
-                                           rng_c3(FIELD_DROPOUT, 0), a.seed);
+                                           a.c3, a.seed);
           kq[0] = kb.x;
           kq[1] = kb.y;
           kq[2] = kb.z;
@@ -340,7 +342,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
       const int jl = 16 * sub + lr, j = kt * TK + jl;
       // this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block (word = row & 3)
       const u32x4_t kw = a.thresh ? philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)j, off,
-                                                  rng_c3(FIELD_DROPOUT, 0), a.seed)
+                                                  a.c3, a.seed)
                                   : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -385,6 +387,8 @@ int fill_args(AttnArgs& a, const AttnProblem& p) {
   a.thresh = dropout_thresh(p.dropout);
   a.seed = p.seed;
   a.offset = p.offset;
+  XTRL_REQUIRE(p.sub < (1u << 24), "attn: dropout stream sub-index %u does not fit 24 bits", p.sub);
+  a.c3 = rng_c3(FIELD_DROPOUT, p.sub);
   a.causal = p.causal;
   return XTRL_OK;
 }
@@ -447,8 +451,9 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
 }
 
 AttnProblem contiguous_problem(const int32_t* lens, int b, int H, int n, int dh, float scale, float p, uint64_t seed,
-                               uint32_t offset) {
+                               uint32_t offset, uint32_t sub) {
   AttnProblem pr{b, H, n, dh, lens, scale, p, seed, offset, {}, {}, {}, {}};
+  pr.sub = sub;
   pr.in = pr.out = pr.grad = attn_layout_bhnd(H, n, dh);
   return pr;
 }
@@ -457,16 +462,16 @@ AttnProblem contiguous_problem(const int32_t* lens, int b, int H, int n, int dh,
 
 extern "C" int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o,
                              float* lse, int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
-                             uint32_t offset, void* stream) {
-  return xtrl::attn_fwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset), q, k, v, o,
+                             uint32_t offset, uint32_t sub, void* stream) {
+  return xtrl::attn_fwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset, sub), q, k, v, o,
                            lse, nullptr, nullptr, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
                              const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
                              int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed,
-                             uint32_t offset, void* stream) {
-  return xtrl::attn_bwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset), q, k, v, o,
+                             uint32_t offset, uint32_t sub, void* stream) {
+  return xtrl::attn_bwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset, sub), q, k, v, o,
                            lse, dout, dq, dk, dv, delta_ws, xtrl::as_stream(stream));
 }
 

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../include/xtrl_hip.h"
 #include "philox.h"
@@ -29,6 +30,20 @@ int check_launch(const char* what) {
 }  // namespace xtrl
 
 extern "C" int xtrl_abi_version(void) { return XTRL_ABI_VERSION; }
+
+// sizeof of a descriptor struct as compiled into the library (bindings check their mirrors)
+extern "C" int64_t xtrl_struct_size(const char* name) {
+  static const struct {
+    const char* name;
+    int64_t size;
+  } sizes[] = {{"XtrlDecodeLayer", sizeof(XtrlDecodeLayer)}, {"XtrlRngState", sizeof(XtrlRngState)},
+               {"XtrlDecodeDesc", sizeof(XtrlDecodeDesc)},   {"XtrlTrainLayer", sizeof(XtrlTrainLayer)},
+               {"XtrlTrainDesc", sizeof(XtrlTrainDesc)},     {"XtrlBatchDesc", sizeof(XtrlBatchDesc)},
+               {"XtrlLossDesc", sizeof(XtrlLossDesc)}};
+  for (const auto& s : sizes)
+    if (name && strcmp(name, s.name) == 0) return s.size;
+  return -1;
+}
 extern "C" const char* xtrl_last_error(void) { return xtrl::g_err; }
 
 // host-side views of the device random streams (reward-dropout coin, tests)

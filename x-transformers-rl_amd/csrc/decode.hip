@@ -239,7 +239,7 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
       D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
   }
   if (sub != 0) return;
-  const uint32_t slot = R.slot_offset + e;
+  const uint32_t slot = D.slot_of_row ? (uint32_t)D.slot_of_row[e] : R.slot_offset + (uint32_t)e;
   const int A = D.A;
   const float* lg = D.logits + (int64_t)e * (D.continuous ? 2 * A : A);
   if (!D.continuous) {

@@ -93,12 +93,12 @@ __device__ __forceinline__ bool epi_v4_ok(const GemmArgs& a, const float* C) {
 
 // FF dropout keep bits in byte mode (GemmArgs::drop_thresh8, p a multiple of 1/256): element (m, n)
 // keeps iff byte (m & 3) of word ((m >> 3) & 3) of philox(seed; n, 2 (m >> 5) + ((m >> 2) & 1),
-// drop_off, FIELD_FF_DROPOUT sub 1) is >= drop_thresh8 — the 16 rows of a 32-row MFMA tile one lane
+// drop_off, FIELD_FF_DROPOUT sub 2 layer + 1) is >= drop_thresh8 — the 16 rows of a 32-row MFMA tile one lane
 // holds (mb + 8 g + q, mb = 32-aligned base + 4 (lane >> 5)) share one block.  k_ff_mask (train.hip)
 // draws the same bits.
 __device__ __forceinline__ u32x4_t ff_block8(const GemmArgs& a, int n, int mb) {
   return philox4x32_10((uint32_t)n, (uint32_t)(((mb >> 5) << 1) | ((mb >> 2) & 1)), a.drop_off,
-                       rng_c3(FIELD_FF_DROPOUT, 1), a.seed);
+                       rng_c3(FIELD_FF_DROPOUT, 2 * a.drop_layer + 1), a.seed);
 }
 // the four bytes of word g (rows mb + 8 g + 0..3) as four "words" compared against drop_thresh8
 __device__ __forceinline__ u32x4_t ff_bytes8(const u32x4_t& kb, int g) {
@@ -139,7 +139,7 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
       for (int g = 0; g < 4; ++g) {
         u32x4_t kw{0u, 0u, 0u, 0u};
         if (DROP && a.drop_thresh && !a.drop_thresh8)
-          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
+          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 2 * a.drop_layer),
                              a.seed);
         else if (DROP && a.drop_thresh8)
           kw = ff_bytes8(kb, g);
@@ -265,7 +265,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
         // (byte mode: the lane's one block gives all 16)
         u32x4_t kw{0u, 0u, 0u, 0u};
         if (DROP && a.drop_thresh && !a.drop_thresh8)
-          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 0),
+          kw = philox4x32_10((uint32_t)n, (uint32_t)((mb + 8 * g) >> 2), a.drop_off, rng_c3(FIELD_FF_DROPOUT, 2 * a.drop_layer),
                              a.seed);
         else if (DROP && a.drop_thresh8)
           kw = ff_bytes8(kb, g);

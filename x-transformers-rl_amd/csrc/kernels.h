@@ -43,7 +43,8 @@ struct GemmArgs {
   const float* aux_in2 = nullptr; int ld_aux_in2 = 0;
   float* aux_out = nullptr;       int ld_aux_out = 0;
   uint64_t seed = 0;              // dropout (EPI_GELU_DROP): keep(m, n) =
-  uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT) word (m & 3)
+  uint32_t drop_off = 0;          //   philox(seed; n, m >> 2, drop_off, FIELD_FF_DROPOUT sub 2 layer) word (m & 3)
+  uint32_t drop_layer = 0;        //   (c3 sub-index = 2 * drop_layer + byte mode)
   uint32_t drop_thresh = 0;       //   >= drop_thresh (0: no dropout)
   uint32_t drop_thresh8 = 0;      // != 0: byte-mode keep bits (p = drop_thresh8 / 256 exactly), see ff_block8
   float inv_keep = 1.f;
@@ -111,6 +112,7 @@ struct AttnProblem {
   AttnLayout in, out, grad;   // q/k/v; o/do (and og); dq/dk/dv
   AttnLayout gate;            // gate pre-activations (x-transformers attn_gate_values)
   int causal = 1;             // 0: bidirectional (key-padding mask only; forward only)
+  uint32_t sub = 0;           // dropout stream sub-index (c3 low 24 bits): the decoder layer
 };
 
 // o (ungated) and lse; if gate != nullptr also og = o * sigmoid(gate) (og in the `out` layout)

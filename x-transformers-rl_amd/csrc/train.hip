@@ -7,6 +7,7 @@
 // (bias / LayerNorm-gain / embedding gradients) are two-phase with a fixed summation order, so the
 // step is deterministic run to run.
 #include <cstdlib>
+#include <vector>
 
 #include "kernels.h"
 #include "philox.h"
@@ -454,19 +455,19 @@ __global__ void k_copy_col(const float* src, int ld, float* dst, int lddst, int 
 // the FF dropout keep mask of the GELU_DROP epilogue (gemm.hip): word mode (one Philox block per
 // 4 rows of a column) or byte mode (thresh8 != 0: one block per 16 rows, see ff_block8)
 __global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint32_t thresh8, uint64_t seed,
-                          uint32_t off) {
+                          uint32_t off, uint32_t layer) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)M * N) return;
   const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
   if (thresh8) {
     const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(((m >> 5) << 1) | ((m >> 2) & 1)), off,
-                                    rng_c3(FIELD_FF_DROPOUT, 1), seed);
+                                    rng_c3(FIELD_FF_DROPOUT, 2 * layer + 1), seed);
     const int g = (m >> 3) & 3;
     const uint32_t w = g == 0 ? r.x : (g == 1 ? r.y : (g == 2 ? r.z : r.w));
     mask[i] = (uint8_t)(((w >> (8 * (m & 3))) & 0xFFu) >= thresh8);
     return;
   }
-  const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(m >> 2), off, rng_c3(FIELD_FF_DROPOUT, 0), seed);
+  const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(m >> 2), off, rng_c3(FIELD_FF_DROPOUT, 2 * layer), seed);
   const int q = m & 3;
   const uint32_t w = q == 0 ? r.x : (q == 1 ? r.y : (q == 2 ? r.z : r.w));
   mask[i] = (uint8_t)(thresh == 0 || w >= thresh);
@@ -488,13 +489,22 @@ struct Ctx {
 // the optimiser step reads dW.  They run on a low-priority side stream, each after an event on the
 // main stream marks its dY ready; the main stream waits for a specific side event before it
 // overwrites a buffer a pending weight gradient still reads (dx, dff, dproj), and for all of them
-// at the end of the backward.  The side stream and its event ring are created once per process
-// (one device per process) and hold no data.  XTRL_WGRAD_STREAM=0: everything on one stream.
-constexpr int kSideEvents = 160;
+// at the end of the backward.  The side stream and its event pool are created once per process
+// (one device per process, grown to the deepest model seen) and hold no data.
+// XTRL_WGRAD_STREAM=0: everything on one stream.
 struct SideStream {
   hipStream_t s = nullptr;
-  hipEvent_t ev[kSideEvents] = {};
+  std::vector<hipEvent_t> ev;
   bool ok = false;
+  // at least n events (false: creation failed, the caller runs single-stream)
+  bool ensure(size_t n) {
+    while (ok && ev.size() < n) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+      ev.push_back(e);
+    }
+    return ok;
+  }
 };
 SideStream& side_stream() {
   static SideStream S = [] {
@@ -504,25 +514,30 @@ SideStream& side_stream() {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
     x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least) == hipSuccess;
-    for (int i = 0; x.ok && i < kSideEvents; ++i)
-      x.ok = hipEventCreateWithFlags(&x.ev[i], hipEventDisableTiming) == hipSuccess;
     return x;
   }();
   return S;
 }
+// events one backward takes: 4 forks before the decoder blocks, 4 forks + 4 marks per block, one
+// fork + one mark for the embeddings and the final join
+constexpr size_t side_events_needed(int L) { return 8 * (size_t)L + 6; }
 
 // fork / mark / wait helpers of one backward call (no-ops on a single stream)
 struct Fork {
   hipStream_t main, side;
   SideStream* S;
   int next = 0;
+  bool failed = false;   // a mark() could not record: the final join reports it
   bool on() const { return S != nullptr; }
-  hipEvent_t take() { return S->ev[next++]; }
+  hipEvent_t take() {
+    if ((size_t)next >= S->ev.size()) return nullptr;   // (sized by side_events_needed: never)
+    return S->ev[next++];
+  }
   // the side stream waits for everything issued on the main stream so far
   int fork() {
     if (!on()) return XTRL_OK;
     hipEvent_t e = take();
-    if (hipEventRecord(e, main) != hipSuccess || hipStreamWaitEvent(side, e, 0) != hipSuccess) {
+    if (!e || hipEventRecord(e, main) != hipSuccess || hipStreamWaitEvent(side, e, 0) != hipSuccess) {
       set_error("train: side-stream fork failed");
       return XTRL_E_HIP;
     }
@@ -532,7 +547,10 @@ struct Fork {
   hipEvent_t mark() {
     if (!on()) return nullptr;
     hipEvent_t e = take();
-    if (hipEventRecord(e, side) != hipSuccess) return nullptr;
+    if (!e || hipEventRecord(e, side) != hipSuccess) {
+      failed = true;
+      return nullptr;
+    }
     return e;
   }
   // the main stream waits for a side event (nullptr: nothing to wait for)
@@ -549,13 +567,14 @@ struct Fork {
 // C[M][N] = A[M][K] . W[N][K]^T (+ bias) with an epilogue
 int linear_fwd(const Ctx& c, const float* A, int lda, const float* W, const float* bias, float* C, int ldc, int M,
                int N, int K, int epi, const float* R = nullptr, float* aux_out = nullptr, int ld_aux = 0,
-               int act_cols = 1 << 30, int bias_col0 = 0, uint32_t drop_off = 0) {
+               int act_cols = 1 << 30, int bias_col0 = 0, uint32_t drop_off = 0, uint32_t drop_layer = 0) {
   GemmArgs g;
   g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.K = K;
   g.R = R; g.ldr = ldc; g.aux_out = aux_out; g.ld_aux_out = ld_aux; g.act_cols = act_cols; g.bias_col0 = bias_col0;
   if (epi == EPI_GELU_DROP) {
     g.seed = c.D->seed;
     g.drop_off = drop_off;
+    g.drop_layer = drop_layer;
     g.drop_thresh = dropout_thresh(c.D->dropout);
     g.drop_thresh8 = dropout_thresh8(c.D->dropout);
     g.inv_keep = c.D->dropout > 0.f ? 1.f / (1.f - c.D->dropout) : 1.f;
@@ -630,7 +649,8 @@ AttnProblem attn_problem(const Ctx& c, const XtrlTrainLayer& Ly, int li) {
   p.scale = D->attn_scale;
   p.dropout = D->dropout;
   p.seed = D->seed;
-  p.offset = D->attn_offset + (uint32_t)li * 65536u;
+  p.offset = D->attn_offset;
+  p.sub = (uint32_t)li;
   p.in = attn_layout_tokens(D->n, 3 * I, D->dh);
   p.out = attn_layout_tokens(D->n, I, D->dh);
   p.grad = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
@@ -693,7 +713,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
       return rc;
     if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
     if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, ff, T, ff, d, EPI_GELU_DROP, nullptr,
-                         Ly.u, ff, 1 << 30, 0, D->ff_offset + (uint32_t)li)))
+                         Ly.u, ff, 1 << 30, 0, D->ff_offset, (uint32_t)li)))
       return rc;
     float* x_out = li + 1 < D->L ? D->layers[li + 1].x_attn : D->x_final;
     if ((rc = linear_fwd(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
@@ -729,7 +749,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4, S1x2 = 2 * (D->S + 1);
   int rc;
   SideStream& side = side_stream();
-  const bool two = side.ok && 4 * D->L + 24 <= kSideEvents;
+  const bool two = side.ok && side.ensure(side_events_needed(D->L));
   Fork F{s, side.s, two ? &side : nullptr};
   const Ctx cw{D, two ? side.s : s, T};   // weight gradients
   // ---- actor / critic heads
@@ -860,6 +880,9 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   }
   // every weight gradient is in before the caller's optimiser step
   if ((rc = F.wait(F.mark()))) return rc;
+  XTRL_REQUIRE(!F.failed, "train: side-stream event record failed");
+  XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L), "train: side events %d != %d", F.next,
+               (int)side_events_needed(D->L));
   return XTRL_OK;
 }
 
@@ -873,12 +896,22 @@ extern "C" int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream) {
   return xtrl::train_backward(desc, xtrl::as_stream(stream));
 }
 
+extern "C" int64_t xtrl_train_part_floats(int T, int b, int d, int A) {
+  if (T <= 0 || d <= 0) return 0;
+  const int64_t ln = (int64_t)((T + xtrl::LN_ROWS - 1) / xtrl::LN_ROWS) * d;            // ln_bwd partials
+  const int64_t cs = (int64_t)std::min(1024, std::max(1, T / 16)) * d;                  // colsum partials
+  const int64_t lat = (int64_t)std::max(b, 1) * d;                                      // latent gradient
+  const int64_t emb = (int64_t)std::max(A, 1) * d;                                      // >= 1 embedding chunk
+  return std::max(std::max(ln, cs), std::max(lat, emb));
+}
+
 extern "C" int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset,
-                                    void* stream) {
+                                    uint32_t layer, void* stream) {
+  XTRL_REQUIRE(layer < (1u << 22), "ff_dropout_mask: layer %u out of range", layer);
   XTRL_REQUIRE(mask && M >= 0 && N >= 0 && p >= 0.f && p < 1.f, "ff_dropout_mask: bad arguments");
   if ((int64_t)M * N == 0) return XTRL_OK;
   hipLaunchKernelGGL(xtrl::k_ff_mask, dim3((unsigned)(((int64_t)M * N + 255) / 256)), dim3(256), 0,
-                     xtrl::as_stream(stream), mask, M, N, xtrl::dropout_thresh(p), xtrl::dropout_thresh8(p), seed, offset);
+                     xtrl::as_stream(stream), mask, M, N, xtrl::dropout_thresh(p), xtrl::dropout_thresh8(p), seed, offset, layer);
   XTRL_LAUNCHED("ff_dropout_mask");
   return XTRL_OK;
 }

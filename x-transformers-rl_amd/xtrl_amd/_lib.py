@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -44,7 +44,7 @@ class DecodeDesc(C.Structure):
                                     'ln_final', 'w_h1', 'b_h1', 'w_a2', 'b_a2', 'w_c2', 'b_c2', 'inv_freq')]
                 + [('layers', C.POINTER(DecodeLayer))]
                 + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
-                                    'alive', 'lens', 'cum_reward', 'episode_of_slot', 'rng', 'traj_states',
+                                    'alive', 'lens', 'cum_reward', 'episode_of_slot', 'slot_of_row', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
                                     'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals', 'xn')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
@@ -94,6 +94,7 @@ class BatchDesc(C.Structure):
 
 SIGNATURES = {
     'xtrl_abi_version': (I32, []),
+    'xtrl_struct_size': (C.c_int64, [C.c_char_p]),
     'xtrl_last_error': (C.c_char_p, []),
     'xtrl_gemm_f32': (I32, [P, I32, P, I32, P, P, P, I32, P, I32, P, I64, I32, I32, I32, I32, P]),
     'xtrl_gemm_ex': (I32, [I32, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, F32, P]),
@@ -104,8 +105,8 @@ SIGNATURES = {
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P]),
     'xtrl_attn_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P]),
-    'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, P]),
-    'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, P]),
+    'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
+    'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_loss_fwd': (I32, [C.POINTER(LossDesc), P]),
     'xtrl_loss_bwd': (I32, [C.POINTER(LossDesc), F32, P]),
     'xtrl_grad_norm': (I32, [P, I64, P, F32, P, P]),
@@ -115,7 +116,8 @@ SIGNATURES = {
     'xtrl_sim_reset': (I32, [P, I32, I32, U64, U32, P, P]),
     'xtrl_train_forward': (I32, [C.POINTER(TrainDesc), P]),
     'xtrl_train_backward': (I32, [C.POINTER(TrainDesc), P]),
-    'xtrl_ff_dropout_mask': (I32, [P, I32, I32, F32, U64, U32, P]),
+    'xtrl_ff_dropout_mask': (I32, [P, I32, I32, F32, U64, U32, U32, P]),
+    'xtrl_train_part_floats': (C.c_int64, [I32, I32, I32, I32]),
     'xtrl_minibatch_gather': (I32, [C.POINTER(BatchDesc), P]),
     'xtrl_rsnorm_update': (I32, [P, P, P, I32, I32, P]),
     'xtrl_attn_fwd_tokens': (I32, [P, I32, P, I32, P, I32, P, P, I32, P, I32, I32, I32, I32, F32, I32, P]),
@@ -127,6 +129,10 @@ SIGNATURES = {
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
 }
+
+STRUCTS = {'XtrlDecodeLayer': DecodeLayer, 'XtrlRngState': RngState, 'XtrlDecodeDesc': DecodeDesc,
+           'XtrlTrainLayer': TrainLayer, 'XtrlTrainDesc': TrainDesc, 'XtrlBatchDesc': BatchDesc,
+           'XtrlLossDesc': LossDesc}
 
 _lib = None
 
@@ -144,6 +150,10 @@ def load():
             fn.restype, fn.argtypes = res, args
         if lib.xtrl_abi_version() != ABI_VERSION:
             raise RuntimeError(f'libxtrl_hip ABI {lib.xtrl_abi_version()} != {ABI_VERSION}')
+        for cname, py in STRUCTS.items():   # a stale build against an edited header fails here
+            got = lib.xtrl_struct_size(cname.encode())
+            if got != C.sizeof(py):
+                raise RuntimeError(f'libxtrl_hip {cname} is {got} bytes, the binding {C.sizeof(py)}: rebuild')
         _lib = lib
     return _lib
 

@@ -52,6 +52,15 @@ def shard_pairs(pairs, world, rank):
     return pairs[start:start + size], start
 
 
+def shard_pairs_by_gene(pairs, world, rank):
+    """Gene-parallel EPO partition: rank r takes the pairs of genes g = r (mod
+    world) -> (this rank's pairs, their global pair indices).  With population == world, gene g
+    lives on rank g; fitnesses are then summed over ranks (each rank fills only its genes)."""
+    mine = [(i, p) for i, p in enumerate(pairs) if p[1] % world == rank]
+    assert mine, 'need at least one (episode, gene) pair per process'
+    return [p for _, p in mine], [i for i, _ in mine]
+
+
 def _on_backend_device(t):
     """RCCL ("nccl") only moves device tensors: stage host tensors through the GPU."""
     if t.device.type == 'cpu' and dist.get_backend() == 'nccl':

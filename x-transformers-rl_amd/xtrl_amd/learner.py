@@ -40,6 +40,11 @@ from .rollout import SIM_HOST, SIM_LANDER, SIM_README, RolloutEngine
 from .train import rsnorm_update
 
 
+# ema-pytorch EMA keyword defaults the restatement honours (xtrl.py:747 passes **ema_kwargs)
+EMA_DEFAULTS = dict(update_after_step=100, update_every=10, inv_gamma=1., power=2 / 3, min_value=0.,
+                    update_model_with_ema_every=None, update_model_with_ema_beta=0.)
+
+
 def epoch_permutation(seed, update, epoch, n):
     g = torch.Generator().manual_seed((int(seed) * 1000003 + int(update)) * 1000003 + int(epoch) & (2 ** 62 - 1))
     return torch.randperm(n, generator=g)
@@ -113,7 +118,7 @@ class Agent(nn.Module):
         if self.gene_pool is not None:
             dist_.broadcast_(self.gene_pool.genes)
 
-        # EMA copy (ema-pytorch semantics restated: update_after_step 100, update_every 10, power 2/3)
+        # EMA copy (ema-pytorch semantics restated, xtrl.py:747: EMA(model, beta=ema_decay, **ema_kwargs))
         self.ema_model = copy.deepcopy(self.model)
         for p in self.ema_model.parameters():
             p.grad = None
@@ -121,9 +126,17 @@ class Agent(nn.Module):
         self.flat.rebind(self.ema_model, self.ema_flat)
         self.gemm_ws = torch.empty(32 << 20, device=dev)    # split-K weight-gradient partial tiles (128 MiB)
         self.model.bind_flat(self.flat, self.gemm_ws)
+        ek = dict(EMA_DEFAULTS)
+        unknown = set(ema_kwargs or {}) - set(ek)
+        if unknown:
+            raise TypeError(f'ema_kwargs {sorted(unknown)} are not supported (known: {sorted(ek)})')
+        ek.update(ema_kwargs or {})
         self.ema_beta = ema_decay
-        self.ema_update_every, self.ema_update_after = 10, 100
-        self.ema_model_every = (ema_kwargs or {}).get('update_model_with_ema_every', None)
+        self.ema_update_every, self.ema_update_after = int(ek['update_every']), int(ek['update_after_step'])
+        self.ema_inv_gamma, self.ema_power, self.ema_min = float(ek['inv_gamma']), float(ek['power']), \
+            float(ek['min_value'])
+        self.ema_model_every = ek['update_model_with_ema_every']
+        self.ema_model_beta = float(ek['update_model_with_ema_beta'])
         self.ema_step, self.ema_initted = 0, False
         # AdoptAtan2 state over the flat buffer
         n = self.flat.n
@@ -240,11 +253,18 @@ class Agent(nn.Module):
         if not self.ema_initted:
             self.ema_flat.copy_(self.flat.flat)
             self.ema_initted = True
-        epoch = max(self.ema_step - self.ema_update_after - 1, 0)
-        decay = 0. if epoch <= 0 else min(max(1 - (1 + epoch) ** (-2 / 3), 0.), self.ema_beta)
-        ops.ema_lerp(self.ema_flat, self.flat.flat, 1. - decay)
+        ops.ema_lerp(self.ema_flat, self.flat.flat, 1. - self.ema_decay())
         if self.ema_model_every is not None and step % self.ema_model_every == 0:
-            self.flat.flat.copy_(self.ema_flat)
+            # the online model takes the EMA weights (ema-pytorch update_model_with_ema)
+            ops.ema_lerp(self.flat.flat, self.ema_flat, 1. - self.ema_model_beta)
+
+    def ema_decay(self):
+        """ema-pytorch get_current_decay (after the step counter's increment)."""
+        epoch = max(self.ema_step - self.ema_update_after - 1, 0)
+        if epoch <= 0:
+            return 0.
+        value = 1 - (1 + epoch / self.ema_inv_gamma) ** -self.ema_power
+        return min(max(value, self.ema_min), self.ema_beta)
 
     # ---- optimiser step: clip_grad_norm_ + AdoptAtan2 + EMA hook (xtrl.py:987-992) ---------------------
     def optimizer_step(self):
@@ -287,7 +307,10 @@ class Agent(nn.Module):
             returns = returns.contiguous()
             gather = self.batch_gather(traj['rewards'].shape[1])
         # one stats row per minibatch, written in place by the fused loss (no per-minibatch clone)
-        n_mb = self.epochs * ((N + self.batch_size - 1) // self.batch_size)
+        n_mb_epoch = (N + self.batch_size - 1) // self.batch_size
+        n_mb = self.epochs * n_mb_epoch
+        attn_stride = self.batch_size * c.heads
+        assert n_mb * attn_stride < 2 ** 32, "attention dropout counters exceed 32 bits"
         stats_rows = torch.zeros(n_mb, L.LOSS_STATS, device=dev) if fused else None
         logs0 = len(self.logs)
         for epoch in range(self.epochs):
@@ -312,8 +335,10 @@ class Agent(nn.Module):
                     mb_old_v, mb_done = old_values[idx].contiguous(), bounds[idx].contiguous()
                 keep = reward_coin(self.seed, update, epoch, mbi, c.reward_dropout)
                 latent = self.latent(gene_ids[idx]) if c.evolutionary else None
-                attn_seed, attn_off, ff_off = self.seed * 1000003 + update, (epoch * 4096 + mbi) * 1024, \
-                    (epoch * 4096 + mbi) * 64
+                # dropout streams: every minibatch of the update its own FF counter and a disjoint
+                # range of attention counters (layer in the Philox c3 sub-index, include/xtrl_hip.h)
+                ordinal = epoch * n_mb_epoch + mbi
+                attn_seed, attn_off, ff_off = self.seed * 1000003 + update, ordinal * attn_stride, ordinal
                 if self.fused_learn:
                     step = self.train_step(b, n)
                     step.forward(swr, prev_act, mb_act, latent, mb_lens, keep, attn_seed, attn_off, ff_off,
@@ -434,7 +459,7 @@ class Learner(nn.Module):
                  num_episodes_per_update=64, lr=0.0008, betas=(0.9, 0.99), lam=0.95, gamma=0.99, eps_clip=0.2,
                  value_clip=0.4, beta_s=.01, regen_reg_rate=1e-4, cautious_factor=0.1, epochs=4, ema_decay=0.9,
                  save_every=100, frac_actor_critic_head_gradient=0.5, accelerate_kwargs: dict = dict(),
-                 agent_kwargs: dict = dict(), use_graph=True):
+                 agent_kwargs: dict = dict(), use_graph=True, shard_by_gene=False):
         super().__init__()
         assert num_episodes_per_update % batch_size == 0   # xtrl.py:1104
         self.accelerator = dist_.DistContext(accelerate_kwargs.get('device') if accelerate_kwargs else None)
@@ -457,7 +482,16 @@ class Learner(nn.Module):
         # (episode, gene) pairs must split evenly (the reference all-gathers instead, xtrl.py:868-871)
         assert world == 1 or len(self.episode_genes) % world == 0, \
             f'{len(self.episode_genes)} (episode, gene) pairs do not split evenly over {world} processes'
-        self.episode_genes_for_process, self.slot_offset = dist_.shard_pairs(self.episode_genes, world, rank)
+        # shard_by_gene (C5, evolutionary): rank r rolls out every episode of genes g = r (mod world),
+        # so with population == world gene g lives on GPU g; otherwise torch.chunk over the pairs
+        self.shard_by_gene = bool(shard_by_gene and evolutionary)
+        if self.shard_by_gene:
+            assert n_genes % world == 0, f'{n_genes} genes do not split evenly over {world} processes'
+            mine, slots = dist_.shard_pairs_by_gene(self.episode_genes, world, rank)
+            self.episode_genes_for_process, self.slot_offset, self.pair_slots = mine, 0, slots
+        else:
+            self.episode_genes_for_process, self.slot_offset = dist_.shard_pairs(self.episode_genes, world, rank)
+            self.pair_slots = None
         self.num_actions, self.continuous_actions = num_actions, continuous_actions
         self.continuous_actions_clamp = continuous_actions_clamp
         self.save_every = save_every
@@ -488,7 +522,7 @@ class Learner(nn.Module):
         ep = torch.tensor([e for e, _ in pairs], dtype=torch.int32)
         genes = torch.tensor([g for _, g in pairs], dtype=torch.long, device=self.device)
         latent = agent.latent(genes) if agent.evolutionary else None
-        traj = eng.run(agent.seed, update, ep, latent, slot_offset=self.slot_offset)
+        traj = eng.run(agent.seed, update, ep, latent, slot_offset=self.slot_offset, slots=self.pair_slots)
         return traj, eng.lens, genes, eng.cum_reward
 
     # ---- host-env rollout (reference loop, batch 1) -----------------------------------------------
@@ -530,13 +564,17 @@ class Learner(nn.Module):
                 kw = dict(seed=int(episode_seeds[episode]))
             latent = agent.latent(torch.tensor([gene], device=dev)) if agent.evolutionary else None
             traj, n_steps, total = eng.run_host_env(lambda: reset(kw), step, agent.seed, update, latent,
-                                                    slot_offset=self.slot_offset + i, max_steps=T)
+                                                    slot_offset=self._slot(i), max_steps=T)
             for k, v in traj.items():
                 if v is not None:
                     out[k][i].copy_(v[0])
             lens[i] = n_steps
             cum[i] = total
         return out, lens.to(dev), genes, cum
+
+    def _slot(self, i):
+        """Global (episode, gene) pair index of this rank's i-th pair (keys its sampling stream)."""
+        return self.pair_slots[i] if self.pair_slots is not None else self.slot_offset + i
 
     def _engine_for_host(self, T):
         key = ('host', T)

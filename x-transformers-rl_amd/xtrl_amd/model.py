@@ -272,7 +272,7 @@ class WorldModelActorCritic(nn.Module):
                 first_v = orig_v
             q = torch.cat((q[..., :rot] * cos + _rotate_half(q[..., :rot]) * sin, q[..., rot:]), dim=-1)
             k = torch.cat((k[..., :rot] * cos + _rotate_half(k[..., :rot]) * sin, k[..., rot:]), dim=-1)
-            o = ops.attention(q, k, v, lens, dh ** -0.5, p_drop, attn_seed, attn_offset + li * 65536)
+            o = ops.attention(q, k, v, lens, dh ** -0.5, p_drop, attn_seed, attn_offset, li)
             o = o.permute(0, 2, 1, 3).reshape(b, n, I)
             if gate_pre is not None:
                 o = o * gate_pre.sigmoid()
@@ -281,7 +281,7 @@ class WorldModelActorCritic(nn.Module):
             h = F.gelu(self._lin(ln_f(x), ffb.ff[0][0]))
             if p_drop > 0:
                 from .train import ff_dropout_mask
-                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset + li, h.device)
+                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset, h.device, layer=li)
                 h = h * keep.view(b, n, -1).to(h.dtype) * (1.0 / (1.0 - p_drop))
             x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)

@@ -112,7 +112,7 @@ class AttentionFn(torch.autograd.Function):
     """softmax(q k^T * scale + causal/key-padding mask) with post-softmax dropout, times v."""
 
     @staticmethod
-    def forward(ctx, q, k, v, lens, scale, dropout_p, seed, offset):
+    def forward(ctx, q, k, v, lens, scale, dropout_p, seed, offset, sub):
         lib = L.lib()
         b, H, n, dh = q.shape
         for t in (q, k, v):
@@ -122,28 +122,31 @@ class AttentionFn(torch.autograd.Function):
         o = torch.empty_like(q)
         lse = torch.empty(b, H, n, device=q.device, dtype=torch.float32)
         L.check(lib.xtrl_attn_fwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), b, H, n, dh,
-                                  float(scale), float(dropout_p), int(seed), int(offset), L.stream()), 'attn_fwd')
+                                  float(scale), float(dropout_p), int(seed), int(offset), int(sub), L.stream()),
+                'attn_fwd')
         ctx.save_for_backward(q, k, v, lens, o, lse)
-        ctx.cfg = (float(scale), float(dropout_p), int(seed), int(offset))
+        ctx.cfg = (float(scale), float(dropout_p), int(seed), int(offset), int(sub))
         return o
 
     @staticmethod
     def backward(ctx, do):
         lib = L.lib()
         q, k, v, lens, o, lse = ctx.saved_tensors
-        scale, p, seed, offset = ctx.cfg
+        scale, p, seed, offset, sub = ctx.cfg
         b, H, n, dh = q.shape
         do = do.contiguous()
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         delta = torch.empty(b, H, n, device=q.device, dtype=torch.float32)
         L.check(lib.xtrl_attn_bwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), L.ptr(do),
                                   L.ptr(dq), L.ptr(dk), L.ptr(dv), L.ptr(delta), b, H, n, dh, scale, p, seed, offset,
-                                  L.stream()), 'attn_bwd')
-        return dq, dk, dv, None, None, None, None, None
+                                  sub, L.stream()), 'attn_bwd')
+        return dq, dk, dv, None, None, None, None, None, None
 
 
-def attention(q, k, v, lens, scale, dropout_p=0., seed=0, offset=0):
-    return AttentionFn.apply(q.contiguous(), k.contiguous(), v.contiguous(), lens, scale, dropout_p, seed, offset)
+def attention(q, k, v, lens, scale, dropout_p=0., seed=0, offset=0, sub=0):
+    """``offset`` / ``sub``: the dropout stream (Philox c2 base and c3 sub-index = decoder layer)."""
+    return AttentionFn.apply(q.contiguous(), k.contiguous(), v.contiguous(), lens, scale, dropout_p, seed, offset,
+                             sub)
 
 
 # --------------------------------------------------------------------------------------------

@@ -54,6 +54,7 @@ class RolloutEngine:
         self.prev_reward, self.alive, self.lens = z(E), z(E, dt=u8), z(E, dt=i32)
         self.cum_reward = z(E, dt=torch.float64)
         self.episode_of_slot = z(E, dt=i32)
+        self.slot_of_row = z(E, dt=i32)   # global pair index per row (non-contiguous shards)
         self.rng = z(groups, 2, dt=torch.int64)
         # trajectory
         self.traj = dict(states=z(E, Tmax, S), actions=z(E, Tmax, dt=i32), actions_f=z(E, Tmax, A) if c.continuous else None,
@@ -113,6 +114,7 @@ class RolloutEngine:
         for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
                   'episode_of_slot'):
             setattr(D, k, rows(getattr(self, k)))
+        D.slot_of_row = None
         D.rng = self.rng[g].data_ptr()
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
@@ -176,7 +178,14 @@ class RolloutEngine:
             self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
 
     # ------------------------------------------------------------------------------------------
-    def _begin(self, seed, update, slot_offset, episode_of_slot, latent):
+    def _begin(self, seed, update, slot_offset, episode_of_slot, latent, slots=None):
+        """``slots``: per-row global pair indices keying the sampling stream (gene-sharded ranks);
+        None: rows are the contiguous pairs slot_offset, slot_offset + 1, ..."""
+        if slots is not None:
+            self.slot_of_row.copy_(torch.as_tensor(slots, dtype=torch.int32))
+        for g, D in enumerate(self.descs):
+            Eg = self.E // self.groups
+            D.slot_of_row = self.slot_of_row[g * Eg:].data_ptr() if slots is not None else None
         for t in self.traj.values():
             if t is not None:
                 t.zero_()
@@ -221,16 +230,16 @@ class RolloutEngine:
             main.wait_event(ev)
 
     @torch.no_grad()
-    def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0):
+    def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0, slots=None):
         """Roll out Tmax steps of the device Sim for all E slots; returns the trajectory dict."""
         assert self.sim_mode != SIM_HOST
-        self._begin(seed, update, slot_offset, episode_of_slot, latent)
+        self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
         if not self.use_graph:
             self._steps()
         else:
             if self.graph is None:
                 self._steps()   # warm-up launch outside capture (code objects loaded)
-                self._begin(seed, update, slot_offset, episode_of_slot, latent)
+                self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self._steps()

@@ -78,7 +78,9 @@ class FusedTrainStep:
                         dx=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
-        part = max(256 * max(ff, 4 * d, B, max_qkv), (T // 64 + 1) * d, 1024 * max(A, 1) * d, b_max * d)
+        # the library states its own partial-sum needs (LayerNorm-backward row blocks, column sums)
+        part = max(256 * max(ff, 4 * d, B, max_qkv), 1024 * max(A, 1) * d,
+                   int(L.lib().xtrl_train_part_floats(T, b_max, d, A)))
         self.buf['part'] = E(part)
         self.tok = torch.empty(b_max, n_max, L.LOSS_TOK, **f32)
         self.stats = torch.zeros(L.LOSS_STATS, **f32)
@@ -186,11 +188,11 @@ class FusedTrainStep:
         L.check(L.lib().xtrl_train_backward(C.byref(self.D), L.stream()), 'train_backward')
 
 
-def ff_dropout_mask(M, N, p, seed, offset, device):
+def ff_dropout_mask(M, N, p, seed, offset, device, layer=0):
     """The feed-forward dropout keep mask the fused step uses (uint8 [M][N]) — reference mode."""
     m = torch.empty(M, N, device=device, dtype=torch.uint8)
     L.check(L.lib().xtrl_ff_dropout_mask(L.ptr(m), M, N, float(p), int(seed) & (2 ** 64 - 1),
-                                         int(offset) & 0xFFFFFFFF, L.stream()), 'ff_dropout_mask')
+                                         int(offset) & 0xFFFFFFFF, int(layer), L.stream()), 'ff_dropout_mask')
     return m
 
 
