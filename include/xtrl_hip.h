@@ -158,8 +158,14 @@ int xtrl_rollout_begin(const XtrlDecodeDesc* desc, void* stream);
 /* one timestep t for all E episodes; with sim_mode == -1 the env step happens on the host and
  * xtrl_rollout_env_feedback() writes its results back. */
 int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream);
+/* Host env results of step t (xtrl.py:1297-1336) for the live rows: next_state [E][S], reward [E],
+ * terminated [E] (stored as is_boundary), truncated [E] or NULL.  An episode ends when terminated,
+ * truncated or t + 1 == t_limit (max_timesteps); with `bootstrap` a truncated, not terminated
+ * episode takes one more decode step that only writes its critic logits (the next state's value,
+ * xtrl.py:1323-1336) into the padding slot traj_values[e][t + 1] (needs t + 1 < Tmax). */
 int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state, const float* reward,
-                              const uint8_t* terminated, void* stream);
+                              const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap,
+                              void* stream);
 
 /* Attention for one decode step (exposed for tests): reads q|k|v|gate|mix rows, applies value
  * residual + rotary, appends k/v at position t and attends over positions 0..t. */
@@ -173,10 +179,12 @@ int xtrl_attn_decode(const XtrlDecodeDesc* desc, int layer, int t, void* stream)
  *   logits row (e, t) at logits + e*ld_row + t*B; rewards / bounds at e*ld_seq + t;
  *   values / returns written densely [E][n]; gamma_lam = float32(gamma * lam) as the reference
  *   multiplies the Python product into the mask
+ *   boot [E] (or NULL): the value of the state after a truncated episode's last step (NaN: none);
+ *   it stands in for v at index lens[e] (xtrl.py:1323-1336 bootstrap memory)
  * ------------------------------------------------------------------------------------------- */
 int xtrl_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, const uint8_t* bounds,
                      int64_t ld_seq, const float* centers, float* values, float* returns, int E, int n, int B,
-                     float gamma, float gamma_lam, void* stream);
+                     float gamma, float gamma_lam, const float* boot, const int32_t* lens, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Training attention (x-transformers Attend with causal + key-padding mask, post-softmax dropout)

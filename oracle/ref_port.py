@@ -165,8 +165,16 @@ class RSNormState:
 # --------------------------------------------------------------------------------------------
 
 
-def calc_gae(rewards, values, masks, gamma=0.99, lam=0.95):
+def calc_gae(rewards, values, masks, gamma=0.99, lam=0.95, boot=None, lens=None):
+    """xtrl.py:616-640.  ``boot`` [b] (NaN: none) with ``lens``: the value of the state after a
+    truncated episode's last step (the bootstrap memory of xtrl.py:1323-1336) stands in for v at
+    index lens[i] — what the reference's GAE would read had that memory joined its episode."""
     v = F.pad(values, (0, 1), value=0.)
+    if boot is not None:
+        v = v.clone()
+        for i, (bv, le) in enumerate(zip(boot.tolist(), lens.tolist())):
+            if bv == bv:
+                v[i, le] = bv
     v_now, v_next = v[..., :-1], v[..., 1:]
     delta = rewards + gamma * v_next * masks - v_now
     gates = gamma * lam * masks
@@ -549,6 +557,71 @@ class OracleLearner:
             episodes.append(dict(mem=mem, len=t + 1, gene=gene))
         return episodes, fitness
 
+    def rollout_env(self, env, update, max_timesteps=None, episode_seeds=None, bootstrap=True):
+        """The reference loop against a host env (xtrl.py:1220-1341), batch 1, one env object for
+        every (episode, gene) pair: reset(**{seed}) -> state | (state, ...); step(action.tolist())
+        -> (s, r, terminated[, truncated, ...]) (a 4-tuple's 4th item is read as truncated,
+        reference quirk B8); the memory stores is_boundary = terminated; done = terminated or
+        truncated.  A truncated, not terminated episode gets the next state's value logits as
+        ep['boot'] (xtrl.py:1323-1336) when ``bootstrap``."""
+        c = self.c
+        T = max_timesteps or c.max_timesteps
+        model = self.ema.ema_model
+        model.eval()
+        episodes = []
+        fitness = torch.zeros(len(self.genes) if c.evolutionary else 1)
+        for slot, (episode, gene) in enumerate(self.episode_genes):
+            kw = dict(seed=int(episode_seeds[episode])) if (c.evolutionary and episode_seeds is not None) else {}
+            out = env.reset(**kw)
+            state = torch.from_numpy(np.asarray(out[0] if isinstance(out, tuple) else out, dtype=np.float32))
+            prev_action = torch.zeros(c.num_actions) if c.continuous else torch.tensor(-1)
+            prev_reward = torch.tensor(0.)
+            latent = self.latent(torch.tensor([gene])) if c.evolutionary else None
+            cache = None
+            mem, total, boot = [], 0., None
+
+            def policy(state, prev_action, prev_reward, cache):
+                swr = self.rsnorm.apply(torch.cat((state, prev_reward[None])))
+                raw, values, _, _, cache = model(swr[:-1].reshape(1, 1, -1),
+                                                 actions=prev_action.reshape(1, 1, *prev_action.shape),
+                                                 rewards=swr[-1], latent_gene=latent, cache=cache)
+                return raw.reshape(-1), values.reshape(-1), cache
+
+            for t in range(T):
+                raw, values, cache = policy(state, prev_action, prev_reward, cache)
+                u = torch.from_numpy(philox_uniform(c.seed, update, slot, t, FIELD_SAMPLE, 1)).float()
+                if c.continuous:
+                    z = torch.from_numpy(philox_uniform(c.seed, update, slot, t, FIELD_SAMPLE, c.num_actions,
+                                                        normal=True)).float()
+                    action = continuous_sample(raw, z, c.squash)
+                    lp = continuous_log_prob(raw, action, c.squash)
+                    if c.clamp is not None:
+                        action = action.clamp(*c.clamp)
+                else:
+                    action = discrete_sample_icdf(raw, u[0])
+                    lp = discrete_log_prob(raw, action)
+                o = env.step(action.tolist())
+                if len(o) >= 4:
+                    nxt, reward, terminated, truncated = o[:4]
+                elif len(o) == 3:
+                    (nxt, reward, terminated), truncated = o, False
+                else:
+                    raise RuntimeError('invalid number of returns from environment .step')
+                reward = float(np.asarray(reward).reshape(-1)[0])
+                total += reward
+                prev_action, prev_reward = action, torch.tensor(reward)
+                mem.append((state, action, lp, torch.tensor(reward), torch.tensor(bool(terminated)), values))
+                state = torch.from_numpy(np.asarray(nxt, dtype=np.float32))
+                done = bool(terminated) or bool(truncated)
+                if done and not terminated and bootstrap:
+                    _, boot, _ = policy(state, prev_action, prev_reward, cache)
+                if done:
+                    break
+            if c.evolutionary:
+                fitness[gene] += total
+            episodes.append(dict(mem=mem, len=t + 1, gene=gene, boot=boot))
+        return episodes, fitness
+
     def learn(self, episodes, fitness, update):
         """xtrl.py:808-1023."""
         c = self.c
@@ -557,7 +630,11 @@ class OracleLearner:
         states, actions, old_lp, rewards, bounds, values = (pad_sequence(list(col), batch_first=True) for col in cols)
         lens = torch.tensor([ep['len'] for ep in episodes])
         gene_ids = torch.tensor([ep['gene'] for ep in episodes])
-        returns = calc_gae(rewards, hl(values), (~bounds).float(), c.gamma, c.lam)
+        boot = None
+        if any(ep.get('boot') is not None for ep in episodes):
+            boot = torch.tensor([float(hl(ep['boot'][None])[0]) if ep.get('boot') is not None else float('nan')
+                                 for ep in episodes])
+        returns = calc_gae(rewards, hl(values), (~bounds).float(), c.gamma, c.lam, boot, lens)
         rs_copy = self.rsnorm.copy()
         self.model.train()
         N = states.shape[0]

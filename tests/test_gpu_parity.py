@@ -798,3 +798,129 @@ def test_ema_schedule_and_model_copy_back_match_oracle():
         tol(agent.flat.flat, online.p, 1e-6, 1e-7)
         copied_back += int(torch.equal(online.p.detach(), ema.ema_model.p.detach()) and ema.initted.item())
     assert agent.ema_step == 40 and lerped >= 10 and copied_back >= 2
+
+
+# ----------------------------------------------------------------------------------------------
+# host environments (xtrl.py:1232-1341): the reference's scalar contract and a vectorised env,
+# 3 / 4 / 5-tuple step returns, truncation with the GAE bootstrap
+# ----------------------------------------------------------------------------------------------
+
+
+class HostLander:
+    """numpy host env, deterministic per episode id (the seed when reset gets one, else the count
+    of resets): N(0,1) states, reward N(0,1) (1 + 0.1 a), termination hazard, truncation at
+    ``limit`` steps (TimeLimit).  ``ret`` = 3: (s, r, terminated); 4: (s, r, terminated, info) with
+    a truthy info on truncation (old gym; the reference reads it as truncated, quirk B8);
+    5: (s, r, terminated, truncated, info), reset -> (s, info)."""
+
+    def __init__(self, S=8, ret=5, hazard=0.08, limit=None, base=1000):
+        self.S, self.ret, self.hazard, self.limit, self.base = S, ret, hazard, limit, base
+        self.count = 0
+
+    def reset(self, seed=None):
+        eid = self.count if seed is None else int(seed)
+        self.count += 1
+        self.rng = np.random.RandomState(self.base + eid)
+        self.t = 0
+        s = self.rng.randn(self.S)
+        return (s, {}) if self.ret == 5 else s
+
+    def step(self, action):
+        a = float(np.sum(action)) if isinstance(action, list) else int(action)
+        self.t += 1
+        s = self.rng.randn(self.S)
+        r = self.rng.randn() * (1 + 0.1 * a)
+        term = bool(self.rng.rand() < self.hazard)
+        trunc = self.limit is not None and self.t >= self.limit
+        if self.ret == 3:
+            return s, r, term
+        if self.ret == 4:
+            return s, r, term, ({'TimeLimit.truncated': True} if trunc else {})
+        return s, r, term, trunc, {}
+
+
+class HostLanderVec:
+    """W HostLander sub-envs behind the batched contract; wave w's sub-env i plays episode id
+    w W + i (the reset count of the scalar env running the same pairs one by one)."""
+
+    def __init__(self, W, **kw):
+        self.num_envs = W
+        self.envs = [HostLander(**kw) for _ in range(W)]
+        self.wave = 0
+
+    def reset(self, seed=None):
+        out = [e.reset(seed=seed[i] if seed is not None else self.wave * self.num_envs + i)
+               for i, e in enumerate(self.envs)]
+        self.wave += 1
+        states = np.stack([o[0] if isinstance(o, tuple) else o for o in out])
+        return (states, {}) if self.envs[0].ret == 5 else states
+
+    def step(self, actions):
+        outs = [e.step(actions[i].tolist() if np.ndim(actions) > 1 else int(actions[i]))
+                for i, e in enumerate(self.envs)]
+        cols = list(zip(*outs))
+        res = [np.stack(cols[0]), np.array(cols[1]), np.array(cols[2])]
+        if len(cols) >= 4:
+            res.append(list(cols[3]) if isinstance(cols[3][0], dict) else np.array(cols[3]))
+        return tuple(res)
+
+
+def _compare_host(learner, oracle, env_gpu, env_cpu, T, seeds=None):
+    traj, lens, genes, cum = learner.rollout_host(env_gpu, 0, T, seeds)
+    torch.cuda.synchronize()
+    episodes, fitness = oracle.rollout_env(env_cpu, 0, T, seeds)
+    compare_rollout(traj, lens, episodes)
+    hl = oracle.model.hl
+    boot = traj['boot'].cpu()
+    for i, ep in enumerate(episodes):
+        if ep['boot'] is None:
+            assert torch.isnan(boot[i]), i
+        else:
+            tol(boot[i], hl(ep['boot'][None])[0], 1e-4, 1e-5)
+    return traj, lens, genes, cum, episodes, fitness
+
+
+@pytest.mark.parametrize('ret,limit', [(3, None), (4, 5), (5, 5), (5, None)])
+def test_host_env_scalar_contract_matches_oracle(ret, limit):
+    """The reference's scalar env (batch 1, pairs one by one) through the device decode: states,
+    actions, log-probs, rewards, is_boundary = terminated, critic logits and lengths as the
+    oracle's reference loop; truncated episodes carry the next state's value (bootstrap)."""
+    learner, _, oracle = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2)
+    _, lens, _, _, episodes, _ = _compare_host(learner, oracle, HostLander(ret=ret, limit=limit),
+                                               HostLander(ret=ret, limit=limit), 9)
+    if limit is not None:
+        assert any(ep['boot'] is not None for ep in episodes)     # some episodes truncated
+
+
+def test_host_env_vectorised_waves_match_oracle():
+    """A vectorised env of 4 sub-envs over 2 genes x 5 episodes (10 pairs: waves of 4, 4, 2 — the
+    last one partial), evolutionary with per-episode reset seeds, truncation at 6 steps."""
+    learner, _, oracle = make_learner(depth=2, gates=True, evo=True, T=8, episodes=5, batch=5)
+    seeds = torch.randint(0, 10 ** 7, (5,), generator=torch.Generator().manual_seed(3))
+    _, _, genes, cum, episodes, fitness = _compare_host(learner, oracle, HostLanderVec(4, limit=6),
+                                                        HostLander(limit=6), 8, seeds)
+    tol(learner.fitness(cum, genes), fitness, 1e-5, 1e-5)
+
+
+def test_host_env_learn_with_truncation_bootstrap_matches_oracle():
+    """One learning update on a truncating host env: GAE reads the bootstrap value at each
+    truncated episode's end (xtrl.py:1323-1336 intent); every minibatch's losses match the
+    oracle's learn at 1e-4."""
+    learner, _, oracle = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2, seed=5)
+    agent = learner.agent
+    traj, lens, genes, cum, episodes, fitness = _compare_host(learner, oracle, HostLander(limit=4),
+                                                              HostLander(limit=4), 9)
+    assert int(torch.isfinite(traj['boot']).sum()) > 0
+    agent.learn(traj, lens, genes, None, update=0)
+    oracle.learn(episodes, fitness, 0)
+    keys = ('loss', 'actor_loss', 'critic_loss', 'autoreg_loss', 'pred_done_loss')
+    ours = np.array([[lg[k] for k in keys] for lg in agent.pop_logs()])
+    theirs = np.array([[lg[k] for k in keys] for lg in oracle.logs])
+    np.testing.assert_allclose(ours, theirs, rtol=1e-4, atol=1e-5)
+
+
+def test_learner_call_runs_batched_vector_env():
+    """train_lander.py's loop (learner(env, n)) on a vectorised env: two updates, finite weights."""
+    learner, _, _ = make_learner(depth=1, gates=False, T=8, episodes=8, batch=4)
+    learner(HostLanderVec(8, ret=5, limit=6), 2)
+    assert learner.agent.step == 2 and torch.isfinite(learner.agent.flat.flat).all()

@@ -232,6 +232,10 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gid / SAMPLE_L, sub = gid % SAMPLE_L;
   if (e >= D.E || !D.alive[e]) return;   // (every lane of the env reads alive before lane 0 clears it)
+  if (D.alive[e] == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
+    if (sub == 0) D.alive[e] = 0;
+    return;
+  }
   const XtrlRngState R = *D.rng;
   if (D.sim_mode >= 0) {
     const uint32_t ep = (uint32_t)D.episode_of_slot[e];
@@ -286,18 +290,23 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
   if (D.sim_mode >= 0) sim_step_env(D, e, t, R);
 }
 
+// host env results of step t (xtrl.py:1297-1336): the memory stores is_boundary = terminated;
+// done = terminated | truncated ends the episode; a truncated (not terminated) episode with
+// `bootstrap` stays for one more decode step (alive = 2) whose critic logits land in the padding
+// slot traj_values[e][t + 1] — the value of the next state the reference computes at :1323-1336.
 __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
-                               const uint8_t* terminated) {
+                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D.E || !D.alive[e]) return;
-  const bool term = terminated[e] != 0;
+  if (e >= D.E || D.alive[e] != 1) return;
+  const bool term = terminated[e] != 0, trunc = truncated && truncated[e] != 0;
   D.traj_rewards[(int64_t)e * D.Tmax + t] = reward[e];
   D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
   D.prev_reward[e] = reward[e];
   D.cum_reward[e] += (double)reward[e];
   D.lens[e] = t + 1;
   for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = next_state[(int64_t)e * D.S + i];
-  if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
+  if (term || t + 1 >= t_limit) D.alive[e] = 0;
+  else if (trunc) D.alive[e] = (bootstrap && t + 1 < D.Tmax) ? 2 : 0;
 }
 
 __global__ void k_rollout_begin(const XtrlDecodeDesc D) {
@@ -419,10 +428,12 @@ int attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
 }
 
 int env_feedback(const XtrlDecodeDesc* D, int t, const float* next_state, const float* reward,
-                 const uint8_t* terminated, hipStream_t s) {
+                 const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
+  XTRL_REQUIRE(next_state && reward && terminated && t >= 0 && t < D->Tmax && t_limit > t && t_limit <= D->Tmax,
+               "env_feedback: bad arguments (t=%d t_limit=%d Tmax=%d)", t, t_limit, D->Tmax);
   hipLaunchKernelGGL(k_env_feedback, dim3((D->E + 255) / 256), dim3(256), 0, s, *D, t, next_state, reward,
-                     terminated);
+                     terminated, truncated, t_limit, bootstrap);
   XTRL_LAUNCHED("env_feedback");
   return XTRL_OK;
 }
@@ -446,8 +457,10 @@ extern "C" int xtrl_attn_decode(const XtrlDecodeDesc* desc, int layer, int t, vo
   return xtrl::attn_decode(desc, layer, t, xtrl::as_stream(stream));
 }
 extern "C" int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state,
-                                         const float* reward, const uint8_t* terminated, void* stream) {
-  return xtrl::env_feedback(desc, t, next_state, reward, terminated, xtrl::as_stream(stream));
+                                         const float* reward, const uint8_t* terminated, const uint8_t* truncated,
+                                         int t_limit, int bootstrap, void* stream) {
+  return xtrl::env_feedback(desc, t, next_state, reward, terminated, truncated, t_limit, bootstrap,
+                            xtrl::as_stream(stream));
 }
 extern "C" int xtrl_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update,
                               const int32_t* episode_of_slot, void* stream) {

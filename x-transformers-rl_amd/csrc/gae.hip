@@ -8,6 +8,8 @@
 // reverse scan gae_t = gate_t * gae_{t+1} + delta_t in sequential order — the same order as the
 // oracle, so the returns are bitwise stable — with FMA contraction disabled so each step rounds
 // like the reference's separate multiply and add.
+// Truncation bootstrap (optional): boot[e] (not NaN) is the value of the state after a truncated
+// episode's last step; it replaces V at index lens[e] (the padding value the scan would read).
 #include "common.h"
 
 namespace xtrl {
@@ -16,7 +18,7 @@ namespace {
 __global__ __launch_bounds__(256) void k_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards,
                                                      const uint8_t* bounds, int64_t ld_seq, const float* centers,
                                                      float* values, float* returns, int n, int B, float gamma,
-                                                     float gamma_lam) {
+                                                     float gamma_lam, const float* boot, const int32_t* lens) {
   extern __shared__ float vs[];   // [n + 1]
   const int e = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int t = w; t < n; t += 4) {
@@ -35,6 +37,12 @@ __global__ __launch_bounds__(256) void k_hlgauss_gae(const float* logits, int64_
     if (lane == 0) vs[t] = sc / s;
   }
   if (threadIdx.x == 0) vs[n] = 0.f;
+  __syncthreads();
+  if (boot && threadIdx.x == 0) {
+    const float bv = boot[e];
+    const int le = lens[e];
+    if (!isnan(bv) && le >= 0 && le <= n) vs[le] = bv;
+  }
   __syncthreads();
   for (int t = threadIdx.x; t < n; t += 256) values[(int64_t)e * n + t] = vs[t];
   if (threadIdx.x != 0) return;
@@ -56,12 +64,13 @@ __global__ __launch_bounds__(256) void k_hlgauss_gae(const float* logits, int64_
 
 int hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, const uint8_t* bounds, int64_t ld_seq,
                 const float* centers, float* values, float* returns, int E, int n, int B, float gamma,
-                float gamma_lam, hipStream_t s) {
+                float gamma_lam, const float* boot, const int32_t* lens, hipStream_t s) {
   XTRL_REQUIRE(logits && rewards && bounds && centers && values && returns, "hlgauss_gae: null operand");
+  XTRL_REQUIRE(!boot || lens, "hlgauss_gae: bootstrap values need the episode lengths");
   XTRL_REQUIRE(E > 0 && n > 0 && B > 0, "hlgauss_gae: bad shape E=%d n=%d B=%d", E, n, B);
   XTRL_REQUIRE((size_t)(n + 1) * 4 <= 160 * 1024, "hlgauss_gae: n=%d too long", n);
   hipLaunchKernelGGL(k_hlgauss_gae, dim3(E), dim3(256), (n + 1) * sizeof(float), s, logits, ld_row, rewards, bounds,
-                     ld_seq, centers, values, returns, n, B, gamma, gamma_lam);
+                     ld_seq, centers, values, returns, n, B, gamma, gamma_lam, boot, lens);
   XTRL_LAUNCHED("hlgauss_gae");
   return XTRL_OK;
 }
@@ -70,7 +79,8 @@ int hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, const
 
 extern "C" int xtrl_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, const uint8_t* bounds,
                                 int64_t ld_seq, const float* centers, float* values, float* returns, int E, int n,
-                                int B, float gamma, float gamma_lam, void* stream) {
+                                int B, float gamma, float gamma_lam, const float* boot, const int32_t* lens,
+                                void* stream) {
   return xtrl::hlgauss_gae(logits, ld_row, rewards, bounds, ld_seq, centers, values, returns, E, n, B, gamma,
-                           gamma_lam, xtrl::as_stream(stream));
+                           gamma_lam, boot, lens, xtrl::as_stream(stream));
 }

@@ -12,6 +12,8 @@ Environments
     (state, reward, terminated[, truncated, ...])``, xtrl.py:1232-1305): episodes are rolled
     out one at a time with batch 1, exactly like the reference loop, the policy step still on
     the device.
+  * a vectorised host env (``num_envs`` sub-envs, batched reset / step): the pairs run in waves
+    of num_envs through the same batched decode (``Learner.rollout_host``).
 
 Randomness protocol (shared with the oracle, see oracle/ref_port.py):
   sampling uniforms  philox(seed; slot, t, update, FIELD_SAMPLE)   slot = global pair index
@@ -87,7 +89,7 @@ class Agent(nn.Module):
                  actor_loss_weight=1., critic_loss_weight=1., autoregressive_loss_weight=1.,
                  # extensions (decision log in DESIGN.md)
                  reward_dropout=0.5, seed=0, rotary_abs_rollout=False, hl_reduction_mean=True, hl_sigma_ratio=2.0,
-                 fused_learn=True, device=None):
+                 fused_learn=True, device=None, truncation_bootstrap=True):
         super().__init__()
         self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
         dev = self.accelerator.device
@@ -166,6 +168,9 @@ class Agent(nn.Module):
         self._deploy = None
         self._genes_dev = None
         self.fused_learn = fused_learn   # False: reference-mode autograd learn step (tests)
+        # host envs: a truncated (not terminated) episode bootstraps GAE from the next state's value
+        # (the intent of xtrl.py:1323-1336, whose bootstrap memory lands outside the episode list)
+        self.truncation_bootstrap = truncation_bootstrap
         self._train_step = None
 
     @property
@@ -287,8 +292,9 @@ class Agent(nn.Module):
         N = lens.shape[0]
         n = int(lens.max().item())
         model = self.model
+        boot = traj.get('boot')     # host envs: truncation-bootstrap values (NaN: none)
         _, returns = ops.hlgauss_gae(traj['values'], traj['rewards'], traj['bounds'], model.hl_centers, n,
-                                     self.gamma, self.lam)
+                                     self.gamma, self.lam, boot, lens if boot is not None else None)
         states = traj['states'][:, :n]
         actions = (traj['actions_f'] if c.continuous else traj['actions'])[:, :n]
         rewards = traj['rewards'][:, :n]
@@ -525,11 +531,23 @@ class Learner(nn.Module):
         traj = eng.run(agent.seed, update, ep, latent, slot_offset=self.slot_offset, slots=self.pair_slots)
         return traj, eng.lens, genes, eng.cum_reward
 
-    # ---- host-env rollout (reference loop, batch 1) -----------------------------------------------
+    # ---- host-env rollout (xtrl.py:1220-1341) ------------------------------------------------------
     def rollout_host(self, env, update, T, episode_seeds=None):
+        """Roll this rank's (episode, gene) pairs out against a host env.  A scalar env (the
+        reference contract) runs the pairs one by one exactly like the reference loop; a vectorised
+        env (``num_envs`` attribute: ``reset(seed=?) -> states [E][S] | (states, ...)``,
+        ``step(actions [E] | [E][A]) -> (states, rewards [E], terminated [E][, truncated [E], ...])``)
+        runs the pairs in waves of num_envs, one batched decode step, one action copy to the host
+        and one env-result copy to the device per timestep (the env's sub-env i takes the wave's
+        i-th pair; sub-envs whose episode ended are still stepped and their results ignored).
+        Semantics as the reference: is_boundary = terminated; done = terminated | truncated; a
+        4-tuple's 4th item is read as truncated (quirk B8); a truncated, not terminated episode
+        bootstraps GAE from the next state's value (xtrl.py:1323-1336; ``truncation_bootstrap``)."""
         agent = self.agent
         c = agent.cfg
-        eng = self._engine_for_host(T)
+        vector = getattr(env, 'num_envs', None) is not None
+        W = int(env.num_envs) if vector else 1
+        eng = self._engine_for_host(W, T)
         eng.pack(agent.ema_model, agent.rs_mean, agent.rs_var)
         pairs = self.episode_genes_for_process
         N, dev = len(pairs), self.device
@@ -539,49 +557,47 @@ class Learner(nn.Module):
                    logp=torch.zeros(N, T, A, device=dev) if c.continuous else torch.zeros(N, T, device=dev),
                    rewards=torch.zeros(N, T, device=dev), bounds=torch.zeros(N, T, dtype=torch.uint8, device=dev),
                    values=torch.zeros(N, T, B, device=dev))
+        boot = torch.full((N,), float('nan'), device=dev)
         lens = torch.zeros(N, dtype=torch.int32)
         cum = torch.zeros(N, dtype=torch.float64)
         genes = torch.tensor([g for _, g in pairs], dtype=torch.long, device=dev)
-
-        def reset(kw):
-            r = env.reset(**kw)
-            return r[0] if isinstance(r, tuple) else r
-
-        def step(action):
-            o = env.step(action.tolist() if hasattr(action, 'tolist') else action)
-            if len(o) >= 4:
-                ns, r, term, trunc = o[:4]
-            elif len(o) == 3:
-                ns, r, term = o
-                trunc = False
-            else:
-                raise RuntimeError('invalid number of returns from environment .step')
-            return ns, float(np.asarray(r).reshape(-1)[0]), bool(term or trunc)
-
-        for i, (episode, gene) in enumerate(pairs):
-            kw = {}
+        for w0 in range(0, N, W):
+            wave = pairs[w0:w0 + W]
+            rows = len(wave)
+            seeds = None
             if agent.evolutionary and episode_seeds is not None:
-                kw = dict(seed=int(episode_seeds[episode]))
-            latent = agent.latent(torch.tensor([gene], device=dev)) if agent.evolutionary else None
-            traj, n_steps, total = eng.run_host_env(lambda: reset(kw), step, agent.seed, update, latent,
-                                                    slot_offset=self._slot(i), max_steps=T)
+                seeds = [int(episode_seeds[e]) for e, _ in wave]
+            reset, step = (_vector_env_fns if vector else _scalar_env_fns)(env, W, seeds, c.continuous)
+            latent = None
+            if agent.evolutionary:
+                latent = agent.latent(torch.tensor([g for _, g in wave] + [0] * (W - rows), device=dev))
+            slots = [self._slot(w0 + i) for i in range(rows)] + [0] * (W - rows)
+            traj, wl, wt, wb = eng.run_host_wave(reset, step, agent.seed, update, rows, latent, slots, T,
+                                                 bootstrap=agent.truncation_bootstrap)
             for k, v in traj.items():
                 if v is not None:
-                    out[k][i].copy_(v[0])
-            lens[i] = n_steps
-            cum[i] = total
+                    out[k][w0:w0 + rows].copy_(v[:rows, :T])
+            lens[w0:w0 + rows] = torch.from_numpy(wl[:rows])
+            cum[w0:w0 + rows] = torch.from_numpy(wt[:rows])
+            for i in map(int, wb[:rows].nonzero()[0]):
+                n = int(wl[i])      # the bootstrap step wrote the next state and its logits at index n
+                boot[w0 + i] = agent.model.hl_value(traj['values'][i, n])
+                if n < T:
+                    out['values'][w0 + i, n].zero_()
+                    out['states'][w0 + i, n].zero_()
+        out['boot'] = boot
         return out, lens.to(dev), genes, cum
+
+    def _engine_for_host(self, W, T):
+        key = ('host', W, T)
+        if self._engine is None or self._engine[0] != key:
+            eng = RolloutEngine(self.agent.model, W, T + 1, sim_mode=SIM_HOST, clamp=self.continuous_actions_clamp)
+            self._engine = (key, eng)
+        return self._engine[1]
 
     def _slot(self, i):
         """Global (episode, gene) pair index of this rank's i-th pair (keys its sampling stream)."""
         return self.pair_slots[i] if self.pair_slots is not None else self.slot_offset + i
-
-    def _engine_for_host(self, T):
-        key = ('host', T)
-        if self._engine is None or self._engine[0] != key:
-            eng = RolloutEngine(self.agent.model, 1, T, sim_mode=SIM_HOST, clamp=self.continuous_actions_clamp)
-            self._engine = (key, eng)
-        return self._engine[1]
 
     # ---- fitness per gene in pair order (xtrl.py:1345-1346, 1362) -------------------------------------
     def fitness(self, cum_reward, genes):
@@ -618,3 +634,57 @@ class Learner(nn.Module):
             if update % self.save_every == 0:
                 agent.save()
         agent.save()
+
+
+# ----------------------------------------------------------------------------------------------
+# host env contracts (xtrl.py:1232-1305) as batched reset / step closures for run_host_wave
+# ----------------------------------------------------------------------------------------------
+
+
+def _parse_step(o):
+    """(next_state, reward, terminated, truncated) of one step return (xtrl.py:1299-1305)."""
+    if len(o) >= 4:
+        return o[0], o[1], o[2], o[3]
+    if len(o) == 3:
+        return o[0], o[1], o[2], False
+    raise RuntimeError('invalid number of returns from environment .step')
+
+
+def _scalar_env_fns(env, W, seeds, continuous):
+    """The reference's scalar contract: reset(**{seed}) -> state | (state, ...); step(action.tolist())."""
+    assert W == 1
+    kw = dict(seed=seeds[0]) if seeds is not None else {}
+
+    def reset():
+        r = env.reset(**kw)
+        return np.asarray(r[0] if isinstance(r, tuple) else r, dtype=np.float32)[None]
+
+    def step(actions, live):
+        a = actions[0].tolist() if continuous else int(actions[0])
+        ns, r, term, trunc = _parse_step(env.step(a))
+        return (np.asarray(ns, dtype=np.float32)[None], np.asarray(r, dtype=np.float64).reshape(-1)[:1],
+                np.array([bool(term)]), np.array([bool(trunc)]))
+    return reset, step
+
+
+def _vector_env_fns(env, W, seeds, continuous):
+    """A vectorised env of W sub-envs: reset(seed=[...]) / step(actions [W] or [W][A])."""
+    def flags(x):
+        if isinstance(x, dict):                   # a 4-tuple's info read as truncated (quirk B8)
+            return np.full(W, bool(x))
+        if isinstance(x, (list, tuple)) and x and isinstance(x[0], dict):
+            return np.array([bool(i) for i in x])
+        return np.broadcast_to(np.asarray(x).astype(bool), (W,))
+
+    def reset():
+        kw = {}
+        if seeds is not None:
+            kw = dict(seed=list(seeds) + [0] * (W - len(seeds)))
+        r = env.reset(**kw)
+        return np.asarray(r[0] if isinstance(r, tuple) else r, dtype=np.float32).reshape(W, -1)
+
+    def step(actions, live):
+        ns, r, term, trunc = _parse_step(env.step(actions.copy()))
+        return (np.asarray(ns, dtype=np.float32).reshape(W, -1), np.asarray(r, dtype=np.float64).reshape(W),
+                flags(term), flags(trunc))
+    return reset, step

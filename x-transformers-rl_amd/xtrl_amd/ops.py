@@ -224,16 +224,21 @@ def fused_loss(raw_actions, values, pred_raw, done_logit, consts: LossConsts):
 # --------------------------------------------------------------------------------------------
 
 
-def hlgauss_gae(logits, rewards, bounds, centers, n, gamma, lam):
-    """logits [E, T, B] (uses [:, :n]), rewards / bounds [E, T] -> (values, returns) [E, n]."""
+def hlgauss_gae(logits, rewards, bounds, centers, n, gamma, lam, boot=None, lens=None):
+    """logits [E, T, B] (uses [:, :n]), rewards / bounds [E, T] -> (values, returns) [E, n].
+    ``boot`` [E] (NaN = none) with ``lens`` [E] int32: truncation-bootstrap values at index lens."""
     lib = L.lib()
     E, T, B = logits.shape
     assert rewards.shape == (E, T) and bounds.shape == (E, T) and bounds.dtype == torch.uint8 and n <= T
+    if boot is not None:
+        assert boot.shape == (E,) and boot.dtype == torch.float32 and boot.is_contiguous()
+        assert lens is not None and lens.shape == (E,) and lens.dtype == torch.int32 and lens.is_contiguous()
     values = torch.empty(E, n, device=logits.device, dtype=torch.float32)
     returns = torch.empty_like(values)
     gl = float(torch.tensor(gamma * lam, dtype=torch.float32))
     L.check(lib.xtrl_hlgauss_gae(L.ptr(logits), T * B, L.ptr(rewards), L.ptr(bounds), T, L.ptr(centers),
-                                 L.ptr(values), L.ptr(returns), E, n, B, float(gamma), gl, L.stream()), 'hlgauss_gae')
+                                 L.ptr(values), L.ptr(returns), E, n, B, float(gamma), gl, L.ptr(boot),
+                                 L.ptr(lens if boot is not None else None), L.stream()), 'hlgauss_gae')
     return values, returns
 
 

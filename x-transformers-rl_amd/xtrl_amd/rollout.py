@@ -248,29 +248,73 @@ class RolloutEngine:
         return self.traj
 
     @torch.no_grad()
-    def run_host_env(self, env_reset, env_step, seed, update, latent=None, slot_offset=0, max_steps=None):
-        """E == 1 rollout against a host (numpy) env: the reference's scalar Sim contract."""
-        assert self.sim_mode == SIM_HOST and self.E == 1
-        state0 = env_reset()
-        self.state.copy_(torch.as_tensor(state0, dtype=torch.float32).reshape(1, -1))
-        self._begin(seed, update, slot_offset, torch.zeros(1, dtype=torch.int32), latent)
+    def run_host_wave(self, env_reset, env_step, seed, update, rows, latent=None, slots=None, max_steps=None,
+                      bootstrap=True):
+        """One wave of a host-env rollout (xtrl.py:1232-1341) over this engine's E rows, the first
+        ``rows`` of them live (a partial last wave leaves the rest dead).  ``env_reset() -> [E][S]``,
+        ``env_step(actions, live) -> (next_state [E][S], reward [E], terminated [E], truncated [E])``
+        as numpy (``actions``: int [E] or float [E][A]; ``live``: bool [E] mask of rows whose
+        episode is running).  Per step one device->host copy of the actions and one host->device
+        copy of the env results.  The engine holds Tmax = max_timesteps + 1 positions so a
+        truncation at the last step can still take its bootstrap decode step.
+        Returns (traj, lens [E] host int, totals [E] host float64, boot_rows)."""
+        assert self.sim_mode == SIM_HOST
+        import numpy as np
+        E, S, A = self.E, self.c.state_dim, self.c.num_actions
+        T = min(self.T - 1, max_steps or self.T - 1)
+        if getattr(self, '_host_stage', None) is None:
+            self._host_stage = torch.empty(E * (S + 1) + 2 * E, dtype=torch.float32, pin_memory=True)
+            self._host_act = torch.empty(E * (A if self.c.continuous else 1),
+                                         dtype=torch.float32 if self.c.continuous else torch.int32, pin_memory=True)
+            self._dev_stage = torch.empty(E * (S + 1) + 2 * E, dtype=torch.float32, device=self.dev)
+        st, dst = self._host_stage, self._dev_stage
+        state0 = np.asarray(env_reset(), dtype=np.float32).reshape(E, S)
+        self.state.copy_(torch.from_numpy(state0))
+        eps = torch.arange(E, dtype=torch.int32)
+        self._begin(seed, update, 0, eps, latent, slots)
+        live = np.arange(E) < rows
+        if rows < E:
+            self.alive[rows:].zero_()
+        boot_rows = np.zeros(E, dtype=bool)
+        lens = np.zeros(E, dtype=np.int64)
+        totals = np.zeros(E, dtype=np.float64)
         lib = L.lib()
-        T = min(self.T, max_steps or self.T)
-        total = 0.
-        t = 0
-        for t in range(T):
-            self.step(t)
-            if self.c.continuous:
-                action = self.prev_action_f[0].cpu().numpy()
-            else:
-                action = int(self.prev_action[0].item())
-            next_state, reward, terminated = env_step(action)
-            total += float(reward)
-            ns = torch.as_tensor(next_state, dtype=torch.float32, device=self.dev).reshape(1, -1)
-            rw = torch.tensor([float(reward)], dtype=torch.float32, device=self.dev)
-            tm = torch.tensor([1 if terminated else 0], dtype=torch.uint8, device=self.dev)
-            L.check(lib.xtrl_rollout_env_feedback(C.byref(self.desc), t, L.ptr(ns), L.ptr(rw), L.ptr(tm), L.stream()),
-                    'env_feedback')
-            if terminated:
+        src = self.prev_action_f if self.c.continuous else self.prev_action
+        st_state = st[:E * S].view(E, S).numpy()
+        st_rew, st_flags = st[E * S:E * (S + 1)].numpy(), st[E * (S + 1):].view(torch.uint8)
+        ns_d, rw_d = dst[:E * S], dst[E * S:E * (S + 1)]
+        fl_d = dst[E * (S + 1):].view(torch.uint8)
+        pending = np.zeros(E, dtype=bool)    # rows taking their bootstrap decode step
+        for t in range(T + 1):
+            if not live.any() and not pending.any():
                 break
-        return self.traj, t + 1, total
+            self.step(t)
+            pending[:] = False
+            if not live.any():
+                break
+            self._host_act.copy_(src.reshape(-1), non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            act = self._host_act.numpy().reshape(E, A) if self.c.continuous else self._host_act.numpy()
+            ns, r, term, trunc = env_step(act, live.copy())
+            ns = np.asarray(ns, dtype=np.float32).reshape(E, S)
+            r = np.asarray(r, dtype=np.float64).reshape(E)
+            term = np.asarray(term).reshape(E).astype(bool)
+            trunc = np.asarray(trunc).reshape(E).astype(bool)
+            totals[live] += r[live]
+            lens[live] = t + 1
+            st_state[:] = ns
+            st_rew[:] = r.astype(np.float32)
+            flags = st_flags.numpy()
+            flags[:E] = term
+            flags[E:2 * E] = trunc
+            dst.copy_(st, non_blocking=True)
+            L.check(lib.xtrl_rollout_env_feedback(C.byref(self.desc), t, L.ptr(ns_d), L.ptr(rw_d), L.ptr(fl_d[:E]),
+                                                  L.ptr(fl_d[E:2 * E]), T, int(bootstrap), L.stream()),
+                    'env_feedback')
+            ended = live & (term | trunc | (t + 1 >= T))
+            boot_now = live & trunc & ~term & (t + 1 < T) & bool(bootstrap)
+            boot_rows |= boot_now
+            pending = boot_now
+            live = live & ~ended
+        torch.cuda.current_stream().synchronize()   # the pinned staging buffer is reused next wave
+        return self.traj, lens, totals, boot_rows
