@@ -164,6 +164,8 @@ class WgradGemmTimer:
 
     def collect(self):
         torch.cuda.synchronize()
+        if self.n.value >= self.cap:
+            raise RuntimeError(f'WgradGemmTimer: {self.cap} event pairs filled, launches went unrecorded')
         for i in range(self.n.value):
             self.ms += self.events[2 * i].elapsed_time(self.events[2 * i + 1])
             self.total_flops += self.flops[i]
@@ -190,6 +192,24 @@ def pmc_traffic(*kernels):
     return round(sum(h['traffic'] * h['dispatches'] for h in hits) / n) if n else None
 
 
+def rocprof_avg_us(*kernels):
+    """Average duration (us, call-weighted) of the kernels whose names contain one of ``kernels``
+    in the newest committed `rocprofv3 --kernel-trace --stats` summary of this bench
+    (profiles/rNN_kernel_stats.csv) — the profiler's clock beside the bench's HIP events."""
+    import csv
+    import glob
+    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_kernel_stats.csv')))
+    if not files:
+        return None
+    calls = total = 0
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if any(k in row['Name'] for k in kernels):
+                calls += int(row['Calls'])
+                total += float(row['TotalDurationNs'])
+    return round(total / calls / 1e3, 2) if calls else None
+
+
 def pmc_mfma_busy(*kernels):
     """Matrix-core busy fraction of the kernels (dispatch-weighted mean of SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), the third PMC pass of tools/gpu_check.sh pmc), or None."""
@@ -203,13 +223,27 @@ def pmc_mfma_busy(*kernels):
     return round(sum(h['mfma_busy'] * h['dispatches'] for h in hits) / n, 4) if n else None
 
 
-def cpu_baseline(cfg, seed, budget_s):
+def host_cores():
+    """Physical cores of this host (psutil), and the CPU share this process may use (affinity)."""
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:
+        phys = None
+    try:
+        share = len(os.sched_getaffinity(0))
+    except Exception:
+        share = os.cpu_count()
+    return phys, share
+
+
+def cpu_baseline(cfg, seed, budget_s, threads=None, episodes=None):
     """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn), one
     update on a bounded number of episodes of the same workload."""
     from oracle import ref_port as R
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
+    threads = threads or int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    episodes = 96 if cfg['T'] >= 100 else 512
+    episodes = episodes or (96 if cfg['T'] >= 100 else 512)
     batch = min(8, episodes)
     c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
                         dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],
@@ -271,7 +305,7 @@ def ppo_loss_delta(learner, env, cfg):
         ref, _, _, _ = R.minibatch_loss(model, rs, mb, latent, R.LossWeights(agent.actor_loss_weight,
                                                                             agent.critic_loss_weight,
                                                                             agent.autoregressive_loss_weight), keep)
-        out.update(gpu=float(loss), cpu=float(ref))
+        out.update(gpu=float(loss.detach()), cpu=float(ref.detach()))
 
     agent.learn(traj, lens, genes, learner.fitness(cum, genes), update=u, probe=probe)
     agent.logs = []
@@ -316,11 +350,17 @@ def main():
     for _ in range(args.warmup):
         one_update(learner, env, T)
     timer = None if args.no_roofline else DecodeAttnTimer(learner, env, T)
+    gtimer = None
     if timer is not None:
-        one_update(learner, env, T)        # capture the graph with the event records inside (untimed)
+        # untimed: capture the rollout graph with the event records inside, and count the
+        # weight-gradient launches of one update to size the timed region's event pool exactly
+        probe_timer = WgradGemmTimer(learner.agent, cap=1 << 14)
+        probe_timer.attach()
+        one_update(learner, env, T)
+        per_update = probe_timer.n.value
+        probe_timer.detach()
         timer.ms, timer.launches, timer.bytes = 0.0, 0, 0.0
-    gtimer = None if args.no_roofline else WgradGemmTimer(learner.agent)
-    if gtimer is not None:
+        gtimer = WgradGemmTimer(learner.agent, cap=per_update * args.steps + 64)
         gtimer.attach()
     if world > 1:
         dist.barrier()
@@ -367,6 +407,7 @@ def main():
                             peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
                             traffic=pmc_traffic(*WgradGemmTimer.KERNELS),
                             mfma_busy=pmc_mfma_busy(*WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
+                            avg_launch_us_rocprof=rocprof_avg_us(*WgradGemmTimer.KERNELS),
                             flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
@@ -375,6 +416,11 @@ def main():
                              achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                              frac=round(achieved / HBM_PEAK_GBS, 4), traffic=pmc_traffic('k_attn_decode'),
                              avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=round(timer.bytes / timer.launches))
+        # the profiler's per-launch time (no event records around the launch) and the fraction it gives
+        us = rocprof_avg_us('k_attn_decode')
+        if us:
+            attn_roofline.update(avg_launch_us_rocprof=us, frac_rocprof=round(
+                timer.bytes / timer.launches / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))
         timer.detach()
 
     loss_delta = None
@@ -389,6 +435,10 @@ def main():
             loss_delta = dict(error=repr(e))
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, args.seed, 20.)
+            phys, share = host_cores()
+            one = cpu_baseline(cfg, args.seed, 20., threads=1, episodes=32 if cfg['T'] >= 100 else 128)
+            cpu.update(host_physical_cores=phys, host_cpu_share=share,
+                       single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
         line = dict(metric='env-steps/s (rollout+update)', value=round(value, 1), unit='env-steps/s', n_gpus=world,
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),

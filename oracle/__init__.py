@@ -23,6 +23,5 @@ Modules
                  this container (tests/golden/make_golden.py; tests/test_oracle_golden.py).
   philox.py      counter-based Philox4x32-10 streams + the synthetic LunarLander-shaped Sim,
                  bit-identical to the HIP implementation (integer arithmetic + exact f32 adds).
-  gae_ref.c      plain-C restatement of HL-Gauss value decode + calc_gae (xtrl.py:616-640)
-                 used to cross-check the numpy/torch version and as a scalar CPU timing point.
+  fractal_ref.py fp64-capable restatement of the fractal policy body forward (fractal_rl.py).
 """
