@@ -97,7 +97,7 @@ def one_update(learner, env, T, probe=None, phases=False):
 
 class DecodeAttnTimer:
     """HIP events around every attention-decode launch of the timed region (XtrlDecodeDesc.prof_events),
-    on env group 0's stream (the decode chains of the other groups run concurrently)."""
+    on the rollout stream."""
 
     def __init__(self, learner, env, T):
         import ctypes as C
@@ -119,7 +119,7 @@ class DecodeAttnTimer:
         self.launches += self.T * self.L
         c = self.eng.c
         H, dh = c.heads, c.dim_head
-        lens = lens.cpu().numpy()[:self.eng.E // self.eng.groups]   # the events time env group 0's launches
+        lens = lens.cpu().numpy()
         t = np.arange(self.T)
         alive = (lens[None, :] > t[:, None]).sum(1)                  # live episodes at step t
         # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + q|k|v|gate|mix row (4 dh + 1)

@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 5
+#define XTRL_ABI_VERSION 6
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -75,6 +75,8 @@ int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, in
  * ------------------------------------------------------------------------------------------- */
 typedef struct XtrlDecodeLayer {
   const float* ln_attn;  /* [d]  pre-attention LayerNorm gamma */
+  /* decode GEMM weights (w_qkv, w_out, w_ff1, w_ff2, w_h1, w_h2) are fragment-packed (xtrl_dgemm_pack)
+   * images of the nn.Linear weights described */
   const float* w_qkv;    /* [n_qkv][d]  rows: to_q | to_k | to_v | to_v_gate (opt) | value-residual mix (opt) */
   const float* b_qkv;    /* [n_qkv]     zeros for q/k/v */
   const float* w_out;    /* [d][I]      to_out */
@@ -112,8 +114,9 @@ typedef struct XtrlDecodeDesc {
   const float* w_se; const float* b_se;             /* to_state_embed [d][S], [d] */
   const float* ln_final;                            /* [d] */
   const float* w_h1; const float* b_h1;             /* [4d][in_dim]: action_head.0 rows then critic_head.0 rows */
-  const float* w_a2; const float* b_a2;             /* action_head.2 [A or 2A][2d] */
-  const float* w_c2; const float* b_c2;             /* critic_head.2 [B][2d] */
+  const float* w_h2; const float* b_h2;             /* [n_act + B][4d] block diagonal: action_head.2 [n_act][2d] over
+                                                       the actor half of the hidden row, critic_head.2 [B][2d] over the
+                                                       critic half (n_act = A or 2A); bias [n_act + B] */
   const float* inv_freq;                            /* [rot_dim/2] rotary inverse frequencies */
   const XtrlDecodeLayer* layers;                    /* HOST array of L layer descriptors */
   const float* rs_mean; const float* rs_var;        /* RSNorm running stats [S+1] */
@@ -138,6 +141,7 @@ typedef struct XtrlDecodeDesc {
   uint8_t* traj_bounds;    /* [E][Tmax] terminated flags */
   float* traj_values;      /* [E][Tmax][B] critic logits */
   /* scratch (device) */
+  /* (per-step activations are indexed by live row, not by episode slot) */
   float* x;      /* [E][d] residual stream */
   float* qkv;    /* [E][n_qkv] */
   float* att;    /* [E][I] */
@@ -145,8 +149,11 @@ typedef struct XtrlDecodeDesc {
   float* ac_in;  /* [E][in_dim]  (final-normed embed | state embed | latent embed) */
   float* logits; /* [E][A or 2A] */
   float* v1;     /* [E][I] first layer's values (value residual) */
-  float* vals;   /* [E][B] critic logits of the current step (copied to traj_values for live episodes) */
-  float* xn;     /* [E][d] layer-normalised residual stream (input of the q|k|v and FF1 projections) */
+  /* live-row compaction: the step-t kernels run over rows 0..live_count[t & 1]-1 only; row r is
+   * episode slot live_rows[(t & 1) * E + r] (written by the step's embedding kernel) */
+  int32_t* live_rows;        /* [2][E] */
+  int32_t* live_count;       /* [2] */
+  const float* lat_embed;    /* [E][d] latent_to_embed(gene) per episode slot (evolutionary) or NULL */
   /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
    * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
   void** prof_events;
@@ -167,9 +174,22 @@ int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* ne
                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap,
                               void* stream);
 
-/* Attention for one decode step (exposed for tests): reads q|k|v|gate|mix rows, applies value
- * residual + rotary, appends k/v at position t and attends over positions 0..t. */
-int xtrl_attn_decode(const XtrlDecodeDesc* desc, int layer, int t, void* stream);
+/* Decode-step projection (the rollout's GEMM):
+ *   C[dst(m), n] = act( LN?(A)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])   for m < (m_dev ? *m_dev : M)
+ * W an nn.Linear weight [N][K] (xtrl.py's Linear layers, x-transformers projections) in the
+ * fragment-packed layout of xtrl_dgemm_pack; ln_gamma != NULL applies the x-transformers LayerNorm
+ * (no affine, eps 1e-5, times gamma) to A's columns [0, ln_k) first (Decoder pre-norms / final
+ * norm, ln_k <= 512); dst(m) = row_map ? row_map[m] : m; act 0 / 1 GELU / 2 SiLU.  K, lda
+ * multiples of 4, A 16-byte aligned. */
+int xtrl_dgemm(const float* A, int lda, const float* Wp, const float* bias, const float* ln_gamma, int ln_k,
+               const float* R, int ldr, float* C, int ldc, const int32_t* row_map, const int32_t* m_dev, int M, int N,
+               int K, int act, void* stream);
+/* Fragment packing of W [N][K] (row stride ldw) into Wp (xtrl_dgemm_packed_floats(N, K) floats):
+ * float4 slot ((n / 16 * JN + j) * 4 + q) * 16 + n % 16 holds W[n][q Kp/4 + 4 j .. + 3], Kp = K
+ * rounded up to 16, JN = Kp / 16, zero-padded past N and K — each MFMA fragment load of the
+ * decode GEMM reads 1 KiB contiguous.  Done once per rollout (the EMA weights are fixed for it). */
+int64_t xtrl_dgemm_packed_floats(int N, int K);
+int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * HL-Gauss value decode + GAE   (xtrl.py:843-852 -> calc_gae :616-640, HLGaussLoss value)

@@ -59,6 +59,66 @@ def test_gemm_f32(M, N, K, mode):
     tol(out, ref, 1e-5, 1e-5)
 
 
+@pytest.mark.parametrize('M,N,K,live', [(1, 5, 8, 1), (37, 260, 256, 30), (1024, 1024, 256, 1024), (1024, 256, 1024, 700),
+                                        (300, 256, 64, 300), (130, 100, 512, 77), (64, 1024, 768, 50), (40, 48, 48, 40),
+                                        (33, 192, 96, 33), (1000, 512, 384, 999)])
+@pytest.mark.parametrize('mode', ['plain', 'ln_gelu', 'ln_silu_part', 'residual', 'scatter'])
+def test_dgemm_decode_projection(M, N, K, live, mode):
+    """xtrl_dgemm (the rollout's projections over compacted live rows) vs an fp64 torch reference:
+    LayerNorm prologue over the first ln_k columns, GELU / SiLU, residual, row scatter, and the
+    device live-row count (rows >= live are not written)."""
+    import ctypes as C
+    from xtrl_amd import _lib as L
+    g = torch.Generator(device='cpu').manual_seed(M * 3 + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV) + 0.5
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    gam = (torch.rand(K, generator=g) + 0.5).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    m_dev = torch.tensor([live], dtype=torch.int32, device=DEV)
+    xd, wd, bd = x.double(), w.double(), b.double()
+    ln_k = min(K, 512) if mode == 'ln_gelu' else (K // 2 if mode == 'ln_silu_part' else 0)   # (ln_k <= 512)
+    ln_k -= ln_k % 4
+    if ln_k:
+        xd = xd.clone()
+        xd[:, :ln_k] = torch.nn.functional.layer_norm(xd[:, :ln_k], (ln_k,), eps=1e-5) * gam[:ln_k].double()
+    ref = xd @ wd.T + bd
+    if mode == 'ln_gelu':
+        ref = torch.nn.functional.gelu(ref)
+    elif mode == 'ln_silu_part':
+        ref = torch.nn.functional.silu(ref)
+    elif mode == 'residual':
+        ref = ref + res.double()
+    act = {'ln_gelu': 1, 'ln_silu_part': 2}.get(mode, 0)
+    sentinel = -7.0
+    rows_out = M + 5 if mode == 'scatter' else M
+    out = torch.full((rows_out, N), sentinel, device=DEV)
+    row_map = None
+    if mode == 'scatter':
+        row_map = torch.randperm(rows_out, generator=g)[:M].to(torch.int32).to(DEV)
+    if mode == 'residual':
+        out[:M] = res
+    wp = torch.empty(L.lib().xtrl_dgemm_packed_floats(N, K), device=DEV)
+    L.check(L.lib().xtrl_dgemm_pack(L.ptr(w), K, N, K, L.ptr(wp), L.stream()), 'dgemm_pack')
+    rc = L.lib().xtrl_dgemm(L.ptr(x), K, L.ptr(wp), L.ptr(b), L.ptr(gam) if ln_k else None, ln_k,
+                            L.ptr(out) if mode == 'residual' else None, N, L.ptr(out), N,
+                            L.ptr(row_map) if row_map is not None else None, L.ptr(m_dev), M, N, K, act, L.stream())
+    L.check(rc, 'dgemm')
+    torch.cuda.synchronize()
+    if mode == 'scatter':
+        got = out[row_map[:live].long()]
+        untouched = torch.ones(rows_out, dtype=torch.bool, device=DEV)
+        untouched[row_map[:live].long()] = False
+        assert bool((out[untouched] == sentinel).all())
+    else:
+        got = out[:live]
+        if mode != 'residual':
+            assert bool((out[live:] == sentinel).all())
+        else:
+            assert torch.equal(out[live:], res[live:])
+    tol(got, ref[:live], 2e-5, 2e-5)
+
+
 def _dot_scale(a, b):
     """sum_k |a[m, k] b[k, n]| (the scale of an fp32 dot product's rounding error)."""
     return a.abs() @ b.abs()

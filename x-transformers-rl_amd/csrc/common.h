@@ -53,6 +53,32 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// DPP forms for latency-bound kernels: four intra-row steps as DPP moves (quad xor 1, xor 2, half-row
+// mirror, row mirror — after the quad steps every lane of a quad holds the same value, so the
+// mirrors pair whole groups), then two cross-row shuffles.  A different association from wave_sum.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  v += __shfl_xor(v, 16, kWave);
+  v += __shfl_xor(v, 32, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  v = fmaxf(v, __shfl_xor(v, 16, kWave));
+  v = fmaxf(v, __shfl_xor(v, 32, kWave));
+  return v;
+}
+
 // 4 x 4 transpose across the four lanes of a quad (lanes with equal lane >> 2): on entry lane
 // c = lane & 3 holds column c of the block (x[q] = element (q, c)), on exit its row c
 // (x[k] = element (c, k)).  Two exchange stages: lane ^ 2 swaps the off-diagonal 2 x 2 blocks,

@@ -1,25 +1,32 @@
 // Rollout: one policy timestep for E concurrent episodes, entirely on device.
 //
 // Replaces the batch-1, host-synchronised body of the reference rollout loop
-// (x_transformers_rl.py:1250-1341) with a vectorised step:
+// (x_transformers_rl.py:1250-1341) with a vectorised step over the LIVE episodes only:
 //
-//   k_embed        RSNorm eval of [state, prev_reward] (xtrl.py:1254-1259, 591), project_in +
-//                  action embedding + reward embedding (xtrl.py:492-503), to_state_embed;
-//                  writes the raw state into the trajectory (Memory.state, xtrl.py:1315)
-//   per layer      LN -> [q|k|v|gate|mix] GEMM (gemm.hip)
+//   k_compact      lists the live episodes (alive != 0) in slot order: row r of every per-step
+//                  buffer is episode slot live_rows[t & 1][r], r < live_count[t & 1]
+//   k_embed        RSNorm eval of [state, prev_reward]
+//                  (xtrl.py:1254-1259, 591), project_in + action embedding + reward embedding
+//                  (xtrl.py:492-503), to_state_embed, latent embedding; writes the raw state into
+//                  the trajectory (Memory.state, xtrl.py:1315)
+//   per layer      [LN -> q|k|v|gate|mix] dgemm (LayerNorm in the GEMM prologue)
 //                  k_attn_decode: value-residual mix, rotary, KV append at t, softmax(q k^T) v
 //                  over positions 0..t, value gate        (x-transformers Attention, cached)
-//                  out-proj GEMM + residual, LN -> FF1 GELU GEMM, FF2 GEMM + residual
-//   final LN       into ac_in[:, 0:d]; heads: [actor|critic] hidden GEMM (SiLU), logits GEMMs
-//                  (critic logits straight into traj_values[:, t, :] of live envs)
-//   k_sample       softmax -> Categorical -> inverse-CDF sample on Philox uniforms, log_prob
-//                  (xtrl.py:1280-1289; torch Categorical(probs) semantics), then the synthetic
-//                  LunarLander-shaped Sim step (philox.h): reward, termination, next state, alive
-//                  mask, episode length, cumulative reward (xtrl.py:1297-1351)
+//                  out-proj dgemm + residual, [LN -> FF1 GELU] dgemm, FF2 dgemm + residual
+//                  (the last layer's FF2 writes the final-norm input straight into ac_in[:, 0:d])
+//   heads          [final LN -> actor|critic hidden SiLU] dgemm; the last Linear layers as one
+//                  block-diagonal dgemm: actor logits to the row buffer, critic logits straight
+//                  into traj_values[slot][t] (row scatter)
+//   k_sample       softmax -> Categorical ->
+//                  inverse-CDF sample on Philox uniforms, log_prob (xtrl.py:1280-1289; torch
+//                  Categorical(probs) semantics), then the synthetic LunarLander-shaped Sim step
+//                  (philox.h): reward, termination, next state, alive mask, episode length,
+//                  cumulative reward (xtrl.py:1297-1351)
+// 5 L + 5 launches per step (C3: 25; round 1: 33), and terminated episodes cost nothing.
 //
-// Layouts in HBM: activations are [E][·] row-major; KV caches [E][H][Tmax][dh] so one (env, head)
-// streams a contiguous Tmax*dh block; trajectories [E][Tmax][·] so the learner reads whole
-// episodes contiguously.
+// Layouts in HBM: per-step activations are [live row][.] row-major; KV caches [E][H][Tmax][dh]
+// (per episode slot) so one (episode, head) streams a contiguous Tmax*dh block; trajectories
+// [E][Tmax][.] so the learner reads whole episodes contiguously.
 #include "kernels.h"
 #include "philox.h"
 
@@ -29,105 +36,214 @@ namespace {
 
 constexpr float F32_EPS = 1.1920928955078125e-07f;
 
+__device__ __forceinline__ float f4c(const float4& v, int k) {
+  return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+__device__ __forceinline__ const int32_t* rows_of(const XtrlDecodeDesc& D, int t) { return D.live_rows + (t & 1) * D.E; }
+
 // ---------------------------------------------------------------------------------------------
-// embeddings (one wave per env)
+// live-row compaction: one workgroup lists the episode slots with alive != 0 in slot order
+// (live_rows[t & 1][0 .. n-1], live_count[t & 1] = n) — deterministic, one launch
 // ---------------------------------------------------------------------------------------------
-// ln_gamma != NULL (d <= 256): the row is also layer-normalised into xn with the first layer's
-// pre-norm gamma, in k_layernorm's order of operations (bit-identical; one launch less per step)
-__global__ __launch_bounds__(256) void k_embed(const XtrlDecodeDesc D, int t, const float* ln_gamma) {
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= D.E) return;
-  const int S = D.S, d = D.d;
-  __shared__ float ns_sh[4][64];
-  float* ns = ns_sh[threadIdx.x >> 6];
-  const float* st = D.state + (int64_t)e * S;
-  const bool alive = D.alive[e] != 0;
-  // RSNorm eval on the packed [state, prev_reward] vector: (x - mean) / clamp(sqrt(var), eps)
-  if (lane <= S) {
-    const float xv = lane < S ? st[lane] : D.prev_reward[e];
-    ns[lane] = (xv - D.rs_mean[lane]) / fmaxf(sqrtf(D.rs_var[lane]), D.rs_eps);
-    if (lane < S && alive) D.traj_states[((int64_t)e * D.Tmax + t) * S + lane] = xv;
-  }
-  wave_sync();
-  const float nr = ns[S];
-  const int a = D.continuous ? 0 : D.prev_action[e];
-  float xs[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int c = lane, k = 0; c < d; c += 64, ++k) {
-    float p = 0.f, se = 0.f;
-    for (int s = 0; s < S; ++s) {
-      p += ns[s] * D.w_pin[c * S + s];
-      se += ns[s] * D.w_se[c * S + s];
+__global__ __launch_bounds__(1024) void k_compact(const XtrlDecodeDesc D, int t) {
+  __shared__ int wsum[16];
+  __shared__ int base_sh;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int32_t* rows = D.live_rows + (t & 1) * D.E;
+  if (tid == 0) base_sh = 0;
+  for (int e0 = 0; e0 < D.E; e0 += 1024) {
+    const int e = e0 + tid;
+    const bool al = e < D.E && D.alive[e] != 0;
+    const uint64_t bal = __ballot(al);
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = base_sh;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    if (al) rows[off + __popcll(bal & ((1ull << lane) - 1ull))] = e;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int i = 0; i < 16; ++i) tot += wsum[i];
+      base_sh += tot;
     }
-    if (D.b_pin) p += D.b_pin[c];
-    float act;
+    __syncthreads();
+  }
+  if (tid == 0) D.live_count[t & 1] = base_sh;
+}
+
+// ---------------------------------------------------------------------------------------------
+// embeddings of the live rows: one wave per row, 16 rows per 1024-thread workgroup; project_in and
+// to_state_embed weights staged once per workgroup in LDS as [s][column] images.  The kernel is
+// latency bound, so it is written as four batches of independent global loads (live count ->
+// slot -> state / previous action -> action-embedding rows), nothing loaded inside a loop
+// ---------------------------------------------------------------------------------------------
+constexpr int EMB_ROWS = 16;
+constexpr int EMB_LDS_FLOATS = 8192;   // 2 d S <= 8192 (C3: 4096); larger: weights read from global
+template <int NC>   // columns per lane: lane + 64 k, k < NC (d <= 64 NC)
+__global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
+  __shared__ float wsh[EMB_LDS_FLOATS];
+  __shared__ float ns_sh[EMB_ROWS][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int S = D.S, d = D.d, dS = d * S;
+  const bool staged = 2 * dS <= EMB_LDS_FLOATS;
+  // weights (independent of the rows): two float4 per thread per matrix cover 2 d S <= 8192
+  float4 wv[2][2];
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int f = min(tid + 1024 * u, (dS >> 2) - 1);
+      wv[0][u] = reinterpret_cast<const float4*>(D.w_pin)[f];
+      wv[1][u] = reinterpret_cast<const float4*>(D.w_se)[f];
+    }
+  }
+  // per-column constants of this lane
+  float remb[NC], bse[NC], bpin[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = min(lane + 64 * k, d - 1);
+    remb[k] = D.reward_embed[c];
+    bse[k] = D.b_se[c];
+    bpin[k] = D.b_pin ? D.b_pin[c] : 0.f;
+  }
+  const int n = D.live_count[t & 1];
+  const int r0 = blockIdx.x * EMB_ROWS;
+  if (r0 >= n) return;   // (whole workgroup)
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int f = tid + 1024 * u;
+      if (f < (dS >> 2)) {   // (c, s) -> [s][c] and [S + s][c]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = 4 * f + i, c = idx / S, sidx = idx - c * S;
+          wsh[sidx * d + c] = f4c(wv[0][u], i);
+          wsh[(S + sidx) * d + c] = f4c(wv[1][u], i);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int r = r0 + w;
+  if (r >= n) return;   // wave-uniform
+  const int e = D.live_rows[(t & 1) * D.E + r];
+  float* ns = ns_sh[w];
+  // RSNorm eval on the packed [state, prev_reward] vector: (x - mean) / clamp(sqrt(var), eps)
+  const float xv = lane < S ? D.state[(int64_t)e * S + lane] : D.prev_reward[e];
+  const int a = D.continuous ? 0 : D.prev_action[e];
+  float lat[NC];
+  if (D.evolutionary && D.lat_embed) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) lat[k] = D.lat_embed[(int64_t)e * d + min(lane + 64 * k, d - 1)];
+  }
+  if (lane <= S) {
+    ns[lane] = (xv - D.rs_mean[lane]) / fmaxf(sqrtf(D.rs_var[lane]), D.rs_eps);
+    if (lane < S) D.traj_states[((int64_t)e * D.Tmax + t) * S + lane] = xv;
+  }
+  float act[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const int c = min(lane + 64 * k, d - 1);
     if (D.continuous) {
       float acc = 0.f;
       for (int i = 0; i < D.A; ++i) acc += D.prev_action_f[e * D.A + i] * D.act_emb[c * D.A + i];
-      act = acc + D.act_emb_b[c];
+      act[k] = acc + D.act_emb_b[c];
     } else {
-      act = a >= 0 ? D.act_emb[a * d + c] : 0.f;
+      act[k] = D.act_emb[max(a, 0) * d + c];
     }
-    const float rew = D.no_reward_cond ? 0.f : nr * D.reward_embed[c];
-    const float xv = p + (act + rew);
-    D.x[(int64_t)e * d + c] = xv;
-    if (k < 4) xs[k] = xv;
-    D.ac_in[(int64_t)e * D.in_dim + d + c] = se + D.b_se[c];
   }
-  if (ln_gamma) {
-    float s = 0.f;
+  wave_sync();
+  const float nr = ns[S];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (lane + 64 * k < d) s += xs[k];
-    const float mean = wave_sum(s) / (float)d;
-    float q = 0.f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (lane + 64 * k < d) {
-        const float dlt = xs[k] - mean;
-        q += dlt * dlt;
-      }
+  for (int k = 0; k < NC; ++k) {
+    const int c = lane + 64 * k;
+    if (c >= d) break;
+    float p = 0.f, se = 0.f;
+    for (int sidx = 0; sidx < S; ++sidx) {
+      const float wp = staged ? wsh[sidx * d + c] : D.w_pin[c * S + sidx];
+      const float wsv = staged ? wsh[(S + sidx) * d + c] : D.w_se[c * S + sidx];
+      p += ns[sidx] * wp;
+      se += ns[sidx] * wsv;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = lane + 64 * k;
-      if (c < d) D.xn[(int64_t)e * d + c] = ((xs[k] - mean) * rstd) * ln_gamma[c];
-    }
+    p += bpin[k];
+    const float ak = (D.continuous || a >= 0) ? act[k] : 0.f;   // SafeEmbedding: -1 -> zero row
+    const float rew = D.no_reward_cond ? 0.f : nr * remb[k];
+    D.x[(int64_t)r * d + c] = p + (ak + rew);
+    D.ac_in[(int64_t)r * D.in_dim + d + c] = se + bse[k];
+    if (D.evolutionary && D.lat_embed) D.ac_in[(int64_t)r * D.in_dim + 2 * d + c] = lat[k];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// attention decode: one wave per (env, head), keys 0..t
+// attention decode: one wave per (live row, head), keys 0..t.  Latency bound: the keys are taken in
+// chunks of CK, and the first chunk's K rows (one key per lane) and V rows (a key per DH/4 lanes,
+// float4 per lane) are loaded in ONE batch right after the row's q|k|v — for t < CK (C3: every
+// step) the whole cache read is one memory round trip.  Reductions by DPP.
 // ---------------------------------------------------------------------------------------------
+// sum over the N consecutive lanes of an aligned group (N = 4, 8 or 16), every lane of the group
+// receiving it (DPP: quad xor steps, half-row and row mirrors)
+template <int N>
+__device__ __forceinline__ float kpi_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  if constexpr (N >= 8) v += dpp_mov<0x141>(v);
+  if constexpr (N >= 16) v += dpp_mov<0x140>(v);
+  return v;
+}
+
 template <int DH>
 __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int layer,
                                                      int t) {
+  constexpr int CK = DH <= 32 ? 128 : 64;          // keys per chunk
+  constexpr int KL = CK / 64, F4 = DH / 4;         // keys per lane (scores), float4 per key row
+  constexpr int LPK = DH / 4, KPI = 64 / LPK;      // P.V: lanes per key row, keys per load instruction
+  constexpr int VU = CK / KPI;                     // V loads per lane per chunk
   extern __shared__ float smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int idx = blockIdx.x * 4 + w;
   const int H = D.H, I = H * DH;
-  const int e = idx / H, h = idx - e * H;
-  const bool valid = e < D.E;
-  float* sc = smem + w * (D.Tmax + 3 * DH);   // scores [Tmax] | q | k_new | v_new
+  const int r = idx / H, h = idx - r * H;
+  if (r >= D.live_count[t & 1]) return;   // wave-uniform
+  const int e = rows_of(D, t)[r];
+  float* sc = smem + w * (D.Tmax + 3 * DH);   // scores / probabilities [Tmax] | q | k_new | v_new
   float* qs = sc + D.Tmax;
   float* ks = qs + DH;
   float* vs = ks + DH;
-  const bool alive = valid && D.alive[e] != 0;
-  if (!alive) return;   // wave-uniform
-  const float* row = D.qkv + (int64_t)e * D.n_qkv;
-  constexpr int G = 64 / DH;   // lane groups for the P.V product
+  const float* row = D.qkv + (int64_t)r * D.n_qkv;
   const int c = lane % DH, g = lane / DH;
   float q = row[h * DH + c], k = row[I + h * DH + c], v = row[2 * I + h * DH + c];
+  float v1v = 0.f, mixv = 0.f, gate4[4] = {0.f, 0.f, 0.f, 0.f};
+  // P.V lane roles: key kk = lane % KPI of a load instruction's KPI rows, channel quad cq = lane / KPI
+  // (the KPI rows of one instruction are consecutive: 1 KiB contiguous; the reduction over kk stays
+  // inside a 16-lane row: DPP steps, no cross-lane permutes)
+  const int kk = lane % KPI, cq = lane / KPI;
+  if (D.value_residual && layer > 0) {
+    v1v = D.v1[(int64_t)r * I + h * DH + c];
+    if (D.learned_mix) mixv = row[3 * I + (D.gate_values ? I : 0) + h];
+  }
+  if (D.gate_values) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gate4[i] = row[3 * I + h * DH + 4 * cq + i];
+  }
+  // the first chunk of the cache (rows written by earlier steps; rows >= t clamped, masked below)
+  const int64_t cache_base = ((int64_t)e * H + h) * D.Tmax * DH;
+  const float* Kc = Ly.k_cache + cache_base;
+  const float* Vc = Ly.v_cache + cache_base;
+  const int tl = max(t - 1, 0);
+  float4 kpre[KL][F4], vpre[VU];
+#pragma unroll
+  for (int u = 0; u < KL; ++u)
+#pragma unroll
+    for (int i = 0; i < F4; ++i) kpre[u][i] = reinterpret_cast<const float4*>(Kc + (int64_t)min(lane + 64 * u, tl) * DH)[i];
+#pragma unroll
+  for (int u = 0; u < VU; ++u)
+    vpre[u] = *reinterpret_cast<const float4*>(Vc + (int64_t)min(kk + KPI * u, tl) * DH + 4 * cq);
   // value residual (first layer stores its values; later layers lerp toward them)
   if (D.value_residual) {
-    float* v1 = D.v1 + (int64_t)e * I + h * DH + c;
     if (layer == 0) {
-      if (g == 0) *v1 = v;
+      if (g == 0) D.v1[(int64_t)r * I + h * DH + c] = v;
     } else if (D.learned_mix) {
-      const int mix_col = 3 * I + (D.gate_values ? I : 0) + h;
-      const float mix = sigmoidf_(row[mix_col]);
-      v = lerpf_(v, *v1, mix);
+      v = lerpf_(v, v1v, sigmoidf_(mixv));
     }
   }
   // rotary (interleaved pairs on the first rot_dim channels); 'zero' mode = position 0 = identity
@@ -139,7 +255,6 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
     q = q * cs + (sgn * qp) * sn;
     k = k * cs + (sgn * kp) * sn;
   }
-  const int64_t cache_base = ((int64_t)e * H + h) * D.Tmax * DH;
   if (g == 0) {
     qs[c] = q;
     ks[c] = k;
@@ -152,100 +267,140 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
   float qreg[DH];
 #pragma unroll
   for (int i = 0; i < DH; ++i) qreg[i] = qs[i];
-  const float* Kc = Ly.k_cache + cache_base;
-  const float* Vc = Ly.v_cache + cache_base;
+  // scores, one key per lane; chunk 0 from the prefetched rows
   float mx = -INFINITY;
-#pragma unroll 2
-  for (int j = lane; j <= t; j += 64) {
-    float s = 0.f;
-    if (j < t) {
-      const float4* kr = reinterpret_cast<const float4*>(Kc + (int64_t)j * DH);
+  for (int j0 = 0; j0 <= t; j0 += CK) {
+    float4 kc[KL][F4];
+    if (j0 == 0) {
 #pragma unroll
-      for (int i = 0; i < DH / 4; ++i) {
-        const float4 kv = kr[i];
-        s += qreg[4 * i] * kv.x;
-        s += qreg[4 * i + 1] * kv.y;
-        s += qreg[4 * i + 2] * kv.z;
-        s += qreg[4 * i + 3] * kv.w;
-      }
+      for (int u = 0; u < KL; ++u)
+#pragma unroll
+        for (int i = 0; i < F4; ++i) kc[u][i] = kpre[u][i];
     } else {
 #pragma unroll
-      for (int i = 0; i < DH; ++i) s += qreg[i] * ks[i];
+      for (int u = 0; u < KL; ++u)
+#pragma unroll
+        for (int i = 0; i < F4; ++i)
+          kc[u][i] = reinterpret_cast<const float4*>(Kc + (int64_t)min(j0 + lane + 64 * u, tl) * DH)[i];
     }
-    s *= scale;
-    sc[j] = s;
-    mx = fmaxf(mx, s);
+#pragma unroll
+    for (int u = 0; u < KL; ++u) {
+      const int j = j0 + lane + 64 * u;
+      float s = 0.f;
+      if (j < t) {
+#pragma unroll
+        for (int i = 0; i < F4; ++i) {
+          s += qreg[4 * i] * kc[u][i].x;
+          s += qreg[4 * i + 1] * kc[u][i].y;
+          s += qreg[4 * i + 2] * kc[u][i].z;
+          s += qreg[4 * i + 3] * kc[u][i].w;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < DH; ++i) s += qreg[i] * ks[i];
+      }
+      s *= scale;
+      if (j <= t) {
+        sc[j] = s;
+        mx = fmaxf(mx, s);
+      }
+    }
   }
-  mx = wave_max(mx);
+  mx = wave_max_dpp(mx);
   float sum = 0.f;
   for (int j = lane; j <= t; j += 64) {
     const float p = expf(sc[j] - mx);
     sc[j] = p;
     sum += p;
   }
-  sum = wave_sum(sum);
+  sum = wave_sum_dpp(sum);
   wave_sync();
-  float acc = 0.f;
-  // eight V rows in flight per lane group (the loads are independent; only the adds chain).
-  // (A one-key-per-lane P.V with a reduce-scatter butterfly measured slower: 14.9 vs 11.5 us.)
-#pragma unroll 8
-  for (int j = g; j <= t; j += G) {
-    const float p = sc[j] / sum;
-    const float vv = (j < t) ? Vc[(int64_t)j * DH + c] : vs[c];
-    acc += p * vv;
-  }
+  // P.V (unnormalised probabilities; one division at the end)
+  const float4 vnew = make_float4(vs[4 * cq], vs[4 * cq + 1], vs[4 * cq + 2], vs[4 * cq + 3]);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = 0; j0 <= t; j0 += CK) {
+    float4 vc[VU];
+    if (j0 == 0) {
 #pragma unroll
-  for (int o = DH; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
-  if (g == 0) {
-    float out = acc;
-    if (D.gate_values) out *= sigmoidf_(row[3 * I + h * DH + c]);
-    D.att[(int64_t)e * I + h * DH + c] = out;
+      for (int u = 0; u < VU; ++u) vc[u] = vpre[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < VU; ++u)
+        vc[u] = *reinterpret_cast<const float4*>(Vc + (int64_t)min(j0 + kk + KPI * u, tl) * DH + 4 * cq);
+    }
+#pragma unroll
+    for (int u = 0; u < VU; ++u) {
+      const int j = j0 + kk + KPI * u;
+      if (j <= t) {
+        const float p = sc[j];
+        const float4 v4 = j < t ? vc[u] : vnew;
+        acc.x += p * v4.x;
+        acc.y += p * v4.y;
+        acc.z += p * v4.z;
+        acc.w += p * v4.w;
+      }
+    }
+  }
+  acc.x = kpi_sum<KPI>(acc.x);
+  acc.y = kpi_sum<KPI>(acc.y);
+  acc.z = kpi_sum<KPI>(acc.z);
+  acc.w = kpi_sum<KPI>(acc.w);
+  if (kk == 0) {
+    float o4[4] = {acc.x / sum, acc.y / sum, acc.z / sum, acc.w / sum};
+    if (D.gate_values) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o4[i] *= sigmoidf_(gate4[i]);
+    }
+    *reinterpret_cast<float4*>(D.att + (int64_t)r * I + h * DH + 4 * cq) = make_float4(o4[0], o4[1], o4[2], o4[3]);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// sampling (one thread per env)
+// actor logits + sampling + device Sim step (SAMPLE_L lanes per live row)
 // ---------------------------------------------------------------------------------------------
-// sampling (xtrl.py:197-277) and, for the device Sim, its step (one thread per live env).  The
-// value logits were written straight into the trajectory by the critic GEMM (masked to live envs).
 __device__ __forceinline__ float reward_factor(int a) { return (float)(1.0 + 0.1 * (double)a); }
 
-__device__ __forceinline__ void sim_step_env(const XtrlDecodeDesc& D, int e, int t, const XtrlRngState& R) {
-  const uint32_t ep = (uint32_t)D.episode_of_slot[e];
-  const float z = rng_normal(R.seed, R.update, ep, t, FIELD_REWARD, 0);
-  const float reward = (D.sim_mode == 1 && !D.continuous) ? z * reward_factor(D.prev_action[e]) : z;
-  bool term = false;
-  if (D.sim_mode == 1 && D.hazard_log2 > 0)
-    term = (rng_u32(R.seed, R.update, ep, t, FIELD_TERM, 0) & ((1u << D.hazard_log2) - 1u)) == 0u;
-  D.traj_rewards[(int64_t)e * D.Tmax + t] = reward;
-  D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
-  D.prev_reward[e] = reward;
-  D.cum_reward[e] += (double)reward;
-  D.lens[e] = t + 1;   // (the next state was written by the env's lanes in k_sample)
-  if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
-}
-
-// SAMPLE_L lanes per env (one wave holds whole envs): lane 0 samples the action and steps the Sim;
-// the next state's S normals are spread over the env's lanes (they do not depend on the action)
+// SAMPLE_L lanes per row (a wave holds whole rows).  The row's lanes stage its logits in LDS and
+// draw its random numbers in parallel (none depends on the action): the next state's S normals
+// (lane i), the sampling uniform (lane 0), the Sim's reward normal (lane 1) and termination word
+// (lane 2); lane 0 then samples the action and finishes the Sim step.
 constexpr int SAMPLE_L = 8;
-__global__ void k_sample(const XtrlDecodeDesc D, int t) {
+__global__ __launch_bounds__(256) void k_sample(const XtrlDecodeDesc D, int t) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = gid / SAMPLE_L, sub = gid % SAMPLE_L;
-  if (e >= D.E || !D.alive[e]) return;   // (every lane of the env reads alive before lane 0 clears it)
-  if (D.alive[e] == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
-    if (sub == 0) D.alive[e] = 0;
+  const int r = gid / SAMPLE_L, sub = gid % SAMPLE_L;
+  if (r >= D.live_count[t & 1]) return;   // (whole rows: SAMPLE_L divides the wave)
+  const int e = rows_of(D, t)[r];
+  const XtrlRngState R = *D.rng;
+  // one batch of independent loads (latency bound kernel)
+  const int al = D.alive[e];   // (every lane of the row reads alive before lane 0 clears it)
+  const uint32_t ep = D.sim_mode >= 0 ? (uint32_t)D.episode_of_slot[e] : 0u;
+  const uint32_t slot = D.slot_of_row ? (uint32_t)D.slot_of_row[e] : R.slot_offset + (uint32_t)e;
+  const double cum = D.cum_reward[e];
+  const int A = D.A, n_act = D.continuous ? 2 * A : A;
+  __shared__ float lg_sh[256 / SAMPLE_L][64];
+  float* lg = lg_sh[threadIdx.x / SAMPLE_L];
+  for (int o = sub; o < n_act; o += SAMPLE_L) lg[o] = D.logits[(int64_t)r * n_act + o];
+  // random numbers of the step, spread over the row's lanes
+  float u = 0.f, zr = 0.f;
+  uint32_t tw = 0u;
+  if (sub == 0 && !D.continuous) u = rng_uniform(R.seed, R.update, slot, t, FIELD_SAMPLE, 0);
+  if (D.sim_mode >= 0) {
+    if (sub == 1) zr = rng_normal(R.seed, R.update, ep, t, FIELD_REWARD, 0);
+    if (sub == 2) tw = rng_u32(R.seed, R.update, ep, t, FIELD_TERM, 0);
+    if (al != 2)
+      for (int i = sub; i < D.S; i += SAMPLE_L)
+        D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
+  }
+  const int base = (threadIdx.x & 63) & ~(SAMPLE_L - 1);
+  zr = __shfl(zr, base + 1, 64);
+  tw = __shfl(tw, base + 2, 64);
+  wave_sync();
+  if (sub != 0) return;
+  if (al == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
+    D.alive[e] = 0;
     return;
   }
-  const XtrlRngState R = *D.rng;
-  if (D.sim_mode >= 0) {
-    const uint32_t ep = (uint32_t)D.episode_of_slot[e];
-    for (int i = sub; i < D.S; i += SAMPLE_L)
-      D.state[(int64_t)e * D.S + i] = rng_normal(R.seed, R.update, ep, t + 1, FIELD_STATE, i);
-  }
-  if (sub != 0) return;
-  const uint32_t slot = D.slot_of_row ? (uint32_t)D.slot_of_row[e] : R.slot_offset + (uint32_t)e;
-  const int A = D.A;
-  const float* lg = D.logits + (int64_t)e * (D.continuous ? 2 * A : A);
+  int a = 0;
   if (!D.continuous) {
     // softmax (xtrl.py:203), Categorical(probs) re-normalisation, inverse CDF on the supplied
     // uniform; probabilities recomputed on the fly (no per-thread array)
@@ -255,8 +410,6 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
     for (int i = 0; i < A; ++i) s += expf(lg[i] - mx);
     float s2 = 0.f;
     for (int i = 0; i < A; ++i) s2 += expf(lg[i] - mx) / s;
-    const float u = rng_uniform(R.seed, R.update, slot, t, FIELD_SAMPLE, 0);
-    int a = 0;
     float cdf = 0.f, pa = 0.f;
     for (int i = 0; i < A; ++i) {
       const float p = (expf(lg[i] - mx) / s) / s2;
@@ -277,17 +430,26 @@ __global__ void k_sample(const XtrlDecodeDesc D, int t) {
       const float var = expf(tanhf(lv / 3.f) * 3.f);
       const float sd = sqrtf(fmaxf(var, 1e-5f));
       const float z = rng_normal(R.seed, R.update, slot, t, FIELD_SAMPLE, i);
-      float s = mean + sd * z;
-      if (D.squash) s = tanhf(s);
-      float lp = -((s - mean) * (s - mean)) / (2.f * sd * sd) - logf(sd) - 0.91893853320467274f;
-      if (D.squash) lp -= logf(fmaxf(1.f - s * s, 1e-20f));
-      if (D.has_clamp) s = fminf(fmaxf(s, D.clamp_lo), D.clamp_hi);
-      D.traj_actions_f[((int64_t)e * D.Tmax + t) * A + i] = s;
+      float sv = mean + sd * z;
+      if (D.squash) sv = tanhf(sv);
+      float lp = -((sv - mean) * (sv - mean)) / (2.f * sd * sd) - logf(sd) - 0.91893853320467274f;
+      if (D.squash) lp -= logf(fmaxf(1.f - sv * sv, 1e-20f));
+      if (D.has_clamp) sv = fminf(fmaxf(sv, D.clamp_lo), D.clamp_hi);
+      D.traj_actions_f[((int64_t)e * D.Tmax + t) * A + i] = sv;
       D.traj_logp[((int64_t)e * D.Tmax + t) * A + i] = lp;
-      D.prev_action_f[e * A + i] = s;
+      D.prev_action_f[e * A + i] = sv;
     }
   }
-  if (D.sim_mode >= 0) sim_step_env(D, e, t, R);
+  if (D.sim_mode >= 0) {   // the synthetic Sim's step (reward, termination, bookkeeping)
+    const float reward = (D.sim_mode == 1 && !D.continuous) ? zr * reward_factor(a) : zr;
+    const bool term = D.sim_mode == 1 && D.hazard_log2 > 0 && (tw & ((1u << D.hazard_log2) - 1u)) == 0u;
+    D.traj_rewards[(int64_t)e * D.Tmax + t] = reward;
+    D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
+    D.prev_reward[e] = reward;
+    D.cum_reward[e] = cum + (double)reward;
+    D.lens[e] = t + 1;
+    if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
+  }
 }
 
 // host env results of step t (xtrl.py:1297-1336): the memory stores is_boundary = terminated;
@@ -334,10 +496,12 @@ __global__ void k_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t 
 
 int check_desc(const XtrlDecodeDesc* D) {
   XTRL_REQUIRE(D && D->layers, "decode: null descriptor");
+  XTRL_REQUIRE(D->live_rows && D->live_count, "decode: live_rows / live_count missing");
   XTRL_REQUIRE(D->E > 0 && D->S > 0 && D->S < 64 && D->A > 0 && D->A <= 32, "decode: bad E/S/A (E=%d S=%d A=%d)",
                D->E, D->S, D->A);
   XTRL_REQUIRE(D->dh == 16 || D->dh == 32 || D->dh == 64, "decode: dim_head %d unsupported (16/32/64)", D->dh);
-  XTRL_REQUIRE(D->H * D->dh <= 4096 && D->d > 0 && D->L > 0 && D->Tmax > 0, "decode: bad dims");
+  XTRL_REQUIRE(D->H * D->dh <= 4096 && D->d > 0 && D->d <= 512 && D->d % 4 == 0 && D->L > 0 && D->Tmax > 0,
+               "decode: bad dims (d must be a multiple of 4, at most 512)");
   XTRL_REQUIRE(D->in_dim == 2 * D->d + (D->evolutionary ? D->d : 0), "decode: in_dim mismatch");
   const int I = D->H * D->dh;
   XTRL_REQUIRE(D->n_qkv == 3 * I + (D->gate_values ? I : 0) + ((D->value_residual && D->learned_mix) ? D->H : 0),
@@ -360,54 +524,70 @@ int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
   return XTRL_OK;
 }
 
+// one decode projection over the live rows of step t
+int dproj(const XtrlDecodeDesc* D, int t, const float* A, int lda, const float* W, int K, const float* bias,
+          const float* gamma, int ln_k, const float* R, int ldr, float* C, int ldc, int N, int epi, hipStream_t s,
+          const int32_t* row_map = nullptr, int n_split = 1 << 30, float* C2 = nullptr, int ldc2 = 0,
+          const int32_t* row_map2 = nullptr) {
+  DGemmArgs g;
+  g.n_split = n_split; g.C2 = C2; g.ldc2 = ldc2; g.row_map2 = row_map2;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias; g.gamma = gamma; g.ln_k = ln_k;
+  g.R = R; g.ldr = ldr; g.C = C; g.ldc = ldc; g.row_map = row_map;
+  g.m_dev = D->live_count + (t & 1);
+  g.M = D->E; g.N = N; g.K = K;
+  return dgemm_run(g, D->E, epi, s);
+}
+
 }  // namespace
 
 int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode: t=%d outside [0, %d)", t, D->Tmax);
-  const int E = D->E, d = D->d, I = D->H * D->dh;
-  const bool embed_ln = d <= 256;   // layer 0's pre-norm inside the embedding kernel
-  hipLaunchKernelGGL(k_embed, dim3((E + 3) / 4), dim3(256), 0, s, *D, t,
-                     embed_ln ? D->layers[0].ln_attn : (const float*)nullptr);
+  const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff;
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
+  XTRL_LAUNCHED("compact");
+  {
+    const dim3 grid((E + EMB_ROWS - 1) / EMB_ROWS), blk(1024);
+    switch ((d + 63) / 64) {
+      case 1: hipLaunchKernelGGL(k_embed<1>, grid, blk, 0, s, *D, t); break;
+      case 2: hipLaunchKernelGGL(k_embed<2>, grid, blk, 0, s, *D, t); break;
+      case 3: hipLaunchKernelGGL(k_embed<3>, grid, blk, 0, s, *D, t); break;
+      case 4: hipLaunchKernelGGL(k_embed<4>, grid, blk, 0, s, *D, t); break;
+      default: hipLaunchKernelGGL(k_embed<8>, grid, blk, 0, s, *D, t); break;
+    }
+  }
   XTRL_LAUNCHED("embed");
+  int rc;
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
-    // pre-norm once per row (a LN prologue inside the GEMM would be recomputed by every column tile)
-    int rc = (l == 0 && embed_ln) ? XTRL_OK : layernorm_f32(D->x, d, Ly.ln_attn, D->xn, d, E, d, s);
-    if (rc) return rc;
-    if ((rc = gemm_f32(D->xn, d, Ly.w_qkv, d, Ly.b_qkv, nullptr, nullptr, 0, D->qkv, D->n_qkv, nullptr, 0, E,
-                       D->n_qkv, d, XTRL_ACT_NONE, s)))
+    if ((rc = dproj(D, t, D->x, d, Ly.w_qkv, d, Ly.b_qkv, Ly.ln_attn, d, nullptr, 0, D->qkv, D->n_qkv, D->n_qkv,
+                    EPI_NONE, s)))
       return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
-    if ((rc = gemm_f32(D->att, I, Ly.w_out, I, nullptr, nullptr, D->x, d, D->x, d, nullptr, 0, E, d, I,
-                       XTRL_ACT_NONE, s)))
+    if ((rc = dproj(D, t, D->att, I, Ly.w_out, I, nullptr, nullptr, 0, D->x, d, D->x, d, d, EPI_NONE, s))) return rc;
+    if ((rc = dproj(D, t, D->x, d, Ly.w_ff1, d, Ly.b_ff1, Ly.ln_ff, d, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
       return rc;
-    if ((rc = layernorm_f32(D->x, d, Ly.ln_ff, D->xn, d, E, d, s))) return rc;
-    if ((rc = gemm_f32(D->xn, d, Ly.w_ff1, d, Ly.b_ff1, nullptr, nullptr, 0, D->hff, D->ff, nullptr, 0, E, D->ff, d,
-                       XTRL_ACT_GELU, s)))
-      return rc;
-    if ((rc = gemm_f32(D->hff, D->ff, Ly.w_ff2, D->ff, Ly.b_ff2, nullptr, D->x, d, D->x, d, nullptr, 0, E, d, D->ff,
-                       XTRL_ACT_NONE, s)))
+    // the last layer's output goes straight into the heads' input row (final norm in their prologue)
+    const bool last = l == D->L - 1;
+    if ((rc = dproj(D, t, D->hff, ff, Ly.w_ff2, ff, Ly.b_ff2, nullptr, 0, D->x, d, last ? D->ac_in : D->x,
+                    last ? D->in_dim : d, d, EPI_NONE, s)))
       return rc;
   }
-  int rc = layernorm_f32(D->x, d, D->ln_final, D->ac_in, D->in_dim, E, d, s);
-  if (rc) return rc;
-  // heads: hidden [E][4d] = SiLU(ac_in . [Wa1; Wc1]^T + b); logits / critic bins from the halves
-  if ((rc = gemm_f32(D->ac_in, D->in_dim, D->w_h1, D->in_dim, D->b_h1, nullptr, nullptr, 0, D->hff, 4 * d, nullptr,
-                     0, E, 4 * d, D->in_dim, XTRL_ACT_SILU, s)))
+  // heads: hidden [n][4d] = SiLU([final_norm(x) | state embed | latent] . [Wa1; Wc1]^T + b)
+  if ((rc = dproj(D, t, D->ac_in, D->in_dim, D->w_h1, D->in_dim, D->b_h1, D->ln_final, d, nullptr, 0, D->hff, 4 * d,
+                  4 * d, EPI_SILU, s)))
     return rc;
-  const int n_act = D->continuous ? 2 * D->A : D->A;
-  if ((rc = gemm_f32(D->hff, 4 * d, D->w_a2, 2 * d, D->b_a2, nullptr, nullptr, 0, D->logits, n_act, nullptr, 0, E,
-                     n_act, 2 * d, XTRL_ACT_NONE, s)))
-    return rc;
-  {   // critic bins straight into the trajectory row t (Memory.value, xtrl.py:1315), live envs only
-    GemmArgs g;
-    g.A = D->hff + 2 * d; g.lda = 4 * d; g.B = D->w_c2; g.ldb = 2 * d; g.bias = D->b_c2;
-    g.C = D->traj_values + (int64_t)t * D->B; g.ldc = D->Tmax * D->B; g.M = E; g.N = D->B; g.K = 2 * d;
-    g.row_mask = D->alive;
-    if ((rc = gemm_run(g, 0, 0, EPI_NONE, s))) return rc;
+  // the heads' last Linear layers as one block-diagonal projection of the hidden row: actor logits
+  // (columns < n_act) to the logits rows, critic bins straight into the trajectory row t of each
+  // live episode (Memory.value, xtrl.py:1315)
+  {
+    const int n_act = D->continuous ? 2 * D->A : D->A;
+    if ((rc = dproj(D, t, D->hff, 4 * d, D->w_h2, 4 * d, D->b_h2, nullptr, 0, nullptr, 0, D->logits, n_act,
+                    n_act + D->B, EPI_NONE, s, nullptr, n_act, D->traj_values + (int64_t)t * D->B, D->Tmax * D->B,
+                    D->live_rows + (t & 1) * E)))
+      return rc;
   }
   hipLaunchKernelGGL(k_sample, dim3((E * SAMPLE_L + 255) / 256), dim3(256), 0, s, *D, t);
   XTRL_LAUNCHED("sample");
@@ -419,12 +599,6 @@ int rollout_begin(const XtrlDecodeDesc* D, hipStream_t s) {
   hipLaunchKernelGGL(k_rollout_begin, dim3((D->E + 255) / 256), dim3(256), 0, s, *D);
   XTRL_LAUNCHED("rollout_begin");
   return XTRL_OK;
-}
-
-int attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
-  if (int rc = check_desc(D)) return rc;
-  XTRL_REQUIRE(l >= 0 && l < D->L && t >= 0 && t < D->Tmax, "attn_decode: bad layer / t");
-  return launch_attn_decode(D, l, t, s);
 }
 
 int env_feedback(const XtrlDecodeDesc* D, int t, const float* next_state, const float* reward,
@@ -452,9 +626,6 @@ extern "C" int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream)
 }
 extern "C" int xtrl_rollout_begin(const XtrlDecodeDesc* desc, void* stream) {
   return xtrl::rollout_begin(desc, xtrl::as_stream(stream));
-}
-extern "C" int xtrl_attn_decode(const XtrlDecodeDesc* desc, int layer, int t, void* stream) {
-  return xtrl::attn_decode(desc, layer, t, xtrl::as_stream(stream));
 }
 extern "C" int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state,
                                          const float* reward, const uint8_t* terminated, const uint8_t* truncated,

@@ -74,6 +74,34 @@ int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias
              int K, int act, hipStream_t s);
 int layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, hipStream_t s);
 
+// ---------------------------------------------------------------------------------------------
+// decode-step GEMM over compacted live rows (dgemm.hip)
+//   C[dst(m), n] = act( LN?(A)[m, :] . W[n, :] + bias[n] ) (+ R[m, n]),  m < (m_dev ? *m_dev : M)
+//   W is an nn.Linear weight [N][K]; LN (x-transformers LayerNorm times gamma) covers A's columns
+//   [0, ln_k); dst(m) = row_map ? row_map[m] : m
+// ---------------------------------------------------------------------------------------------
+struct DGemmArgs {
+  const float* A = nullptr; int lda = 0;
+  const float* W = nullptr; int ldw = 0;
+  const float* bias = nullptr;
+  const float* gamma = nullptr; int ln_k = 0;
+  const float* R = nullptr; int ldr = 0;
+  float* C = nullptr; int ldc = 0;
+  const int32_t* row_map = nullptr;
+  const int32_t* m_dev = nullptr;
+  int M = 0, N = 0, K = 0;
+  // columns n >= n_split go to C2[dst2(m) * ldc2 + n - n_split], dst2(m) = row_map2 ? row_map2[m] : m
+  // (the heads' last Linear: actor logits to a row buffer, critic logits into the trajectory)
+  int n_split = 1 << 30;
+  float* C2 = nullptr; int ldc2 = 0;
+  const int32_t* row_map2 = nullptr;
+};
+// `rows` bounds the live-row count (sizes the grid); epi: EPI_NONE / EPI_GELU / EPI_SILU;
+// W fragment-packed by dgemm_pack (dgemm_packed_floats(N, K) floats)
+int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s);
+int64_t dgemm_packed_floats(int N, int K);
+int dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s);
+
 // dropout threshold of probability p on a uint32 word: keep iff word >= thresh
 // p * 256 when that is an integer in [1, 255] (byte-mode FF dropout keep bits), else 0
 inline uint32_t dropout_thresh8(float p) {

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -41,12 +41,13 @@ class DecodeDesc(C.Structure):
                                     'learned_mix', 'rotary_abs', 'rot_dim', 'sim_mode', 'hazard_log2', 'no_reward_cond')]
                 + [('rs_eps', F32), ('clamp_lo', F32), ('clamp_hi', F32), ('has_clamp', I32)]
                 + [(n, P) for n in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se',
-                                    'ln_final', 'w_h1', 'b_h1', 'w_a2', 'b_a2', 'w_c2', 'b_c2', 'inv_freq')]
+                                    'ln_final', 'w_h1', 'b_h1', 'w_h2', 'b_h2', 'inv_freq')]
                 + [('layers', C.POINTER(DecodeLayer))]
                 + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
                                     'alive', 'lens', 'cum_reward', 'episode_of_slot', 'slot_of_row', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
-                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals', 'xn')]
+                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'live_rows', 'live_count',
+                                    'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
 
 
@@ -103,7 +104,9 @@ SIGNATURES = {
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
-    'xtrl_attn_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
+    'xtrl_dgemm': (I32, [P, I32, P, P, P, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, P]),
+    'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),
+    'xtrl_dgemm_packed_floats': (I64, [I32, I32]),
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P, P, P]),
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),

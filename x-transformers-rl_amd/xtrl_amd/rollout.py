@@ -9,15 +9,12 @@ One ``RolloutEngine`` owns, for a fixed (E envs x Tmax steps) shape:
 hipGraph of the whole rollout (the graph is reusable across updates because every buffer is
 persistent and the seed / update index live in device memory).
 
-Env groups (``groups`` > 1, off by default): the E envs are split into contiguous row blocks, each
-with its own descriptor (row-offset pointers into the same buffers, its own RNG slot offset),
-decoded as independent chains on separate HIP streams.  Measured on MI355X (C3, 1024 envs): the
-chains do NOT overlap inside a replayed hipGraph — rollout time grows with the group count
-(1: 48 ms, 2: 69 ms, 4: 116 ms per update) — so the default is one chain.
+Per step only the live episodes are decoded: the step's embedding kernel compacts them into
+rows 0..n-1 (``live_rows`` / ``live_count``, double-buffered by step parity) and every later
+kernel of the step reads the live count from device memory, so the captured graph needs no host
+sync and terminated episodes cost nothing.
 """
 from __future__ import annotations
-
-import os
 
 import ctypes as C
 
@@ -32,15 +29,10 @@ SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
 
 class RolloutEngine:
     def __init__(self, model: WorldModelActorCritic, E: int, Tmax: int, *, sim_mode=SIM_LANDER, hazard_log2=6,
-                 clamp=None, use_graph=False, groups=None):
+                 clamp=None, use_graph=False):
         c = model.cfg
         dev = next(model.parameters()).device
         self.c, self.E, self.T, self.dev = c, E, Tmax, dev
-        if groups is None:
-            groups = int(os.environ.get('XTRL_ROLLOUT_GROUPS', '1'))
-        while groups > 1 and E % groups:
-            groups -= 1
-        self.groups = groups
         self.sim_mode, self.use_graph = sim_mode, use_graph
         d, H, dh, S, A, B = c.dim, c.heads, c.dim_head, c.state_dim, c.num_actions, c.num_bins
         I = H * dh
@@ -55,7 +47,9 @@ class RolloutEngine:
         self.cum_reward = z(E, dt=torch.float64)
         self.episode_of_slot = z(E, dt=i32)
         self.slot_of_row = z(E, dt=i32)   # global pair index per row (non-contiguous shards)
-        self.rng = z(groups, 2, dt=torch.int64)
+        self.rng = z(2, dt=torch.int64)
+        self.live_rows, self.live_count = z(2, E, dt=i32), z(2, dt=i32)
+        self.lat_embed = z(E, d) if c.evolutionary else None
         # trajectory
         self.traj = dict(states=z(E, Tmax, S), actions=z(E, Tmax, dt=i32), actions_f=z(E, Tmax, A) if c.continuous else None,
                          logp=z(E, Tmax, A) if c.continuous else z(E, Tmax), rewards=z(E, Tmax),
@@ -63,38 +57,32 @@ class RolloutEngine:
         # scratch
         self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
         self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
-        self.vals, self.xn = z(E, B), z(E, d)
         self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
-        # packed weights
+        # decode weights (nn.Linear layouts; the GEMM operands are packed from them, self.wpk)
         self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
                       act_emb_b=z(d) if c.continuous else None, reward_embed=z(d), w_se=z(d, S), b_se=z(d),
-                      ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_a2=z(nA, 2 * d), b_a2=z(nA),
-                      w_c2=z(B, 2 * d), b_c2=z(B), inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
+                      ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_h2=z(nA + B, 4 * d), b_h2=z(nA + B),
+                      inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
         self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), ln_ff=z(d),
                         w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
         self.w_lat = None
+        # fragment-packed images of the decode GEMM weights (xtrl_dgemm_pack, refreshed by pack())
+        pk = lambda t: z(int(L.lib().xtrl_dgemm_packed_floats(t.shape[0], t.shape[1])))
+        self._pk_src = [(self.w, 'w_h1'), (self.w, 'w_h2')] + [(wl, k) for wl in self.wl
+                                                               for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
+        self.wpk = {(id(src), k): pk(src[k]) for src, k in self._pk_src}
         self._build_desc(clamp, hazard_log2)
         self.graph = None
 
     # ------------------------------------------------------------------------------------------
     def _build_desc(self, clamp, hazard_log2):
-        G = self.groups
-        self.descs, self._layers_g = [], []
-        for g in range(G):
-            D, layers = self._group_desc(g, self.E // G, clamp, hazard_log2)
-            self.descs.append(D)
-            self._layers_g.append(layers)
-        self.desc = self.descs[0]
-
-    def _group_desc(self, g, Eg, clamp, hazard_log2):
-        """Descriptor of env rows [g*Eg, (g+1)*Eg): same weights, row-offset buffers."""
-        c = self.c
-        r0, r1 = g * Eg, (g + 1) * Eg
-        rows = lambda t: None if t is None else C.c_void_p(t[r0:r1].data_ptr())
+        c, Eg = self.c, self.E
+        rows = L.ptr
         layers = (L.DecodeLayer * c.depth)()
         for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
-            layers[i] = L.DecodeLayer(*(L.ptr(w[k]) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
-                                                              'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc))
+            wv = lambda k: self.wpk.get((id(w), k), w[k])
+            layers[i] = L.DecodeLayer(*(L.ptr(wv(k)) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
+                                                               'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -106,21 +94,22 @@ class RolloutEngine:
         if clamp is not None:
             D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
         w = self.w
-        for k in ('w_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1', 'w_a2',
-                  'b_a2', 'w_c2', 'b_c2', 'inv_freq', 'rs_mean', 'rs_var'):
-            setattr(D, k, w[k].data_ptr() if w[k] is not None else None)
+        for k in ('w_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1', 'w_h2',
+                  'b_h2', 'inv_freq', 'rs_mean', 'rs_var'):
+            t = self.wpk.get((id(w), k), w[k])
+            setattr(D, k, t.data_ptr() if t is not None else None)
         D.b_pin = None
         D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
         for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
                   'episode_of_slot'):
             setattr(D, k, rows(getattr(self, k)))
         D.slot_of_row = None
-        D.rng = self.rng[g].data_ptr()
+        D.rng = self.rng.data_ptr()
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
-        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'vals', 'xn'):
+        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'live_rows', 'live_count', 'lat_embed'):
             setattr(D, k, rows(getattr(self, k)))
-        return D, layers
+        self.desc, self._layers = D, layers
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -139,10 +128,12 @@ class RolloutEngine:
         w['ln_final'].copy_(model.transformer.attn_layers.final_norm.gamma)
         torch.cat((model.action_head[0].weight, model.critic_head[0].weight), out=w['w_h1'])
         torch.cat((model.action_head[0].bias, model.critic_head[0].bias), out=w['b_h1'])
-        w['w_a2'].copy_(model.action_head[2].weight)
-        w['b_a2'].copy_(model.action_head[2].bias)
-        w['w_c2'].copy_(model.critic_head[2].weight)
-        w['b_c2'].copy_(model.critic_head[2].bias)
+        # heads' last Linear as one block-diagonal weight over the [actor | critic] hidden row
+        nA, d2 = w['b_h2'].numel() - c.num_bins, 2 * c.dim
+        w['w_h2'].zero_()
+        w['w_h2'][:nA, :d2].copy_(model.action_head[2].weight)
+        w['w_h2'][nA:, d2:].copy_(model.critic_head[2].weight)
+        torch.cat((model.action_head[2].bias, model.critic_head[2].bias), out=w['b_h2'])
         inv = model.transformer.attn_layers.rotary_pos_emb.inv_freq
         w['inv_freq'][:inv.numel()].copy_(inv)
         w['rs_mean'].copy_(rs_mean)
@@ -176,6 +167,11 @@ class RolloutEngine:
             wl['b_ff2'].copy_(ffb.ff[2].bias)
         if c.evolutionary:
             self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
+        lib = L.lib()
+        for src, k in self._pk_src:
+            t = src[k]
+            L.check(lib.xtrl_dgemm_pack(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(self.wpk[(id(src), k)]),
+                                        L.stream()), f'dgemm_pack({k})')
 
     # ------------------------------------------------------------------------------------------
     def _begin(self, seed, update, slot_offset, episode_of_slot, latent, slots=None):
@@ -183,51 +179,24 @@ class RolloutEngine:
         None: rows are the contiguous pairs slot_offset, slot_offset + 1, ..."""
         if slots is not None:
             self.slot_of_row.copy_(torch.as_tensor(slots, dtype=torch.int32))
-        for g, D in enumerate(self.descs):
-            Eg = self.E // self.groups
-            D.slot_of_row = self.slot_of_row[g * Eg:].data_ptr() if slots is not None else None
+        self.desc.slot_of_row = self.slot_of_row.data_ptr() if slots is not None else None
         for t in self.traj.values():
             if t is not None:
                 t.zero_()
-        Eg = self.E // self.groups
-        self.rng.copy_(torch.tensor([[seed & 0x7FFFFFFFFFFFFFFF,
-                                      (int(update) & 0xFFFFFFFF) | ((int(slot_offset) + g * Eg) << 32)]
-                                     for g in range(self.groups)], dtype=torch.int64))
+        self.rng.copy_(torch.tensor([seed & 0x7FFFFFFFFFFFFFFF, (int(update) & 0xFFFFFFFF) | (int(slot_offset) << 32)],
+                                    dtype=torch.int64))
         self.episode_of_slot.copy_(episode_of_slot.to(torch.int32))
         if self.c.evolutionary:
-            d = self.c.dim
-            self.ac_in[:, 2 * d:].copy_(F.linear(latent, *self.w_lat))
-        for D in self.descs:
-            L.check(L.lib().xtrl_rollout_begin(C.byref(D), L.stream()), 'rollout_begin')
+            self.lat_embed.copy_(F.linear(latent, *self.w_lat))
+        L.check(L.lib().xtrl_rollout_begin(C.byref(self.desc), L.stream()), 'rollout_begin')
 
     def step(self, t):
         L.check(L.lib().xtrl_decode_step(C.byref(self.desc), int(t), L.stream()), f'decode_step(t={t})')
 
     def _steps(self):
-        lib = L.lib()
-        if self.groups == 1:
-            s = L.stream()
-            for t in range(self.T):
-                L.check(lib.xtrl_decode_step(C.byref(self.desc), t, s), f'decode_step(t={t})')
-            return
-        # one independent chain per env group, each on its own stream (fork / join on events)
-        if getattr(self, '_streams', None) is None:
-            self._streams = [torch.cuda.Stream(device=self.dev) for _ in range(self.groups)]
-        main = torch.cuda.current_stream()
-        fork = torch.cuda.Event()
-        fork.record(main)
-        joins = []
-        for D, st in zip(self.descs, self._streams):
-            st.wait_event(fork)
-            with torch.cuda.stream(st):
-                s = L.stream()
-                for t in range(self.T):
-                    L.check(lib.xtrl_decode_step(C.byref(D), t, s), f'decode_step(t={t})')
-                ev = torch.cuda.Event()
-                ev.record(st)
-                joins.append(ev)
-        for ev in joins:
-            main.wait_event(ev)
+        lib, s = L.lib(), L.stream()
+        for t in range(self.T):
+            L.check(lib.xtrl_decode_step(C.byref(self.desc), t, s), f'decode_step(t={t})')
 
     @torch.no_grad()
     def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0, slots=None):
