@@ -141,9 +141,9 @@ class WgradGemmTimer:
     # resident round (the C3 shapes), the register-staged one otherwise
     KERNELS = ('k_gemm_ws<true, true', 'k_gemm<2, 2, 1, 2, 2, true, true')
 
-    def __init__(self, agent, cap=8192):
+    def __init__(self, agent, T, cap=8192):
         import ctypes as C
-        self.C, self.cap = C, cap
+        self.C, self.cap, self.T = C, cap, T
         self.events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cap)]
         for e in self.events:
             e.record()
@@ -155,7 +155,9 @@ class WgradGemmTimer:
         self.ms, self.launches, self.total_flops = 0.0, 0, 0.0
 
     def attach(self):
-        D = self.agent._train_step.D
+        # buffers sized for the longest episode (a later, longer update would otherwise rebuild
+        # the train step and drop the event pointers)
+        D = self.agent.train_step(self.agent.batch_size, self.T).D
         D.prof_events = self.C.cast(self.arr, self.C.POINTER(self.C.c_void_p))
         D.prof_flops = self.C.cast(self.flops, self.C.c_void_p)
         D.prof_cap = self.cap
@@ -354,13 +356,13 @@ def main():
     if timer is not None:
         # untimed: capture the rollout graph with the event records inside, and count the
         # weight-gradient launches of one update to size the timed region's event pool exactly
-        probe_timer = WgradGemmTimer(learner.agent, cap=1 << 14)
+        probe_timer = WgradGemmTimer(learner.agent, T, cap=1 << 14)
         probe_timer.attach()
         one_update(learner, env, T)
         per_update = probe_timer.n.value
         probe_timer.detach()
         timer.ms, timer.launches, timer.bytes = 0.0, 0, 0.0
-        gtimer = WgradGemmTimer(learner.agent, cap=per_update * args.steps + 64)
+        gtimer = WgradGemmTimer(learner.agent, T, cap=per_update * args.steps + 64)
         gtimer.attach()
     if world > 1:
         dist.barrier()
@@ -387,6 +389,9 @@ def main():
     env_steps = int(total)
     value = env_steps / elapsed
 
+    # committed profiles (profiles/rNN_*) are of the default C3 bench: quoted for that workload only
+    prof = (lambda f, *k: f(*k)) if args.config == 'c3' else (lambda f, *k: None)
+
     phase_ms = dict(rollout=round(sum(e[0].elapsed_time(e[1]) for e in PHASES) / len(PHASES), 2),
                     learn=round(sum(e[1].elapsed_time(e[2]) for e in PHASES) / len(PHASES), 2))
     roofline = attn_roofline = None
@@ -405,19 +410,19 @@ def main():
                                    ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
                                     'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
                             peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
-                            traffic=pmc_traffic(*WgradGemmTimer.KERNELS),
-                            mfma_busy=pmc_mfma_busy(*WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
-                            avg_launch_us_rocprof=rocprof_avg_us(*WgradGemmTimer.KERNELS),
+                            traffic=prof(pmc_traffic, *WgradGemmTimer.KERNELS),
+                            mfma_busy=prof(pmc_mfma_busy, *WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
+                            avg_launch_us_rocprof=prof(rocprof_avg_us, *WgradGemmTimer.KERNELS),
                             flops_per_launch=round(flops), launches=gtimer.launches)
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
         achieved = timer.bytes / timer.launches / avg_s / 1e9
         attn_roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache)', bound='hbm',
                              achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                             frac=round(achieved / HBM_PEAK_GBS, 4), traffic=pmc_traffic('k_attn_decode'),
+                             frac=round(achieved / HBM_PEAK_GBS, 4), traffic=prof(pmc_traffic, 'k_attn_decode'),
                              avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=round(timer.bytes / timer.launches))
         # the profiler's per-launch time (no event records around the launch) and the fraction it gives
-        us = rocprof_avg_us('k_attn_decode')
+        us = prof(rocprof_avg_us, 'k_attn_decode')
         if us:
             attn_roofline.update(avg_launch_us_rocprof=us, frac_rocprof=round(
                 timer.bytes / timer.launches / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))

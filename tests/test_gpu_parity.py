@@ -124,7 +124,7 @@ def _dot_scale(a, b):
     return a.abs() @ b.abs()
 
 
-@pytest.mark.parametrize('layout', ['NN', 'NT', 'TT'])
+@pytest.mark.parametrize('layout', ['NN', 'NT', 'TT', 'TT32'])
 def test_gemm_large_tile_split_bf16_accuracy(layout):
     """The large-tile geometry computes fp32 products as six bf16 piece products (csrc/gemm.hip,
     X6).  Its error against fp64 must stay at the native fp32 level: max |C - C64| / sum|a b| below
@@ -144,9 +144,14 @@ def test_gemm_large_tile_split_bf16_accuracy(layout):
     elif layout == 'NT':   # A [M][K], B [K][N] (input-gradient GEMM)
         ops.gemm_ex(a.to(DEV), b.to(DEV), 0, 1, M, N, K, out)
         ref, sc = ad @ bd, _dot_scale(ad, bd)
-    else:                  # weight gradient: dW[N][K'] = dY^T X over M tokens (split over tokens)
-        dy, x = a[:, :256].contiguous(), torch.randn(M, 1024, generator=g).float()
-        dw = torch.zeros(256, 1024, device=DEV)
+    else:                  # weight gradient: dW[N][K'] = dY^T X over M tokens (split over tokens); TT32: a
+        # token count that is a multiple of 32 (the native-f32 LDS-DMA ring kernel), ragged feature tiles
+        if layout == 'TT32':
+            a = a[:4096, :260].contiguous()
+            M = 4096
+        nk = (260, 1000) if layout == 'TT32' else (256, 1024)
+        dy, x = a[:, :nk[0]].contiguous(), torch.randn(M, nk[1], generator=g).float()
+        dw = torch.zeros(dy.shape[1], x.shape[1], device=DEV)
         ws = torch.empty(32 << 20, device=DEV)
         ops.wgrad(dy.to(DEV), x.to(DEV), dw, ws, beta=0.)
         out = dw
