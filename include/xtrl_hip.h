@@ -105,6 +105,8 @@ typedef struct XtrlDecodeDesc {
   int sim_mode;         /* 0 readme, 1 lander, -1 host env (no device sim step) */
   int hazard_log2;
   int no_reward_cond;   /* 1: model called with rewards=None (deploy without reward, xtrl.py:1042-1061) */
+  int state_only;       /* 1: the embedding is project_in(state) alone (the fractal body ignores the action /
+                           reward arguments, fractal_rl.py:540-553) */
   float rs_eps;
   float clamp_lo, clamp_hi; int has_clamp;
   /* weights (EMA model for the rollout, xtrl.py:1194) */
@@ -190,6 +192,54 @@ int xtrl_dgemm(const float* A, int lda, const float* Wp, const float* bias, cons
  * decode GEMM reads 1 KiB contiguous.  Done once per rollout (the EMA weights are fixed for it). */
 int64_t xtrl_dgemm_packed_floats(int N, int K);
 int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fractal policy body, one decode step (fractal_rl.py:37-346, 510-619 restated per timestep and
+ * causal so it can stand in for the Decoder in the rollout / PPO loop — DESIGN §6).  Per live row
+ * (the XtrlDecodeDesc's compaction, embedding (state_only = 1, b_pin = input_embed.bias + level
+ * embedding 0), heads and sampling are reused; its layers[l] hold level l's K/V caches and
+ * n_qkv = 3 I):
+ *   for each level l: x <- x + level_embed[l] (l > 0)
+ *     x1 = LN1(x + W_out attn(W_q x, W_k x, W_v x))      causal self-attention over the cache
+ *     x2 = LN2(x1 + W_out_g W_v_g g)                    cross-attention to the one-token global state
+ *     x3 = LN3(x2 + FF(x2))                             (softmax over one key == 1)
+ *     m  = mean over this episode's steps 0..t of x3    (running sums per episode slot)
+ *     g <- g + W_gu m + b_gu;  p_l = W_p,l m + b_p,l    (global state update, level projection)
+ *     x <- x3
+ *   features = W_fa2 ReLU(W_fa0 [p_0 | ... | p_{L-1} | g] + b) + b  -> ac_in[:, 0:d] -> heads
+ * GEMM weights fragment-packed (xtrl_dgemm_pack); LayerNorms nn.LayerNorm (eps, weight, bias). */
+typedef struct XtrlFractalLevel {
+  const float* w_qkv;                       /* [3I][d]  self_attn.to_q | to_k | to_v */
+  const float* w_out;                       /* [d][I]   self_attn.to_out */
+  const float* ln1_w; const float* ln1_b;   /* [d] norm1 */
+  const float* w_gv;                        /* [I][d]   global_attn.to_v */
+  const float* w_go;                        /* [d][I]   global_attn.to_out */
+  const float* ln2_w; const float* ln2_b;
+  const float* w_ff1; const float* b_ff1;   /* [ff][d], [ff] */
+  const float* w_ff2; const float* b_ff2;   /* [d][ff], [d] */
+  const float* ln3_w; const float* ln3_b;
+  const float* w_proj; const float* b_proj; /* level_projections[l] [d][d], [d] */
+  const float* level_emb;                   /* [d] level_embeds[l] + scale_embeds[l] (added for l > 0) */
+  float* sums;                              /* [E][d] running sum of this level's outputs per episode slot */
+} XtrlFractalLevel;
+
+typedef struct XtrlFractalDesc {
+  int levels;
+  float ln_eps;
+  const XtrlFractalLevel* level;            /* HOST array of `levels` descriptors */
+  const float* g_init;                      /* [d] global_state_init */
+  const float* w_gu; const float* b_gu;     /* global_state_update [d][d], [d] */
+  const float* w_fa0; const float* b_fa0;   /* final_aggregation.0 [2d][(L+1) d], [2d] */
+  const float* w_fa2; const float* b_fa2;   /* final_aggregation.2 [d][2d], [d] */
+  float* g;                                 /* [E][d] global state of the step's rows */
+  float* x1; float* x2; float* x3; float* mean;   /* [E][d] */
+  float* allf;                              /* [E][(L+1) d] */
+  float* hagg;                              /* [E][2d] */
+} XtrlFractalDesc;
+
+/* one timestep of the fractal policy for the live rows of `desc` (xtrl_rollout_begin first; the
+ * level sums are zeroed by the caller at the start of an episode batch) */
+int xtrl_fractal_decode_step(const XtrlDecodeDesc* desc, const XtrlFractalDesc* fd, int t, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * HL-Gauss value decode + GAE   (xtrl.py:843-852 -> calc_gae :616-640, HLGaussLoss value)

@@ -478,7 +478,9 @@ class OracleLearner:
     shared-uniform sampling protocol and counter-based minibatch permutations / reward coins
     (oracle/philox.py) so that a vectorised GPU run can be compared step by step."""
 
-    def __init__(self, c: LearnerConfig, init_state_dict=None, genes=None):
+    def __init__(self, c: LearnerConfig, init_state_dict=None, genes=None, model_factory=None):
+        """``model_factory(ModelConfig) -> module`` swaps the policy body (OracleWMAC by default;
+        fractal_ref.OracleFractalPolicy for the causal fractal body)."""
         self.c = c
         torch.manual_seed(c.seed)
         self.gp = None
@@ -493,7 +495,7 @@ class OracleLearner:
                          self.gp['dim'] if c.evolutionary else 0, c.frac_head_grad, c.beta_s, c.eps_clip,
                          c.value_clip, c.dropout, c.reward_dropout, True, c.gate_values, c.value_residual,
                          c.learned_mix)
-        self.model = OracleWMAC(mc)
+        self.model = model_factory(mc) if model_factory is not None else OracleWMAC(mc)
         if init_state_dict is not None:
             self.model.load_state_dict(init_state_dict)
         self.rsnorm = RSNormState(c.state_dim + 1)

@@ -7,7 +7,9 @@ import math
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
+from oracle import fractal_ref as FR
 from oracle import ref_port as R
 from oracle import thirdparty as tp
 
@@ -312,9 +314,15 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
-                 hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None):
+                 hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None):
+    """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides."""
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(seed)
+    factory = None
+    if fractal_levels is not None:
+        assert not gates
+        agent_extra = dict(agent_extra or {}, policy_body='fractal', fractal_levels=fractal_levels)
+        factory = lambda mc: FR.OracleFractalPolicy(mc, fractal_levels)   # noqa: E731
     wm = dict(attn_dim_head=16, heads=4, depth=depth)
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
@@ -340,7 +348,7 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
                         reward_dropout=reward_dropout)
     sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
     genes = learner.agent.gene_pool.genes.clone() if evo else None
-    oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes)
+    oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes, model_factory=factory)
     return learner, env, oracle
 
 
@@ -408,6 +416,85 @@ def test_rollout_graph_replay_equals_eager():
     torch.cuda.synchronize()
     for k, v in eager.items():
         assert torch.equal(v, traj[k]), k
+
+
+# ---- the causal fractal policy body (oracle/fractal_ref.OracleFractalPolicy) ------------
+
+
+@pytest.mark.parametrize('levels,evo,cont,dim', [(1, False, False, 48), (2, False, False, 48), (3, True, False, 64),
+                                                 (2, False, True, 48), (2, True, False, 256)])
+def test_fractal_rollout_matches_oracle(levels, evo, cont, dim):
+    """xtrl_fractal_decode_step (per level: K/V cache, running level means, per-step global state)
+    reproduces the oracle's batch-1 streaming rollout: identical actions and states, logp / values
+    within 1e-4."""
+    learner, env, oracle = make_learner(depth=levels, gates=False, evo=evo, cont=cont, dim=dim, fractal_levels=levels,
+                                        episodes=12 if dim == 256 else 8)
+    traj, lens, _, cum = learner.rollout_device(env, 0, 12)
+    torch.cuda.synchronize()
+    episodes, fitness = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes, cont=cont)
+    if evo:
+        tol(learner.fitness(cum, torch.tensor([g for _, g in learner.episode_genes])), fitness, 1e-5, 1e-5)
+
+
+def test_fractal_rollout_graph_replay_equals_eager():
+    learner, env, _ = make_learner(depth=2, gates=False, T=16, episodes=16, fractal_levels=2)
+    traj, _, _, _ = learner.rollout_device(env, 0, 16)
+    eager = {k: v.clone() for k, v in traj.items() if v is not None}
+    learner.use_graph = True
+    learner._engine = None
+    for update in (0, 0):   # capture, then replay
+        traj, _, _, _ = learner.rollout_device(env, update, 16)
+    torch.cuda.synchronize()
+    for k, v in eager.items():
+        assert torch.equal(v, traj[k]), k
+
+
+def test_fractal_forward_train_ragged_matches_oracle():
+    """The learn-step forward (cumulative-mean form, flash attention with key padding) equals the
+    oracle's streaming form position by position on ragged episodes; gradients of a random
+    functional of every output agree within 1e-4 of the gradient scale."""
+    learner, _, oracle = make_learner(depth=3, gates=False, dim=64, fractal_levels=3, evo=True)
+    agent = learner.agent
+    model, om = agent.model, oracle.model
+    g = torch.Generator().manual_seed(11)
+    b, n, S = 5, 23, 8
+    state = torch.randn(b, n, S, generator=g)
+    lens = torch.tensor([23, 1, 7, 16, 22], dtype=torch.int32)
+    nxt = torch.randint(-1, 4, (b, n), generator=g)
+    lat = F.normalize(torch.randn(b, 8, generator=g), dim=-1)
+    model.eval()
+    om.eval()
+    agent.flat.zero_grad()
+    outs = model.forward_train(state.cuda(), None, None, nxt.cuda(), lat.cuda(), lens.cuda())
+    ref = om(state, next_actions=nxt, latent_gene=lat)
+    mask = (torch.arange(n)[None] < lens[:, None].long())
+    for name, a, r in zip(('raw_actions', 'values'), outs[:2], ref[:2]):
+        a = a.detach().cpu()[mask]
+        r = r.detach()[mask]
+        assert float((a - r).abs().max()) <= 1e-4 * float(r.abs().max()) + 1e-6, name
+    w = [torch.randn(o.shape, generator=g) * mask.reshape(b, n, *([1] * (o.ndim - 2))) for o in outs]
+    sum((o * wi.cuda()).sum() for o, wi in zip(outs, w)).backward()
+    # oracle side: the same functional of (raw_actions, values, pred_raw, done_logit)
+    om.zero_grad()
+    ref = om(state, next_actions=nxt, latent_gene=lat)
+    (sum((o * wi).sum() for o, wi in zip((ref[0], ref[1]) + _oracle_wm_raw(om, state, nxt), w))).backward()
+    gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
+    scale = max(float(p.grad.abs().max()) for p in om.parameters() if p.grad is not None)
+    for name, p in om.named_parameters():
+        if p.grad is None:
+            continue
+        err = float((gpu_g[name] - p.grad).abs().max())
+        assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
+
+
+def _oracle_wm_raw(om, state, nxt):
+    """(pred_raw, done_logit) of the oracle fractal policy — the world-model heads before the
+    mean / variance split and the sigmoid (forward_train's outputs 3 and 4)."""
+    cache = dict(t=0, k=[None] * om.levels, v=[None] * om.levels, sums=[None] * om.levels)
+    feats = torch.stack([om._step(state[:, i], cache) for i in range(state.shape[1])], dim=1)
+    ewa = torch.cat((feats, om.embed_actions(nxt)), dim=-1)
+    return om.to_pred(ewa), om.to_pred_done(ewa)[..., 0]
 
 
 # ----------------------------------------------------------------------------------------------
@@ -559,13 +646,15 @@ def oracle_minibatch_tensors(episodes):
     return states, actions, old_lp, rewards, bounds, values, lens, genes
 
 
-@pytest.mark.parametrize('evo,gates,cont', [(False, False, False), (True, True, False), (False, True, True)])
-def test_ppo_loss_and_grads_identical_weights(evo, gates, cont):
+@pytest.mark.parametrize('evo,gates,cont,frac', [(False, False, False, None), (True, True, False, None),
+                                                  (False, True, True, None), (False, False, False, 2),
+                                                  (True, False, True, 3)])
+def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac):
     """BASELINE metric 'PPO loss delta vs CPU ref': for every minibatch of two learning updates the
     oracle recomputes loss and gradients with the GPU's current weights / RSNorm / genes on the
     same minibatch; loss within 1e-4 relative, gradients within 1e-4 of the gradient scale."""
     learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, cont=cont, T=10, episodes=6, batch=2, seed=5,
-                                        hazard=2)
+                                        hazard=2, fractal_levels=frac)
     agent = learner.agent
     c = oracle.c
     worst = [0.]
@@ -613,12 +702,14 @@ def test_ppo_loss_and_grads_identical_weights(evo, gates, cont):
     print(f'worst gradient error / gradient scale: {worst[0]:.2e}')
 
 
-@pytest.mark.parametrize('evo,gates', [(False, False), (True, True)])
-def test_learner_two_updates_match_oracle(evo, gates):
+@pytest.mark.parametrize('evo,gates,frac', [(False, False, None), (True, True, None), (False, False, 2),
+                                             (True, False, 2)])
+def test_learner_two_updates_match_oracle(evo, gates, frac):
     """Free-running: both sides train on their own.  The first update matches at 1e-4; later
     minibatches may drift because AdoptAtan2's cautious mask (sign of m*g) is discontinuous, so a
     1e-7 gradient difference can flip an element's step size 10x (documented in DESIGN.md)."""
-    learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, T=10, episodes=6, batch=2, seed=5, hazard=2)
+    learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, T=10, episodes=6, batch=2, seed=5, hazard=2,
+                                        fractal_levels=frac)
     agent = learner.agent
     keys = ('loss', 'actor_loss', 'critic_loss', 'autoreg_loss', 'pred_done_loss')
     for u in range(2):
@@ -670,9 +761,11 @@ def test_e2e_reference_contract(evolutionary, continuous_actions, tmp_path):
     assert (tmp_path / 'ppo.pt').exists()
 
 
-def test_deploy_forward_matches_oracle_cached_decode():
-    """Agent.forward (online model, KV cache threaded through hiddens) vs the oracle module."""
-    learner, env, oracle = make_learner(depth=2, gates=True)
+@pytest.mark.parametrize('frac', [None, 2])
+def test_deploy_forward_matches_oracle_cached_decode(frac):
+    """Agent.forward (online model, KV cache — and for the fractal body the level running sums —
+    threaded through hiddens) vs the oracle module."""
+    learner, env, oracle = make_learner(depth=2, gates=frac is None, fractal_levels=frac)
     agent = learner.agent
     agent.rs_mean.copy_(torch.linspace(-0.5, 0.5, 9))
     agent.rs_var.copy_(torch.linspace(0.5, 2., 9))

@@ -39,7 +39,8 @@ extern "C" int64_t xtrl_struct_size(const char* name) {
   } sizes[] = {{"XtrlDecodeLayer", sizeof(XtrlDecodeLayer)}, {"XtrlRngState", sizeof(XtrlRngState)},
                {"XtrlDecodeDesc", sizeof(XtrlDecodeDesc)},   {"XtrlTrainLayer", sizeof(XtrlTrainLayer)},
                {"XtrlTrainDesc", sizeof(XtrlTrainDesc)},     {"XtrlBatchDesc", sizeof(XtrlBatchDesc)},
-               {"XtrlLossDesc", sizeof(XtrlLossDesc)}};
+               {"XtrlLossDesc", sizeof(XtrlLossDesc)},       {"XtrlFractalLevel", sizeof(XtrlFractalLevel)},
+               {"XtrlFractalDesc", sizeof(XtrlFractalDesc)}};
   for (const auto& s : sizes)
     if (name && strcmp(name, s.name) == 0) return s.size;
   return -1;

@@ -166,8 +166,8 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
       se += ns[sidx] * wsv;
     }
     p += bpin[k];
-    const float ak = (D.continuous || a >= 0) ? act[k] : 0.f;   // SafeEmbedding: -1 -> zero row
-    const float rew = D.no_reward_cond ? 0.f : nr * remb[k];
+    const float ak = D.state_only ? 0.f : ((D.continuous || a >= 0) ? act[k] : 0.f);   // SafeEmbedding: -1 -> 0
+    const float rew = (D.no_reward_cond || D.state_only) ? 0.f : nr * remb[k];
     D.x[(int64_t)r * d + c] = p + (ak + rew);
     D.ac_in[(int64_t)r * D.in_dim + d + c] = se + bse[k];
     if (D.evolutionary && D.lat_embed) D.ac_in[(int64_t)r * D.in_dim + 2 * d + c] = lat[k];
@@ -494,6 +494,27 @@ __global__ void k_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t 
   for (int i = 0; i < S; ++i) state[(int64_t)e * S + i] = rng_normal(seed, update, (uint32_t)ep_of_slot[e], 0, FIELD_STATE, i);
 }
 
+// fractal body: running mean of a level's outputs over this episode's steps 0..t (one thread per
+// element of the live rows); sums[slot] accumulates in step order, restarting at t = 0
+__global__ __launch_bounds__(256) void k_copy_rows(const float* src, int lds, float* dst, int ldd, int M, int D) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(i / D), c = (int)(i - (int64_t)r * D);
+  if (r < M) dst[(int64_t)r * ldd + c] = src[(int64_t)r * lds + c];
+}
+
+__global__ __launch_bounds__(256) void k_running_mean(const XtrlDecodeDesc D, int t, const float* x, float* sums,
+                                                      float* mean) {
+  const int d = D.d;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(i / d), c = (int)(i - (int64_t)r * d);
+  if (r >= D.live_count[t & 1]) return;
+  const int e = rows_of(D, t)[r];
+  const float prev = sums[(int64_t)e * d + c];
+  const float s = (t > 0 ? prev : 0.f) + x[(int64_t)r * d + c];   // step 0 starts the episode's sum
+  sums[(int64_t)e * d + c] = s;
+  mean[(int64_t)r * d + c] = s / (float)(t + 1);
+}
+
 int check_desc(const XtrlDecodeDesc* D) {
   XTRL_REQUIRE(D && D->layers, "decode: null descriptor");
   XTRL_REQUIRE(D->live_rows && D->live_count, "decode: live_rows / live_count missing");
@@ -538,6 +559,26 @@ int dproj(const XtrlDecodeDesc* D, int t, const float* A, int lda, const float* 
   return dgemm_run(g, D->E, epi, s);
 }
 
+// heads + sampling of a decode step: hidden [n][4d] = SiLU([LN_final?(x) | state embed | latent] .
+// [Wa1; Wc1]^T + b); the last Linear layers as one block-diagonal projection (actor logits to the
+// logits rows, critic bins straight into the trajectory row t of each live episode: Memory.value,
+// xtrl.py:1315); then sampling and the Sim step
+int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s) {
+  const int E = D->E, d = D->d;
+  int rc;
+  if ((rc = dproj(D, t, D->ac_in, D->in_dim, D->w_h1, D->in_dim, D->b_h1, final_norm ? D->ln_final : nullptr,
+                  final_norm ? d : 0, nullptr, 0, D->hff, 4 * d, 4 * d, EPI_SILU, s)))
+    return rc;
+  const int n_act = D->continuous ? 2 * D->A : D->A;
+  if ((rc = dproj(D, t, D->hff, 4 * d, D->w_h2, 4 * d, D->b_h2, nullptr, 0, nullptr, 0, D->logits, n_act,
+                  n_act + D->B, EPI_NONE, s, nullptr, n_act, D->traj_values + (int64_t)t * D->B, D->Tmax * D->B,
+                  D->live_rows + (t & 1) * E)))
+    return rc;
+  hipLaunchKernelGGL(k_sample, dim3((E * SAMPLE_L + 255) / 256), dim3(256), 0, s, *D, t);
+  XTRL_LAUNCHED("sample");
+  return XTRL_OK;
+}
+
 }  // namespace
 
 int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
@@ -575,23 +616,69 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
                     last ? D->in_dim : d, d, EPI_NONE, s)))
       return rc;
   }
-  // heads: hidden [n][4d] = SiLU([final_norm(x) | state embed | latent] . [Wa1; Wc1]^T + b)
-  if ((rc = dproj(D, t, D->ac_in, D->in_dim, D->w_h1, D->in_dim, D->b_h1, D->ln_final, d, nullptr, 0, D->hff, 4 * d,
-                  4 * d, EPI_SILU, s)))
-    return rc;
-  // the heads' last Linear layers as one block-diagonal projection of the hidden row: actor logits
-  // (columns < n_act) to the logits rows, critic bins straight into the trajectory row t of each
-  // live episode (Memory.value, xtrl.py:1315)
-  {
-    const int n_act = D->continuous ? 2 * D->A : D->A;
-    if ((rc = dproj(D, t, D->hff, 4 * d, D->w_h2, 4 * d, D->b_h2, nullptr, 0, nullptr, 0, D->logits, n_act,
-                    n_act + D->B, EPI_NONE, s, nullptr, n_act, D->traj_values + (int64_t)t * D->B, D->Tmax * D->B,
-                    D->live_rows + (t & 1) * E)))
+  return decode_heads(D, t, true, s);
+}
+
+int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t, hipStream_t s) {
+  if (int rc = check_desc(D)) return rc;
+  XTRL_REQUIRE(F && F->level && F->levels == D->L && F->levels > 0, "fractal_decode: levels mismatch");
+  XTRL_REQUIRE(t >= 0 && t < D->Tmax, "fractal_decode: t=%d outside [0, %d)", t, D->Tmax);
+  XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs &&
+                   D->n_qkv == 3 * D->H * D->dh && D->d <= 512,
+               "fractal_decode: the descriptor must describe plain attention (n_qkv = 3 I) with state_only = 1");
+  const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels;
+  const int64_t Ed = (int64_t)E * d;
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
+  XTRL_LAUNCHED("compact");
+  hipLaunchKernelGGL(k_embed<8>, dim3((E + EMB_ROWS - 1) / EMB_ROWS), dim3(1024), 0, s, *D, t);   // x = W_in s + b_in + le_0
+  XTRL_LAUNCHED("embed");
+  rows_add_launch(nullptr, 0, F->g_init, F->g, d, E, d, s);   // per-step global state of every row starts at init
+  XTRL_LAUNCHED("rows_add");
+  int rc;
+  for (int l = 0; l < Lv; ++l) {
+    const XtrlFractalLevel& Q = F->level[l];
+    const float* xin = D->x;
+    if (l > 0) {   // the previous level's output plus this level's embedding
+      rows_add_launch(F->x3, d, Q.level_emb, D->x, d, E, d, s);
+      XTRL_LAUNCHED("rows_add");
+    }
+    if ((rc = dproj(D, t, xin, d, Q.w_qkv, d, nullptr, nullptr, 0, nullptr, 0, D->qkv, D->n_qkv, 3 * I, EPI_NONE, s)))
       return rc;
+    if ((rc = launch_attn_decode(D, l, t, s))) return rc;
+    if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s))) return rc;
+    add_layernorm_launch(xin, d, F->mean, d, Q.ln1_w, Q.ln1_b, F->x1, d, E, d, F->ln_eps, s);   // x1 = LN1(x + attn)
+    XTRL_LAUNCHED("add_layernorm");
+    // cross-attention to the one-token global state: W_out (W_v g)
+    if ((rc = dproj(D, t, F->g, d, Q.w_gv, d, nullptr, nullptr, 0, nullptr, 0, D->att, I, I, EPI_NONE, s))) return rc;
+    if ((rc = dproj(D, t, D->att, I, Q.w_go, I, nullptr, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s))) return rc;
+    add_layernorm_launch(F->x1, d, F->mean, d, Q.ln2_w, Q.ln2_b, F->x2, d, E, d, F->ln_eps, s);
+    XTRL_LAUNCHED("add_layernorm");
+    if ((rc = dproj(D, t, F->x2, d, Q.w_ff1, d, Q.b_ff1, nullptr, 0, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
+      return rc;
+    if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s)))
+      return rc;
+    add_layernorm_launch(F->x2, d, F->mean, d, Q.ln3_w, Q.ln3_b, F->x3, d, E, d, F->ln_eps, s);
+    XTRL_LAUNCHED("add_layernorm");
+    hipLaunchKernelGGL(k_running_mean, dim3((unsigned)((Ed + 255) / 256)), dim3(256), 0, s, *D, t, F->x3, Q.sums,
+                       F->mean);
+    XTRL_LAUNCHED("running_mean");
+    // level projection of the running mean, then the global-state update (after the block used g)
+    if ((rc = dproj(D, t, F->mean, d, Q.w_proj, d, Q.b_proj, nullptr, 0, nullptr, 0, F->allf + (int64_t)l * d,
+                    (Lv + 1) * d, d, EPI_NONE, s)))
+      return rc;
+    if ((rc = dproj(D, t, F->mean, d, F->w_gu, d, F->b_gu, nullptr, 0, F->g, d, F->g, d, d, EPI_NONE, s))) return rc;
   }
-  hipLaunchKernelGGL(k_sample, dim3((E * SAMPLE_L + 255) / 256), dim3(256), 0, s, *D, t);
-  XTRL_LAUNCHED("sample");
-  return XTRL_OK;
+  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((Ed + 255) / 256)), dim3(256), 0, s, F->g, d,
+                     F->allf + (int64_t)Lv * d, (Lv + 1) * d, E, d);
+  XTRL_LAUNCHED("copy_rows");
+  // final aggregation -> the heads' input row (no final norm: the encoder has none)
+  if ((rc = dproj(D, t, F->allf, (Lv + 1) * d, F->w_fa0, (Lv + 1) * d, F->b_fa0, nullptr, 0, nullptr, 0, F->hagg,
+                  2 * d, 2 * d, EPI_RELU, s)))
+    return rc;
+  if ((rc = dproj(D, t, F->hagg, 2 * d, F->w_fa2, 2 * d, F->b_fa2, nullptr, 0, nullptr, 0, D->ac_in, D->in_dim, d,
+                  EPI_NONE, s)))
+    return rc;
+  return decode_heads(D, t, false, s);
 }
 
 int rollout_begin(const XtrlDecodeDesc* D, hipStream_t s) {
@@ -636,4 +723,7 @@ extern "C" int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, cons
 extern "C" int xtrl_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update,
                               const int32_t* episode_of_slot, void* stream) {
   return xtrl::sim_reset(state, E, S, seed, update, episode_of_slot, xtrl::as_stream(stream));
+}
+extern "C" int xtrl_fractal_decode_step(const XtrlDecodeDesc* desc, const XtrlFractalDesc* fd, int t, void* stream) {
+  return xtrl::fractal_decode_step(desc, fd, t, xtrl::as_stream(stream));
 }

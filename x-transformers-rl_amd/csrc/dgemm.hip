@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) void k_dgemm(const DGemmArgs a) {
         float v = (acc[mt][nt][0][i] + acc[mt][nt][1][i]) + bias[nt];
         if constexpr (EPI == EPI_GELU) v = geluf_(v);
         if constexpr (EPI == EPI_SILU) v = siluf_(v);
+        if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.f);
         if constexpr (RES) v += resv[mt][nt][i];
         if (m < M && n < a.N) {
           if (n < a.n_split) a.C[dst[mt][i] * a.ldc + n] = v;
@@ -284,7 +285,8 @@ int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s) {
   XTRL_REQUIRE(a.K <= 2048 && a.lda >= a.K && a.ldc >= std::min(a.N, a.n_split),
                "dgemm: bad K / leading dimensions");
   XTRL_REQUIRE(!a.gamma || (a.ln_k > 0 && a.ln_k <= a.K && a.ln_k <= 512), "dgemm: bad LayerNorm width (<= 512)");
-  XTRL_REQUIRE(epi == EPI_NONE || epi == EPI_GELU || epi == EPI_SILU, "dgemm: epilogue %d unsupported", epi);
+  XTRL_REQUIRE(epi == EPI_NONE || epi == EPI_GELU || epi == EPI_SILU || epi == EPI_RELU,
+               "dgemm: epilogue %d unsupported", epi);
   XTRL_REQUIRE(a.n_split >= a.N || (a.C2 && a.n_split >= 0 && a.ldc2 >= a.N - a.n_split), "dgemm: bad column split");
   if (rows == 0) return XTRL_OK;
   const bool ln = a.gamma != nullptr, res = a.R != nullptr;
@@ -297,6 +299,10 @@ int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s) {
   } while (0)
   if (epi == EPI_GELU) XTRL_DG(EPI_GELU);
   else if (epi == EPI_SILU) XTRL_DG(EPI_SILU);
+  else if (epi == EPI_RELU) {
+    XTRL_REQUIRE(!ln && !res, "dgemm: the ReLU epilogue has no LayerNorm / residual variant");
+    dispatch_dg<EPI_RELU, false, false>(a, rows, s);
+  }
   else XTRL_DG(EPI_NONE);
 #undef XTRL_DG
   XTRL_LAUNCHED("dgemm");
@@ -315,5 +321,5 @@ extern "C" int xtrl_dgemm(const float* A, int lda, const float* Wp, const float*
   xtrl::DGemmArgs a;
   a.A = A; a.lda = lda; a.W = Wp; a.ldw = xtrl::dgemm_packed_floats(1, K) / 16; a.bias = bias; a.gamma = ln_gamma; a.ln_k = ln_k;
   a.R = R; a.ldr = ldr; a.C = C; a.ldc = ldc; a.row_map = row_map; a.m_dev = m_dev; a.M = M; a.N = N; a.K = K;
-  return xtrl::dgemm_run(a, M, act, xtrl::as_stream(stream));
+  return xtrl::dgemm_run(a, M, act == 3 ? xtrl::EPI_RELU : act, xtrl::as_stream(stream));
 }

@@ -90,6 +90,16 @@ __global__ __launch_bounds__(256) void k_wm_post(const float* raw, int ldr, int 
 }
 
 }  // namespace
+
+// launchers shared with the fractal decode step (decode.hip)
+void rows_add_launch(const float* x, int ldx, const float* v, float* y, int ldy, int M, int D, hipStream_t s) {
+  hipLaunchKernelGGL(k_rows_add, dim3((M + RW - 1) / RW), dim3(256), 0, s, x, ldx, v, y, ldy, M, D);
+}
+void add_layernorm_launch(const float* x, int ldx, const float* r, int ldr, const float* g, const float* b, float* y,
+                          int ldy, int M, int D, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_layernorm, dim3((M + RW - 1) / RW), dim3(256), 0, s, x, ldx, r, ldr, 1, g, b, y, ldy, M, D,
+                     eps);
+}
 }  // namespace xtrl
 
 using namespace xtrl;

@@ -102,6 +102,11 @@ int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s);
 int64_t dgemm_packed_floats(int N, int K);
 int dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s);
 
+// fractal body row kernels (fractal.hip): y = x + v (x NULL: v); y = LN(x + r) g + b (nn.LayerNorm)
+void rows_add_launch(const float* x, int ldx, const float* v, float* y, int ldy, int M, int D, hipStream_t s);
+void add_layernorm_launch(const float* x, int ldx, const float* r, int ldr, const float* g, const float* b, float* y,
+                          int ldy, int M, int D, float eps, hipStream_t s);
+
 // dropout threshold of probability p on a uint32 word: keep iff word >= thresh
 // p * 256 when that is an integer in [1, 255] (byte-mode FF dropout keep bits), else 0
 inline uint32_t dropout_thresh8(float p) {

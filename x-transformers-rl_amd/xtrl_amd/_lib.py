@@ -38,7 +38,8 @@ class RngState(C.Structure):
 class DecodeDesc(C.Structure):
     _fields_ = ([(n, I32) for n in ('E', 'S', 'A', 'B', 'd', 'L', 'H', 'dh', 'Tmax', 'G', 'ff', 'in_dim', 'n_qkv',
                                     'continuous', 'squash', 'evolutionary', 'gate_values', 'value_residual',
-                                    'learned_mix', 'rotary_abs', 'rot_dim', 'sim_mode', 'hazard_log2', 'no_reward_cond')]
+                                    'learned_mix', 'rotary_abs', 'rot_dim', 'sim_mode', 'hazard_log2', 'no_reward_cond',
+                                    'state_only')]
                 + [('rs_eps', F32), ('clamp_lo', F32), ('clamp_hi', F32), ('has_clamp', I32)]
                 + [(n, P) for n in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se',
                                     'ln_final', 'w_h1', 'b_h1', 'w_h2', 'b_h2', 'inv_freq')]
@@ -49,6 +50,17 @@ class DecodeDesc(C.Structure):
                                     'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'live_rows', 'live_count',
                                     'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
+
+
+class FractalLevel(C.Structure):
+    _fields_ = [(n, P) for n in ('w_qkv', 'w_out', 'ln1_w', 'ln1_b', 'w_gv', 'w_go', 'ln2_w', 'ln2_b', 'w_ff1', 'b_ff1',
+                                 'w_ff2', 'b_ff2', 'ln3_w', 'ln3_b', 'w_proj', 'b_proj', 'level_emb', 'sums')]
+
+
+class FractalDesc(C.Structure):
+    _fields_ = ([('levels', I32), ('ln_eps', F32), ('level', C.POINTER(FractalLevel))]
+                + [(n, P) for n in ('g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2', 'g', 'x1', 'x2', 'x3',
+                                    'mean', 'allf', 'hagg')])
 
 
 class LossDesc(C.Structure):
@@ -106,6 +118,7 @@ SIGNATURES = {
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
     'xtrl_dgemm': (I32, [P, I32, P, P, P, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, P]),
     'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),
+    'xtrl_fractal_decode_step': (I32, [C.POINTER(DecodeDesc), C.POINTER(FractalDesc), I32, P]),
     'xtrl_dgemm_packed_floats': (I64, [I32, I32]),
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P, P, P]),
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
@@ -135,7 +148,7 @@ SIGNATURES = {
 
 STRUCTS = {'XtrlDecodeLayer': DecodeLayer, 'XtrlRngState': RngState, 'XtrlDecodeDesc': DecodeDesc,
            'XtrlTrainLayer': TrainLayer, 'XtrlTrainDesc': TrainDesc, 'XtrlBatchDesc': BatchDesc,
-           'XtrlLossDesc': LossDesc}
+           'XtrlLossDesc': LossDesc, 'XtrlFractalLevel': FractalLevel, 'XtrlFractalDesc': FractalDesc}
 
 _lib = None
 

@@ -26,6 +26,7 @@ from __future__ import annotations
 import math
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from . import _lib as L
@@ -287,3 +288,116 @@ class FractalWorldModelActorCritic(nn.Module):
             level_feats.append(m)
         cache = dict(fractal_levels=levels, global_state=None, level_features=level_feats)
         return raw_actions, values, state_pred, dones, cache
+
+
+# ----------------------------------------------------------------------------------------------
+# Per-timestep, causal fractal policy body: the FractalWorldModelActorCritic of
+# fractal_rl.py:349-619 with every sequence pooling made causal, so position t sees states 0..t
+# only and the body stands in for the Decoder inside the Learner (PPO / world-model losses per
+# timestep, KV-cached rollout).  Decision log:
+#   * self-attention causal + key padding (the reference's encoder attends bidirectionally);
+#   * the global state is per timestep: g_t <- g_t + W_gu mean_{s <= t}(level_s) + b_gu
+#     (reference: one state per sequence from mean_n);
+#   * cross-attention reads g_t (one key, softmax == 1: W_out W_v g_t);
+#   * level outputs pooled causally: p_l,t = W_p,l mean_{s <= t}(level_s) + b_p,l (the projection of
+#     the running mean == the running mean of the projections);
+#   * features_t = final_aggregation([p_0,t | ... | g_t]); heads per timestep on
+#     [frac_gradient(features_t) | to_state_embed(s_t) (| latent)] (reference: state embed mean-pooled);
+#   * like the reference forward, the encoder reads the states only (the action / reward arguments
+#     condition nothing but the world-model heads' next action).
+# Parameter names are the reference class's, so its checkpoints load.
+# ----------------------------------------------------------------------------------------------
+
+
+class FractalPolicyActorCritic(FractalWorldModelActorCritic):
+    def __init__(self, c, levels):
+        super().__init__(c.state_dim, c.num_actions, c.num_bins, c.reward_range, embed_dim=c.dim,
+                         num_fractal_levels=levels, heads=c.heads, dim_head=c.dim_head, ff_mult=c.ff_mult,
+                         dropout=c.dropout, continuous_actions=c.continuous, squash_continuous=c.squash,
+                         evolutionary=c.evolutionary, dim_latent_gene=c.dim_gene if c.evolutionary else None)
+        self.cfg, self.levels = c, levels
+        lo, hi = c.reward_range
+        support = torch.linspace(lo, hi, c.num_bins + 1, dtype=torch.float32)
+        self.register_buffer('hl_support', support, persistent=False)
+        self.register_buffer('hl_centers', (support[:-1] + support[1:]) / 2, persistent=False)
+        self.hl_sigma = c.hl_sigma_ratio * (hi - lo) / c.num_bins
+
+    def hl_value(self, logits):
+        return (logits.softmax(dim=-1) * self.hl_centers).sum(-1)
+
+    def flat_order(self):
+        """Every parameter once; groups whose size is a multiple of 4 floats first (16-byte aligned
+        GEMM weights)."""
+        params = dict(self.named_parameters())
+        names = list(params)
+        names.sort(key=lambda n: params[n].numel() % 4 != 0)
+        return names
+
+    def bind_flat(self, flat, ws):
+        self._flat, self._ws = flat, ws
+
+    def embed_actions(self, actions):
+        if self.cfg.continuous:
+            return self._lin(actions, self.action_embeds)
+        onehot = F.one_hot(actions.clamp(min=0), self.cfg.num_actions).to(torch.float32)
+        onehot = onehot * (actions >= 0)[..., None].to(torch.float32)
+        return onehot @ self.action_embeds.embed.weight
+
+    def _lin(self, x, mod):
+        b = mod.bias
+        return ops.xlinear(x, mod.weight, b, mod.weight.grad, b.grad if b is not None else None, self._ws)
+
+    def level_embed(self, li):
+        le = self.fractal_encoder.level_embedding
+        return le.level_embeds[li] + le.scale_embeds[li]
+
+    def forward_train(self, state, actions, rewards, next_actions, latent_gene, lens, reward_keep=True,
+                      attn_seed=0, attn_offset=0, ff_offset=0):
+        """Learn-step forward (autograd over the HIP GEMM / flash-attention ops; LayerNorm, running
+        means and concatenations as PyTorch ops) -> (raw_actions, values, pred_raw, done_logit)."""
+        c = self.cfg
+        enc = self.fractal_encoder
+        b, n, _ = state.shape
+        d, H, dh = c.dim, c.heads, c.dim_head
+        I = H * dh
+        p_drop = c.dropout if self.training else 0.
+        split = lambda t: t.reshape(b, n, H, dh).permute(0, 2, 1, 3)
+        cnt = torch.arange(1, n + 1, device=state.device, dtype=torch.float32)[None, :, None]
+        x = self._lin(state, enc.input_embed)
+        g = enc.global_state_init.reshape(1, 1, d).expand(b, n, d)
+        projs = []
+        for li in range(self.levels):
+            blk = enc.get_fractal_block(li)
+            x = x + self.level_embed(li)
+            sa, ga = blk.self_attn, blk.global_attn
+            q, k, v = split(self._lin(x, sa.to_q)), split(self._lin(x, sa.to_k)), split(self._lin(x, sa.to_v))
+            o = ops.attention(q.contiguous(), k.contiguous(), v.contiguous(), lens, dh ** -0.5, p_drop, attn_seed,
+                              attn_offset, li)
+            o = o.permute(0, 2, 1, 3).reshape(b, n, I)
+            x1 = blk.norm1(x + self._lin(o, sa.to_out))
+            x2 = blk.norm2(x1 + self._lin(self._lin(g, ga.to_v), ga.to_out))
+            ff0, ff2 = blk.ff.ff[0][0], blk.ff.ff[2]
+            h = F.gelu(self._lin(x2, ff0))
+            if p_drop > 0:
+                from .train import ff_dropout_mask
+                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset, h.device, layer=li)
+                h = h * keep.view(b, n, -1).to(h.dtype) * (1.0 / (1.0 - p_drop))
+            x3 = blk.norm3(x2 + self._lin(h, ff2))
+            mean = x3.cumsum(dim=1) / cnt
+            projs.append(self._lin(mean, enc.level_projections[li]))
+            g = g + self._lin(mean, enc.global_state_update)
+            x = x3
+        fa0, fa2 = enc.final_aggregation[0], enc.final_aggregation[2]
+        feat = self._lin(F.relu(self._lin(torch.cat(projs + [g], dim=-1), fa0)), fa2)
+        ewa = torch.cat((feat, self.embed_actions(next_actions)), dim=-1)
+        pred_raw = self._lin(F.silu(self._lin(ewa, self.to_pred[0])), self.to_pred[2])
+        done_logit = self._lin(ewa, self.to_pred_done[0])[..., 0]
+        f = c.frac_head_grad
+        feat = feat.detach() * (1. - f) + feat * f
+        ac_in = torch.cat((feat, self._lin(state, self.to_state_embed)), dim=-1)
+        if c.evolutionary:
+            lat = self._lin(latent_gene, self.latent_to_embed)
+            ac_in = torch.cat((ac_in, lat[:, None, :].expand(-1, n, -1)), dim=-1)
+        raw_actions = self._lin(F.silu(self._lin(ac_in, self.action_head[0])), self.action_head[2])
+        values = self._lin(F.silu(self._lin(ac_in, self.critic_head[0])), self.critic_head[2])
+        return raw_actions, values, pred_raw, done_logit

@@ -38,7 +38,8 @@ from . import ops
 from .evolution import LatentGenePool, evolve_seed
 from .model import ModelConfig, WorldModelActorCritic
 from .params import FlatParams
-from .rollout import SIM_HOST, SIM_LANDER, SIM_README, RolloutEngine
+from .fractal import FractalPolicyActorCritic
+from .rollout import SIM_HOST, SIM_LANDER, SIM_README, make_engine
 from .train import rsnorm_update
 
 
@@ -89,7 +90,7 @@ class Agent(nn.Module):
                  actor_loss_weight=1., critic_loss_weight=1., autoregressive_loss_weight=1.,
                  # extensions (decision log in DESIGN.md)
                  reward_dropout=0.5, seed=0, rotary_abs_rollout=False, hl_reduction_mean=True, hl_sigma_ratio=2.0,
-                 fused_learn=True, device=None, truncation_bootstrap=True):
+                 fused_learn=True, device=None, truncation_bootstrap=True, policy_body='decoder', fractal_levels=None):
         super().__init__()
         self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
         dev = self.accelerator.device
@@ -113,7 +114,20 @@ class Agent(nn.Module):
                         learned_mix=wm.get('learned_value_residual_mix', False), rotary_abs_rollout=rotary_abs_rollout,
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
-        self.model = WorldModelActorCritic(c).to(dev)
+        # policy body: the x-transformers Decoder (x_transformers_rl.py) or the per-timestep causal
+        # fractal encoder (fractal_rl.py:349-619 made causal, fractal.FractalPolicyActorCritic)
+        if policy_body == 'fractal':
+            if c.gate_values or c.value_residual:
+                raise NotImplementedError('the fractal policy body has no gated values / value residual: '
+                                          'set attn_gate_values / add_value_residual to False')
+            levels = int(fractal_levels or c.depth)
+            self.model = FractalPolicyActorCritic(c, levels).to(dev)
+            fused_learn = False   # the fused learn step (train.FusedTrainStep) is the decoder's
+        elif policy_body == 'decoder':
+            self.model = WorldModelActorCritic(c).to(dev)
+        else:
+            raise ValueError(f"policy_body must be 'decoder' or 'fractal', not {policy_body!r}")
+        self.policy_body = policy_body
         # the minibatch RSNorm mean (xtrl_minibatch_gather) rides behind the gradient: one all-reduce
         self.flat = FlatParams(self.model, dev, order=self.model.flat_order(), extra=state_dim + 1)
         dist_.broadcast_(self.flat.flat)          # identical initial weights on every rank (DDP semantics)
@@ -430,16 +444,14 @@ class Agent(nn.Module):
     def forward(self, state, reward=None, hiddens=None, latent_gene_id=0):
         c = self.cfg
         if self._deploy is None or self._deploy[1] != self.step:
-            eng = RolloutEngine(self.model, 1, 4096 if c.dim_head == 16 else 1024, sim_mode=SIM_HOST)
+            eng = make_engine(self.model, 1, 4096 if c.dim_head == 16 else 1024, sim_mode=SIM_HOST)
             self._deploy = (eng, self.step)
         eng = self._deploy[0]
         eng.pack(self.model, self.rs_mean, self.rs_var)
         t = 0 if hiddens is None else hiddens['t']
         if hiddens is not None:
-            for (k, v), (hk, hv) in zip(eng.kv, hiddens['kv']):
-                k.copy_(hk)
-                v.copy_(hv)
-            eng.v1.copy_(hiddens['v1'])
+            for dst, src in zip(eng.cache_tensors(), hiddens['cache']):
+                dst.copy_(src)
         state = torch.as_tensor(np.asarray(state), dtype=torch.float32, device=self.device).reshape(1, -1)
         eng.state.copy_(state)
         latent = self.latent(torch.tensor([latent_gene_id], device=self.device)) if c.evolutionary else None
@@ -449,7 +461,7 @@ class Agent(nn.Module):
         eng.prev_action.fill_(-1)     # the deploy forward passes no actions (xtrl.py:1056-1061)
         eng.step(t)
         raw = eng.logits[0].clone()
-        new_h = dict(t=t + 1, kv=[(k.clone(), v.clone()) for k, v in eng.kv], v1=eng.v1.clone())
+        new_h = dict(t=t + 1, cache=[x.clone() for x in eng.cache_tensors()])
         return raw, new_h
 
 
@@ -515,8 +527,8 @@ class Learner(nn.Module):
         if self._engine is None or self._engine[0] != key:
             E = len(self.episode_genes_for_process)
             mode = SIM_LANDER if env.mode == 'lander' else SIM_README
-            eng = RolloutEngine(self.agent.model, E, T, sim_mode=mode, hazard_log2=env.hazard_log2,
-                                clamp=self.continuous_actions_clamp, use_graph=self.use_graph)
+            eng = make_engine(self.agent.model, E, T, sim_mode=mode, hazard_log2=env.hazard_log2,
+                              clamp=self.continuous_actions_clamp, use_graph=self.use_graph)
             self._engine = (key, eng)
         return self._engine[1]
 
@@ -591,7 +603,7 @@ class Learner(nn.Module):
     def _engine_for_host(self, W, T):
         key = ('host', W, T)
         if self._engine is None or self._engine[0] != key:
-            eng = RolloutEngine(self.agent.model, W, T + 1, sim_mode=SIM_HOST, clamp=self.continuous_actions_clamp)
+            eng = make_engine(self.agent.model, W, T + 1, sim_mode=SIM_HOST, clamp=self.continuous_actions_clamp)
             self._engine = (key, eng)
         return self._engine[1]
 

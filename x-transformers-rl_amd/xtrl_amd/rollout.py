@@ -17,6 +17,7 @@ sync and terminated episodes cost nothing.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 
 import torch
 import torch.nn.functional as F
@@ -29,8 +30,8 @@ SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
 
 class RolloutEngine:
     def __init__(self, model: WorldModelActorCritic, E: int, Tmax: int, *, sim_mode=SIM_LANDER, hazard_log2=6,
-                 clamp=None, use_graph=False):
-        c = model.cfg
+                 clamp=None, use_graph=False, cfg=None):
+        c = cfg if cfg is not None else model.cfg
         dev = next(model.parameters()).device
         self.c, self.E, self.T, self.dev = c, E, Tmax, dev
         self.sim_mode, self.use_graph = sim_mode, use_graph
@@ -63,16 +64,27 @@ class RolloutEngine:
                       act_emb_b=z(d) if c.continuous else None, reward_embed=z(d), w_se=z(d, S), b_se=z(d),
                       ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_h2=z(nA + B, 4 * d), b_h2=z(nA + B),
                       inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
-        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), ln_ff=z(d),
-                        w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
         self.w_lat = None
+        self._pk_src = [(self.w, 'w_h1'), (self.w, 'w_h2')]
+        self._alloc_body(z)
         # fragment-packed images of the decode GEMM weights (xtrl_dgemm_pack, refreshed by pack())
         pk = lambda t: z(int(L.lib().xtrl_dgemm_packed_floats(t.shape[0], t.shape[1])))
-        self._pk_src = [(self.w, 'w_h1'), (self.w, 'w_h2')] + [(wl, k) for wl in self.wl
-                                                               for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
         self.wpk = {(id(src), k): pk(src[k]) for src, k in self._pk_src}
         self._build_desc(clamp, hazard_log2)
         self.graph = None
+
+    def _alloc_body(self, z):
+        """Per-layer decoder weights (self.wl) and their packed GEMM operands."""
+        c = self.c
+        d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
+        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), ln_ff=z(d),
+                        w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
+
+    def _wv(self, src, k):
+        """The tensor the descriptor points at for weight k of src: its packed image if it has one."""
+        t = self.wpk.get((id(src), k), src.get(k))
+        return L.ptr(t) if t is not None else None
 
     # ------------------------------------------------------------------------------------------
     def _build_desc(self, clamp, hazard_log2):
@@ -80,9 +92,8 @@ class RolloutEngine:
         rows = L.ptr
         layers = (L.DecodeLayer * c.depth)()
         for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
-            wv = lambda k: self.wpk.get((id(w), k), w[k])
-            layers[i] = L.DecodeLayer(*(L.ptr(wv(k)) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
-                                                               'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc))
+            layers[i] = L.DecodeLayer(*(self._wv(w, k) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
+                                                                 'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -94,11 +105,9 @@ class RolloutEngine:
         if clamp is not None:
             D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
         w = self.w
-        for k in ('w_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1', 'w_h2',
-                  'b_h2', 'inv_freq', 'rs_mean', 'rs_var'):
-            t = self.wpk.get((id(w), k), w[k])
-            setattr(D, k, t.data_ptr() if t is not None else None)
-        D.b_pin = None
+        for k in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1',
+                  'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var'):
+            setattr(D, k, self._wv(w, k))
         D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
         for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
                   'episode_of_slot'):
@@ -117,27 +126,10 @@ class RolloutEngine:
         """Copy (EMA) model weights into the decode layout (xtrl.py:721-734, 304-369 names)."""
         c, w = self.c, self.w
         w['w_pin'].copy_(model.transformer.project_in.weight)
-        if c.continuous:
-            w['act_emb'].copy_(model.action_embeds.weight)
-            w['act_emb_b'].copy_(model.action_embeds.bias)
-        else:
-            w['act_emb'].copy_(model.action_embeds.embed.weight)
-        w['reward_embed'].copy_(model.reward_embed)
-        w['w_se'].copy_(model.to_state_embed.weight)
-        w['b_se'].copy_(model.to_state_embed.bias)
         w['ln_final'].copy_(model.transformer.attn_layers.final_norm.gamma)
-        torch.cat((model.action_head[0].weight, model.critic_head[0].weight), out=w['w_h1'])
-        torch.cat((model.action_head[0].bias, model.critic_head[0].bias), out=w['b_h1'])
-        # heads' last Linear as one block-diagonal weight over the [actor | critic] hidden row
-        nA, d2 = w['b_h2'].numel() - c.num_bins, 2 * c.dim
-        w['w_h2'].zero_()
-        w['w_h2'][:nA, :d2].copy_(model.action_head[2].weight)
-        w['w_h2'][nA:, d2:].copy_(model.critic_head[2].weight)
-        torch.cat((model.action_head[2].bias, model.critic_head[2].bias), out=w['b_h2'])
         inv = model.transformer.attn_layers.rotary_pos_emb.inv_freq
         w['inv_freq'][:inv.numel()].copy_(inv)
-        w['rs_mean'].copy_(rs_mean)
-        w['rs_var'].copy_(rs_var)
+        self._pack_common(model, rs_mean, rs_var)
         I = c.inner
         for wl, (attn_l, ff_l) in zip(self.wl, model.blocks()):
             (ln_a, _, _), blk, _ = attn_l
@@ -165,8 +157,34 @@ class RolloutEngine:
             wl['b_ff1'].copy_(ffb.ff[0][0].bias)
             wl['w_ff2'].copy_(ffb.ff[2].weight)
             wl['b_ff2'].copy_(ffb.ff[2].bias)
+        self._pack_gemm_weights()
+
+    def _pack_common(self, model, rs_mean, rs_var):
+        """Action / reward / state embeddings, the actor-critic heads, RSNorm and the latent map —
+        the parts every policy body shares (x_transformers_rl.py:304-369, fractal_rl.py:386-446)."""
+        c, w = self.c, self.w
+        if c.continuous:
+            w['act_emb'].copy_(model.action_embeds.weight)
+            w['act_emb_b'].copy_(model.action_embeds.bias)
+        else:
+            w['act_emb'].copy_(model.action_embeds.embed.weight)
+        w['reward_embed'].copy_(model.reward_embed)
+        w['w_se'].copy_(model.to_state_embed.weight)
+        w['b_se'].copy_(model.to_state_embed.bias)
+        torch.cat((model.action_head[0].weight, model.critic_head[0].weight), out=w['w_h1'])
+        torch.cat((model.action_head[0].bias, model.critic_head[0].bias), out=w['b_h1'])
+        # heads' last Linear as one block-diagonal weight over the [actor | critic] hidden row
+        nA, d2 = w['b_h2'].numel() - c.num_bins, 2 * c.dim
+        w['w_h2'].zero_()
+        w['w_h2'][:nA, :d2].copy_(model.action_head[2].weight)
+        w['w_h2'][nA:, d2:].copy_(model.critic_head[2].weight)
+        torch.cat((model.action_head[2].bias, model.critic_head[2].bias), out=w['b_h2'])
+        w['rs_mean'].copy_(rs_mean)
+        w['rs_var'].copy_(rs_var)
         if c.evolutionary:
             self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
+
+    def _pack_gemm_weights(self):
         lib = L.lib()
         for src, k in self._pk_src:
             t = src[k]
@@ -194,9 +212,12 @@ class RolloutEngine:
         L.check(L.lib().xtrl_decode_step(C.byref(self.desc), int(t), L.stream()), f'decode_step(t={t})')
 
     def _steps(self):
-        lib, s = L.lib(), L.stream()
         for t in range(self.T):
-            L.check(lib.xtrl_decode_step(C.byref(self.desc), t, s), f'decode_step(t={t})')
+            self.step(t)
+
+    def cache_tensors(self):
+        """The per-episode decode state carried between deploy calls (Agent.forward hiddens)."""
+        return [t for kv in self.kv for t in kv] + [self.v1]
 
     @torch.no_grad()
     def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0, slots=None):
@@ -287,3 +308,98 @@ class RolloutEngine:
             live = live & ~ended
         torch.cuda.current_stream().synchronize()   # the pinned staging buffer is reused next wave
         return self.traj, lens, totals, boot_rows
+
+
+class FractalRolloutEngine(RolloutEngine):
+    """KV-cached rollout of the causal fractal policy body (fractal.FractalPolicyActorCritic)
+    through ``xtrl_fractal_decode_step``.  Per level it keeps the self-attention K/V caches and the
+    running sum of the level's outputs over the episode so far (the causal mean pools of the
+    global-state update and the level projection); the step's global state starts at
+    global_state_init and is updated level by level (fractal_rl.py:318-340, causal)."""
+
+    def __init__(self, model, E: int, Tmax: int, **kw):
+        c = dataclasses.replace(model.cfg, depth=model.levels, gate_values=False, value_residual=False,
+                                learned_mix=False, rotary_abs_rollout=False)
+        self.levels = model.levels
+        self.ln_eps = float(model.fractal_encoder.get_fractal_block(0).norm1.eps)
+        super().__init__(model, E, Tmax, cfg=c, **kw)
+
+    def _alloc_body(self, z):
+        c, E, Lv = self.c, self.E, self.levels
+        d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
+        self.w.update(b_pin=z(d), g_init=z(d), w_gu=z(d, d), b_gu=z(d), w_fa0=z(2 * d, (Lv + 1) * d), b_fa0=z(2 * d),
+                      w_fa2=z(d, 2 * d), b_fa2=z(d))
+        self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), ln1_w=z(d), ln1_b=z(d), w_gv=z(I, d), w_go=z(d, I),
+                        ln2_w=z(d), ln2_b=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d),
+                        ln3_b=z(d), w_proj=z(d, d), b_proj=z(d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
+        self.fbuf = dict(g=z(E, d), x1=z(E, d), x2=z(E, d), x3=z(E, d), mean=z(E, d), allf=z(E, (Lv + 1) * d),
+                         hagg=z(E, 2 * d))
+        self._pk_src += [(self.w, k) for k in ('w_gu', 'w_fa0', 'w_fa2')]
+        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_gv', 'w_go', 'w_ff1', 'w_ff2', 'w_proj')]
+
+    def _build_desc(self, clamp, hazard_log2):
+        super()._build_desc(clamp, hazard_log2)
+        self.desc.state_only = 1
+        Lv = self.levels
+        levels = (L.FractalLevel * Lv)()
+        names = [n for n, _ in L.FractalLevel._fields_]
+        for i, wl in enumerate(self.wl):
+            levels[i] = L.FractalLevel(*(self._wv(wl, k) for k in names))
+        F_ = L.FractalDesc()
+        F_.levels, F_.ln_eps = Lv, self.ln_eps
+        F_.level = C.cast(levels, C.POINTER(L.FractalLevel))
+        for k in ('g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2'):
+            setattr(F_, k, self._wv(self.w, k))
+        for k, t in self.fbuf.items():
+            setattr(F_, k, L.ptr(t))
+        self.fdesc, self._flevels = F_, levels
+
+    @torch.no_grad()
+    def pack(self, model, rs_mean, rs_var):
+        """Copy the (EMA) fractal body into the decode layout (fractal_rl.py:274-346 names)."""
+        w = self.w
+        enc = model.fractal_encoder
+        w['w_pin'].copy_(enc.input_embed.weight)
+        w['b_pin'].copy_(enc.input_embed.bias + model.level_embed(0))   # level 0's embedding folded in
+        self._pack_common(model, rs_mean, rs_var)
+        w['g_init'].copy_(enc.global_state_init.reshape(-1))
+        w['w_gu'].copy_(enc.global_state_update.weight)
+        w['b_gu'].copy_(enc.global_state_update.bias)
+        fa0, fa2 = enc.final_aggregation[0], enc.final_aggregation[2]
+        w['w_fa0'].copy_(fa0.weight)
+        w['b_fa0'].copy_(fa0.bias)
+        w['w_fa2'].copy_(fa2.weight)
+        w['b_fa2'].copy_(fa2.bias)
+        for li, wl in enumerate(self.wl):
+            blk = enc.get_fractal_block(li)
+            sa, ga = blk.self_attn, blk.global_attn
+            torch.cat((sa.to_q.weight, sa.to_k.weight, sa.to_v.weight), out=wl['w_qkv'])
+            wl['w_out'].copy_(sa.to_out.weight)
+            wl['w_gv'].copy_(ga.to_v.weight)
+            wl['w_go'].copy_(ga.to_out.weight)
+            for j, nm in ((1, blk.norm1), (2, blk.norm2), (3, blk.norm3)):
+                wl[f'ln{j}_w'].copy_(nm.weight)
+                wl[f'ln{j}_b'].copy_(nm.bias)
+            ff0, ff2 = blk.ff.ff[0][0], blk.ff.ff[2]
+            wl['w_ff1'].copy_(ff0.weight)
+            wl['b_ff1'].copy_(ff0.bias)
+            wl['w_ff2'].copy_(ff2.weight)
+            wl['b_ff2'].copy_(ff2.bias)
+            pj = enc.level_projections[li]
+            wl['w_proj'].copy_(pj.weight)
+            wl['b_proj'].copy_(pj.bias)
+            wl['level_emb'].copy_(model.level_embed(li))
+        self._pack_gemm_weights()
+
+    def step(self, t):
+        L.check(L.lib().xtrl_fractal_decode_step(C.byref(self.desc), C.byref(self.fdesc), int(t), L.stream()),
+                f'fractal_decode_step(t={t})')
+
+    def cache_tensors(self):
+        return [t for kv in self.kv for t in kv] + [wl['sums'] for wl in self.wl]
+
+
+def make_engine(model, E, Tmax, **kw):
+    """The rollout engine of a policy body: the decoder's or the fractal body's."""
+    cls = FractalRolloutEngine if getattr(model, 'levels', None) is not None else RolloutEngine
+    return cls(model, E, Tmax, **kw)
