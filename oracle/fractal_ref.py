@@ -226,9 +226,11 @@ class OracleFractalPolicy(nn.Module):
         from . import ref_port as R
         return R.safe_embed(self.action_embeds.embed.weight, actions)
 
-    def _step(self, s_t, cache):
+    def _step(self, s_t, cache, key_mask=None):
         """One position for every row: s_t [b, S]; cache holds per level the K / V rows so far
-        [b, H, t, dh] and the running sums of the level outputs [b, d]."""
+        [b, H, t, dh] and the running sums of the level outputs [b, d].  key_mask [b, t + 1]: the
+        key-padding mask of a padded minibatch (the learn step's attention masks keys past each
+        episode's length, as x-transformers' mask does for the decoder)."""
         enc = self.fractal_encoder
         b = s_t.shape[0]
         H, dh = self.heads, self.dim_head
@@ -244,7 +246,10 @@ class OracleFractalPolicy(nn.Module):
             K = k if t == 0 else torch.cat((cache['k'][li], k), dim=2)
             V = v if t == 0 else torch.cat((cache['v'][li], v), dim=2)
             cache['k'][li], cache['v'][li] = K, V
-            a = ((q @ K.transpose(-1, -2)) / math.sqrt(dh)).softmax(dim=-1) @ V
+            sim = (q @ K.transpose(-1, -2)) / math.sqrt(dh)
+            if key_mask is not None:
+                sim = sim.masked_fill(~key_mask[:, None, None, :], -torch.finfo(sim.dtype).max)
+            a = sim.softmax(dim=-1) @ V
             x1 = blk.norm1(x + sa.to_out(a.reshape(b, H * dh)))
             ga = blk.global_attn    # attention of the row over the one global-state token
             gq, gk, gv = ga.to_q(x1).view(b, H, 1, dh), ga.to_k(g).view(b, H, 1, dh), ga.to_v(g).view(b, H, 1, dh)
@@ -268,7 +273,11 @@ class OracleFractalPolicy(nn.Module):
         b, n, _ = state.shape
         if cache is None:
             cache = dict(t=0, k=[None] * self.levels, v=[None] * self.levels, sums=[None] * self.levels)
-        feats = torch.stack([self._step(state[:, i], cache) for i in range(n)], dim=1)
+        t0 = cache['t']
+        if mask is not None:
+            assert t0 == 0, 'a key-padding mask applies to a whole sequence'
+        feats = torch.stack([self._step(state[:, i], cache, None if mask is None else mask[:, :i + 1])
+                             for i in range(n)], dim=1)
         state_pred = dones = None
         if next_actions is not None:
             ewa = torch.cat((feats, self.embed_actions(next_actions)), dim=-1)

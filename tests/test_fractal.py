@@ -155,3 +155,61 @@ def test_fractal_world_model_matches_oracle(cont, evo):
         assert err <= 1e-4 * float(r.abs().max()) + 1e-6, (name, err)
     for a, r in zip(out[4]['fractal_levels'], ref[4]):
         assert float((a.double().cpu() - r).abs().max()) <= 1e-4 * float(r.abs().max()) + 1e-6
+
+
+# ----------------------------------------------------------------------------------------------
+# the causal fractal policy body (Agent(policy_body='fractal')): host-side checks
+# ----------------------------------------------------------------------------------------------
+
+def _policy_pair(levels=2, cont=False, evo=False, dim=32):
+    from oracle import ref_port as R
+    from xtrl_amd.fractal import FractalPolicyActorCritic
+    from xtrl_amd.model import ModelConfig
+    c = ModelConfig(state_dim=8, num_actions=4, dim=dim, depth=levels, heads=4, dim_head=8, continuous=cont,
+                    evolutionary=evo, dim_gene=8 if evo else 0, reward_range=(-2., 2.))
+    mc = R.ModelConfig(8, 4, dim, levels, 4, 8, 100, (-2., 2.), 100, cont, True, evo, 8 if evo else 0)
+    return FractalPolicyActorCritic(c, levels), FR.OracleFractalPolicy(mc, levels)
+
+
+@pytest.mark.parametrize('cont,evo', [(False, False), (True, True)])
+def test_policy_body_keeps_reference_names_and_oracle_layout(cont, evo):
+    """The Learner's fractal body is FractalWorldModelActorCritic's module tree (reference names,
+    separate blocks per level): its state_dict equals the reference class's and the oracle's."""
+    from xtrl_amd.fractal import FractalWorldModelActorCritic
+    ours, orc = _policy_pair(3, cont, evo)
+    ref = FractalWorldModelActorCritic(8, 4, 100, (-2., 2.), embed_dim=32, num_fractal_levels=3, heads=4, dim_head=8,
+                                       continuous_actions=cont, evolutionary=evo, dim_latent_gene=8 if evo else None)
+    shapes = lambda m: {k: tuple(v.shape) for k, v in m.state_dict().items()}   # noqa: E731
+    assert shapes(ours) == shapes(ref) == shapes(orc)
+    assert sorted(ours.flat_order()) == sorted(n for n, _ in ours.named_parameters())
+
+
+def test_policy_oracle_streaming_equals_whole_sequence_and_is_causal():
+    """Position t of the oracle depends on states 0..t only, and running it position by position
+    with the cache equals one call over the sequence (the rollout's and the learn step's views)."""
+    _, orc = _policy_pair(2, evo=True)
+    _rand_init(orc, 4)
+    g = torch.Generator().manual_seed(5)
+    st = torch.randn(3, 9, 8, generator=g, dtype=torch.float64)
+    lat = torch.randn(3, 8, generator=g, dtype=torch.float64)
+    orc = orc.double()
+    raw, val, *_ = orc(st, latent_gene=lat)
+    cache, outs = None, []
+    for t in range(9):
+        r, _, _, _, cache = orc(st[:, t:t + 1], latent_gene=lat, cache=cache)
+        outs.append(r)
+    torch.testing.assert_close(torch.cat(outs, 1), raw, rtol=1e-12, atol=1e-12)
+    st2 = st.clone()
+    st2[:, 5:] += 1.0                      # the future changes, the past does not
+    raw2, val2, *_ = orc(st2, latent_gene=lat)
+    torch.testing.assert_close(raw2[:, :5], raw[:, :5], rtol=0, atol=0)
+    torch.testing.assert_close(val2[:, :5], val[:, :5], rtol=0, atol=0)
+    assert float((raw2[:, 5:] - raw[:, 5:]).abs().max()) > 1e-3
+
+
+def test_policy_body_rejects_decoder_only_options():
+    from xtrl_amd import Learner
+    with pytest.raises(NotImplementedError):
+        Learner(state_dim=8, num_actions=4, reward_range=(-1., 1.), batch_size=2, num_episodes_per_update=2,
+                world_model=dict(attn_dim_head=16, heads=4, depth=2, attn_gate_values=True),
+                agent_kwargs=dict(policy_body='fractal'))

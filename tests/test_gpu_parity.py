@@ -467,8 +467,8 @@ def test_fractal_forward_train_ragged_matches_oracle():
     om.eval()
     agent.flat.zero_grad()
     outs = model.forward_train(state.cuda(), None, None, nxt.cuda(), lat.cuda(), lens.cuda())
-    ref = om(state, next_actions=nxt, latent_gene=lat)
     mask = (torch.arange(n)[None] < lens[:, None].long())
+    ref = om(state, next_actions=nxt, latent_gene=lat, mask=mask)
     for name, a, r in zip(('raw_actions', 'values'), outs[:2], ref[:2]):
         a = a.detach().cpu()[mask]
         r = r.detach()[mask]
@@ -477,8 +477,8 @@ def test_fractal_forward_train_ragged_matches_oracle():
     sum((o * wi.cuda()).sum() for o, wi in zip(outs, w)).backward()
     # oracle side: the same functional of (raw_actions, values, pred_raw, done_logit)
     om.zero_grad()
-    ref = om(state, next_actions=nxt, latent_gene=lat)
-    (sum((o * wi).sum() for o, wi in zip((ref[0], ref[1]) + _oracle_wm_raw(om, state, nxt), w))).backward()
+    ref = om(state, next_actions=nxt, latent_gene=lat, mask=mask)
+    (sum((o * wi).sum() for o, wi in zip((ref[0], ref[1]) + _oracle_wm_raw(om, state, nxt, mask), w))).backward()
     gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
     scale = max(float(p.grad.abs().max()) for p in om.parameters() if p.grad is not None)
     for name, p in om.named_parameters():
@@ -488,11 +488,11 @@ def test_fractal_forward_train_ragged_matches_oracle():
         assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
 
 
-def _oracle_wm_raw(om, state, nxt):
+def _oracle_wm_raw(om, state, nxt, mask):
     """(pred_raw, done_logit) of the oracle fractal policy — the world-model heads before the
     mean / variance split and the sigmoid (forward_train's outputs 3 and 4)."""
     cache = dict(t=0, k=[None] * om.levels, v=[None] * om.levels, sums=[None] * om.levels)
-    feats = torch.stack([om._step(state[:, i], cache) for i in range(state.shape[1])], dim=1)
+    feats = torch.stack([om._step(state[:, i], cache, mask[:, :i + 1]) for i in range(state.shape[1])], dim=1)
     ewa = torch.cat((feats, om.embed_actions(nxt)), dim=-1)
     return om.to_pred(ewa), om.to_pred_done(ewa)[..., 0]
 
@@ -1050,10 +1050,13 @@ def test_host_env_scalar_contract_matches_oracle(ret, limit):
         assert any(ep['boot'] is not None for ep in episodes)     # some episodes truncated
 
 
-def test_host_env_vectorised_waves_match_oracle():
+@pytest.mark.parametrize('frac', [None, 2])
+def test_host_env_vectorised_waves_match_oracle(frac):
     """A vectorised env of 4 sub-envs over 2 genes x 5 episodes (10 pairs: waves of 4, 4, 2 — the
-    last one partial), evolutionary with per-episode reset seeds, truncation at 6 steps."""
-    learner, _, oracle = make_learner(depth=2, gates=True, evo=True, T=8, episodes=5, batch=5)
+    last one partial), evolutionary with per-episode reset seeds, truncation at 6 steps (the
+    truncation bootstrap step included); decoder and fractal policy bodies."""
+    learner, _, oracle = make_learner(depth=2, gates=frac is None, evo=True, T=8, episodes=5, batch=5,
+                                      fractal_levels=frac)
     seeds = torch.randint(0, 10 ** 7, (5,), generator=torch.Generator().manual_seed(3))
     _, _, genes, cum, episodes, fitness = _compare_host(learner, oracle, HostLanderVec(4, limit=6),
                                                         HostLander(limit=6), 8, seeds)
