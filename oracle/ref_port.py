@@ -660,7 +660,7 @@ class OracleLearner:
                     self.genes, _ = evolve(self.genes, fitness, gp['num_islands'], gp['num_selected'],
                                            gp['tournament_size'], step=self.gp_step)
                     self.gp_step += 1
-                self.logs.append({k: float(v) for k, v in logs.items()} | dict(loss=float(loss.detach())))
+                self.logs.append({k: float(v.detach()) for k, v in logs.items()} | dict(loss=float(loss.detach())))
         self.rsnorm = rs_copy
         self.step += 1
 

@@ -27,6 +27,7 @@
 // Layouts in HBM: per-step activations are [live row][.] row-major; KV caches [E][H][Tmax][dh]
 // (per episode slot) so one (episode, head) streams a contiguous Tmax*dh block; trajectories
 // [E][Tmax][.] so the learner reads whole episodes contiguously.
+#include "dgemm_body.h"
 #include "kernels.h"
 #include "philox.h"
 
@@ -80,10 +81,17 @@ __global__ __launch_bounds__(1024) void k_compact(const XtrlDecodeDesc D, int t)
 // ---------------------------------------------------------------------------------------------
 constexpr int EMB_ROWS = 16;
 constexpr int EMB_LDS_FLOATS = 8192;   // 2 d S <= 8192 (C3: 4096); larger: weights read from global
-template <int NC>   // columns per lane: lane + 64 k, k < NC (d <= 64 NC)
+constexpr int EMB_MAX_E = 8192;        // E up to this: the compaction runs inside k_embed (CMP)
+// CMP: every workgroup ranks the live slots itself (one load of the alive bytes, ballots, an LDS
+// scan — the same slot order as k_compact) and stores its own rows' entries of live_rows[t & 1];
+// workgroup 0 stores live_count[t & 1].  No separate compaction launch, and the embedding's
+// first dependent load (the live count) is gone.  Otherwise k_compact ran before.
+template <int NC, bool CMP>   // columns per lane: lane + 64 k, k < NC (d <= 64 NC)
 __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
   __shared__ float wsh[EMB_LDS_FLOATS];
   __shared__ float ns_sh[EMB_ROWS][64];
+  __shared__ int rows_sh[CMP ? EMB_MAX_E : 1];
+  __shared__ int wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int S = D.S, d = D.d, dS = d * S;
   const bool staged = 2 * dS <= EMB_LDS_FLOATS;
@@ -97,6 +105,37 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
       wv[1][u] = reinterpret_cast<const float4*>(D.w_se)[f];
     }
   }
+  int n_live = 0;   // (CMP: the live count, the same in every thread)
+  if constexpr (CMP) {   // rank the live slots (alive != 0) in slot order
+    uint8_t alv[EMB_MAX_E / 1024];
+#pragma unroll
+    for (int c = 0; c < EMB_MAX_E / 1024; ++c) {
+      const int e = min(1024 * c + tid, D.E - 1);
+      alv[c] = D.alive[e];
+    }
+    int base = 0;
+#pragma unroll
+    for (int c = 0; c < EMB_MAX_E / 1024; ++c) {
+      if (1024 * c >= D.E) break;   // (uniform)
+      const int e = 1024 * c + tid;
+      const bool al = e < D.E && alv[c] != 0;
+      const uint64_t bal = __ballot(al);
+      if (lane == 0) wsum[w] = __popcll(bal);
+      __syncthreads();
+      int off = base, tot = 0;
+      for (int i = 0; i < 16; ++i) {
+        off += i < w ? wsum[i] : 0;
+        tot += wsum[i];
+      }
+      if (al) rows_sh[off + __popcll(bal & ((1ull << lane) - 1ull))] = e;
+      base += tot;
+      __syncthreads();
+    }
+    const int r = blockIdx.x * EMB_ROWS + tid;
+    if (tid < EMB_ROWS && r < base) D.live_rows[(t & 1) * D.E + r] = rows_sh[r];
+    if (blockIdx.x == 0 && tid == 0) D.live_count[t & 1] = base;
+    n_live = base;
+  }
   // per-column constants of this lane
   float remb[NC], bse[NC], bpin[NC];
 #pragma unroll
@@ -106,7 +145,7 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
     bse[k] = D.b_se[c];
     bpin[k] = D.b_pin ? D.b_pin[c] : 0.f;
   }
-  const int n = D.live_count[t & 1];
+  const int n = CMP ? n_live : D.live_count[t & 1];
   const int r0 = blockIdx.x * EMB_ROWS;
   if (r0 >= n) return;   // (whole workgroup)
   if (staged) {
@@ -126,7 +165,7 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
   __syncthreads();
   const int r = r0 + w;
   if (r >= n) return;   // wave-uniform
-  const int e = D.live_rows[(t & 1) * D.E + r];
+  const int e = CMP ? rows_sh[r] : D.live_rows[(t & 1) * D.E + r];
   float* ns = ns_sh[w];
   // RSNorm eval on the packed [state, prev_reward] vector: (x - mean) / clamp(sqrt(var), eps)
   const float xv = lane < S ? D.state[(int64_t)e * S + lane] : D.prev_reward[e];
@@ -365,21 +404,34 @@ __device__ __forceinline__ float reward_factor(int a) { return (float)(1.0 + 0.1
 // (lane i), the sampling uniform (lane 0), the Sim's reward normal (lane 1) and termination word
 // (lane 2); lane 0 then samples the action and finishes the Sim step.
 constexpr int SAMPLE_L = 8;
-__global__ __launch_bounds__(256) void k_sample(const XtrlDecodeDesc D, int t) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int r = gid / SAMPLE_L, sub = gid % SAMPLE_L;
-  if (r >= D.live_count[t & 1]) return;   // (whole rows: SAMPLE_L divides the wave)
-  const int e = rows_of(D, t)[r];
-  const XtrlRngState R = *D.rng;
-  // one batch of independent loads (latency bound kernel)
-  const int al = D.alive[e];   // (every lane of the row reads alive before lane 0 clears it)
-  const uint32_t ep = D.sim_mode >= 0 ? (uint32_t)D.episode_of_slot[e] : 0u;
-  const uint32_t slot = D.slot_of_row ? (uint32_t)D.slot_of_row[e] : R.slot_offset + (uint32_t)e;
-  const double cum = D.cum_reward[e];
-  const int A = D.A, n_act = D.continuous ? 2 * A : A;
-  __shared__ float lg_sh[256 / SAMPLE_L][64];
-  float* lg = lg_sh[threadIdx.x / SAMPLE_L];
-  for (int o = sub; o < n_act; o += SAMPLE_L) lg[o] = D.logits[(int64_t)r * n_act + o];
+
+// per-row inputs of the sampling / Sim step, loaded in one batch
+struct SampleIn {
+  XtrlRngState R;
+  int al;
+  uint32_t ep, slot;
+  double cum;
+};
+__device__ __forceinline__ SampleIn sample_load(const XtrlDecodeDesc& D, int e) {
+  SampleIn in;
+  in.R = *D.rng;
+  in.al = D.alive[e];   // (every lane of the row reads alive before lane 0 clears it)
+  in.ep = D.sim_mode >= 0 ? (uint32_t)D.episode_of_slot[e] : 0u;
+  in.slot = D.slot_of_row ? (uint32_t)D.slot_of_row[e] : 0u;
+  in.cum = D.cum_reward[e];
+  return in;
+}
+
+// the sample and the Sim step of one live row (slot e) by its SAMPLE_L lanes (sub = lane of the
+// row's aligned group, every lane of the group active); lg = the row's actor outputs in LDS
+__device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e, int sub, const float* lg,
+                                           const SampleIn& in) {
+  const XtrlRngState& R = in.R;
+  const int al = in.al;
+  const uint32_t ep = in.ep;
+  const uint32_t slot = D.slot_of_row ? in.slot : R.slot_offset + (uint32_t)e;
+  const double cum = in.cum;
+  const int A = D.A;
   // random numbers of the step, spread over the row's lanes
   float u = 0.f, zr = 0.f;
   uint32_t tw = 0u;
@@ -394,7 +446,6 @@ __global__ __launch_bounds__(256) void k_sample(const XtrlDecodeDesc D, int t) {
   const int base = (threadIdx.x & 63) & ~(SAMPLE_L - 1);
   zr = __shfl(zr, base + 1, 64);
   tw = __shfl(tw, base + 2, 64);
-  wave_sync();
   if (sub != 0) return;
   if (al == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
     D.alive[e] = 0;
@@ -450,6 +501,63 @@ __global__ __launch_bounds__(256) void k_sample(const XtrlDecodeDesc D, int t) {
     D.lens[e] = t + 1;
     if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
   }
+}
+
+// SAMPLE_L lanes per row (a wave holds whole rows).  The row's lanes stage its logits in LDS and
+// draw its random numbers in parallel (none depends on the action): the next state's S normals
+// (lane i), the sampling uniform (lane 0), the Sim's reward normal (lane 1) and termination word
+// (lane 2); lane 0 then samples the action and finishes the Sim step.  (Used where the head
+// projection and the sampling are not fused: n_act > 64.)
+__global__ __launch_bounds__(256) void k_sample(const XtrlDecodeDesc D, int t) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = gid / SAMPLE_L, sub = gid % SAMPLE_L;
+  if (r >= D.live_count[t & 1]) return;   // (whole rows: SAMPLE_L divides the wave)
+  const int e = rows_of(D, t)[r];
+  const SampleIn in = sample_load(D, e);
+  const int n_act = D.continuous ? 2 * D.A : D.A;
+  __shared__ float lg_sh[256 / SAMPLE_L][64];
+  float* lg = lg_sh[threadIdx.x / SAMPLE_L];
+  for (int o = sub; o < n_act; o += SAMPLE_L) lg[o] = D.logits[(int64_t)r * n_act + o];
+  wave_sync();
+  sample_row(D, t, e, sub, lg, in);
+}
+
+// the heads' last projection (block-diagonal [actor | critic], 16-row panels) with the sampling of
+// its rows fused: the column-block-0 workgroups hold every actor output of their 16 rows (n_act <=
+// 64), keep them in LDS and run sample_row for each row (SAMPLE_L lanes per row, the per-row
+// inputs prefetched with the GEMM operands) — no sampling launch, no logits round trip
+struct SampleHook {
+  const XtrlDecodeDesc& D;
+  int t, n_act;
+  bool on;
+  float (*lg)[64];
+  int row, sub, e;
+  SampleIn in;
+  // the row's slot first (its load lands with the GEMM operands), the loads that depend on it
+  // once they have landed (in flight during the MFMA loop)
+  __device__ __forceinline__ void prefetch(int m0, int M) {
+    row = threadIdx.x / SAMPLE_L;
+    sub = threadIdx.x % SAMPLE_L;
+    if (on && row < 16) e = rows_of(D, t)[min(m0 + row, M - 1)];
+  }
+  __device__ __forceinline__ void landed() {
+    if (on && row < 16) in = sample_load(D, e);
+  }
+  __device__ __forceinline__ void value(int r, int n, float v) {
+    if (on && n < n_act) lg[r][n] = v;
+  }
+  __device__ __forceinline__ void finish(int m0, int M) {
+    if (!on) return;   // (workgroup-uniform)
+    __syncthreads();
+    if (row < 16 && m0 + row < M) sample_row(D, t, e, sub, lg[row], in);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_heads_sample(const DGemmArgs a, const XtrlDecodeDesc D, int t) {
+  extern __shared__ float As[];
+  __shared__ float lg_sh[16][64];
+  SampleHook hook{D, t, D.continuous ? 2 * D.A : D.A, blockIdx.x == 0, lg_sh};
+  dgemm_body<1, 1, EPI_NONE, false, false>(a, As, hook);
 }
 
 // host env results of step t (xtrl.py:1297-1336): the memory stores is_boundary = terminated;
@@ -530,6 +638,30 @@ int check_desc(const XtrlDecodeDesc* D) {
   return XTRL_OK;
 }
 
+// compaction (inside the embedding for E <= EMB_MAX_E) + embeddings of step t
+template <bool CMP>
+void launch_embed_t(const XtrlDecodeDesc* D, int t, hipStream_t s) {
+  const dim3 grid((D->E + EMB_ROWS - 1) / EMB_ROWS), blk(1024);
+  switch ((D->d + 63) / 64) {
+    case 1: hipLaunchKernelGGL((k_embed<1, CMP>), grid, blk, 0, s, *D, t); break;
+    case 2: hipLaunchKernelGGL((k_embed<2, CMP>), grid, blk, 0, s, *D, t); break;
+    case 3: hipLaunchKernelGGL((k_embed<3, CMP>), grid, blk, 0, s, *D, t); break;
+    case 4: hipLaunchKernelGGL((k_embed<4, CMP>), grid, blk, 0, s, *D, t); break;
+    default: hipLaunchKernelGGL((k_embed<8, CMP>), grid, blk, 0, s, *D, t); break;
+  }
+}
+int launch_embed(const XtrlDecodeDesc* D, int t, hipStream_t s) {
+  if (D->E <= EMB_MAX_E) {
+    launch_embed_t<true>(D, t, s);
+  } else {
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
+    XTRL_LAUNCHED("compact");
+    launch_embed_t<false>(D, t, s);
+  }
+  XTRL_LAUNCHED("embed");
+  return XTRL_OK;
+}
+
 int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
   const int waves = D->E * D->H;
   const size_t lds = 4 * (size_t)(D->Tmax + 3 * D->dh) * sizeof(float);
@@ -570,6 +702,19 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
                   final_norm ? d : 0, nullptr, 0, D->hff, 4 * d, 4 * d, EPI_SILU, s)))
     return rc;
   const int n_act = D->continuous ? 2 * D->A : D->A;
+  if (n_act <= 64) {   // block-diagonal projection + sampling in one launch
+    DGemmArgs g;
+    g.A = D->hff; g.lda = 4 * d; g.W = D->w_h2; g.ldw = 4 * d; g.bias = D->b_h2;
+    g.C = D->logits; g.ldc = n_act; g.n_split = n_act;
+    g.C2 = D->traj_values + (int64_t)t * D->B; g.ldc2 = D->Tmax * D->B; g.row_map2 = D->live_rows + (t & 1) * E;
+    g.m_dev = D->live_count + (t & 1); g.M = E; g.N = n_act + D->B; g.K = 4 * d;
+    XTRL_REQUIRE(g.K % 4 == 0 && g.K <= 2048, "decode heads: 4 d must be a multiple of 4, at most 2048");
+    const dim3 grid((g.N + 63) / 64, (E + 15) / 16);
+    const size_t lds = (size_t)16 * (dg_kp(g.K) + 4) * sizeof(float);
+    hipLaunchKernelGGL(k_heads_sample, grid, dim3(256), lds, s, g, *D, t);
+    XTRL_LAUNCHED("heads_sample");
+    return XTRL_OK;
+  }
   if ((rc = dproj(D, t, D->hff, 4 * d, D->w_h2, 4 * d, D->b_h2, nullptr, 0, nullptr, 0, D->logits, n_act,
                   n_act + D->B, EPI_NONE, s, nullptr, n_act, D->traj_values + (int64_t)t * D->B, D->Tmax * D->B,
                   D->live_rows + (t & 1) * E)))
@@ -584,21 +729,9 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
 int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode: t=%d outside [0, %d)", t, D->Tmax);
-  const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff;
-  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
-  XTRL_LAUNCHED("compact");
-  {
-    const dim3 grid((E + EMB_ROWS - 1) / EMB_ROWS), blk(1024);
-    switch ((d + 63) / 64) {
-      case 1: hipLaunchKernelGGL(k_embed<1>, grid, blk, 0, s, *D, t); break;
-      case 2: hipLaunchKernelGGL(k_embed<2>, grid, blk, 0, s, *D, t); break;
-      case 3: hipLaunchKernelGGL(k_embed<3>, grid, blk, 0, s, *D, t); break;
-      case 4: hipLaunchKernelGGL(k_embed<4>, grid, blk, 0, s, *D, t); break;
-      default: hipLaunchKernelGGL(k_embed<8>, grid, blk, 0, s, *D, t); break;
-    }
-  }
-  XTRL_LAUNCHED("embed");
+  const int d = D->d, I = D->H * D->dh, ff = D->ff;
   int rc;
+  if ((rc = launch_embed(D, t, s))) return rc;
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
     if ((rc = dproj(D, t, D->x, d, Ly.w_qkv, d, Ly.b_qkv, Ly.ln_attn, d, nullptr, 0, D->qkv, D->n_qkv, D->n_qkv,
@@ -628,10 +761,7 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
                "fractal_decode: the descriptor must describe plain attention (n_qkv = 3 I) with state_only = 1");
   const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels;
   const int64_t Ed = (int64_t)E * d;
-  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
-  XTRL_LAUNCHED("compact");
-  hipLaunchKernelGGL(k_embed<8>, dim3((E + EMB_ROWS - 1) / EMB_ROWS), dim3(1024), 0, s, *D, t);   // x = W_in s + b_in + le_0
-  XTRL_LAUNCHED("embed");
+  if (int rc = launch_embed(D, t, s)) return rc;   // x = W_in s + b_in + le_0
   rows_add_launch(nullptr, 0, F->g_init, F->g, d, E, d, s);   // per-step global state of every row starts at init
   XTRL_LAUNCHED("rows_add");
   int rc;
