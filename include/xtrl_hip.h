@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 6
+#define XTRL_ABI_VERSION 7
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -87,6 +87,9 @@ typedef struct XtrlDecodeLayer {
   const float* b_ff2;    /* [d] */
   float* k_cache;        /* [E][H][Tmax][dh]  keys (post-rotary) */
   float* v_cache;        /* [E][H][Tmax][dh]  values (post value-residual mix) */
+  const float* w_out_t;  /* [I][d]  to_out transposed (plain fp32), or NULL: when set (and the shape
+                            allows) the attention kernel applies the out-projection + residual
+                            itself, x += W_out o, and no out-projection GEMM runs */
 } XtrlDecodeLayer;
 
 typedef struct XtrlRngState {   /* device memory; read by the sampling / sim kernels */

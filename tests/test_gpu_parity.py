@@ -795,7 +795,7 @@ def _first_minibatch(agent, traj, lens, genes, fit):
     out = {}
 
     def probe(epoch, mbi, idx, loss, stats):
-        out['loss'] = float(loss)
+        out['loss'] = float(loss.detach())
         out['grad'] = agent.flat.grad.detach().clone()
         raise _Captured()
 

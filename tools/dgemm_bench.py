@@ -27,6 +27,14 @@ CASES = [  # name, M(live), N, K, ln, act, res
     ('ff2', 1024, 256, 1024, False, 0, True),
     ('h1', 1024, 1024, 512, True, 2, False),
     ('h2', 1024, 104, 1024, False, 0, False),
+    ('ff1-440-noln', 440, 1024, 256, False, 1, False),
+    ('ff1-440-lnonly', 440, 1024, 256, True, 0, False),
+    ('ff1-440-plain', 440, 1024, 256, False, 0, False),
+    ('qkv-440-noln', 440, 260, 256, False, 0, False),
+    ('ff2-440', 440, 256, 1024, False, 0, True),
+    ('out-440', 440, 256, 64, False, 0, True),
+    ('h1-440', 440, 1024, 512, True, 2, False),
+    ('h1-440-noln', 440, 1024, 512, False, 2, False),
 ]
 
 

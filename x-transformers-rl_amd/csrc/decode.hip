@@ -230,20 +230,38 @@ __device__ __forceinline__ float kpi_sum(float v) {
   return v;
 }
 
-template <int DH>
-__global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int layer,
-                                                     int t) {
+// FUSE: one workgroup per live row (H waves), and the out-projection + residual applied here:
+// wave h multiplies its head's output by rows [h DH, (h+1) DH) of W_out^T (prefetched with the
+// cache rows: float4 columns 4 lane + 256 j), the H partial rows meet in LDS and are summed in head
+// order onto the residual row x[r] — the out-projection GEMM launch of the layer is gone.
+// FJ = ceil(d / 256) float4 column groups per lane (FJ = 0: not fused, the output goes to D.att)
+template <int DH, int FJ>
+__global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int layer,
+                                                      int t) {
   constexpr int CK = DH <= 32 ? 128 : 64;          // keys per chunk
   constexpr int KL = CK / 64, F4 = DH / 4;         // keys per lane (scores), float4 per key row
   constexpr int LPK = DH / 4, KPI = 64 / LPK;      // P.V: lanes per key row, keys per load instruction
   constexpr int VU = CK / KPI;                     // V loads per lane per chunk
   extern __shared__ float smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int idx = blockIdx.x * 4 + w;
-  const int H = D.H, I = H * DH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int idx = blockIdx.x * nw + w;
+  const int H = D.H, I = H * DH, d = D.d;
   const int r = idx / H, h = idx - r * H;
-  if (r >= D.live_count[t & 1]) return;   // wave-uniform
+  if (r >= D.live_count[t & 1]) return;   // wave-uniform (FUSE: workgroup-uniform)
+  constexpr bool FUSE = FJ > 0;
   const int e = rows_of(D, t)[r];
+  // fused out-projection operands: this head's rows of W_out^T and the residual row
+  float4 wt[FUSE ? FJ : 1][FUSE ? DH : 1];
+  float4 xres = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int c = 0; c < DH; ++c)
+        wt[j][c] = *reinterpret_cast<const float4*>(Ly.w_out_t + (int64_t)(h * DH + c) * d +
+                                                    min(4 * lane + 256 * j, d - 4));
+    if (4 * (int)threadIdx.x < d) xres = *reinterpret_cast<const float4*>(D.x + (int64_t)r * d + 4 * threadIdx.x);
+  }
   float* sc = smem + w * (D.Tmax + 3 * DH);   // scores / probabilities [Tmax] | q | k_new | v_new
   float* qs = sc + D.Tmax;
   float* ks = qs + DH;
@@ -390,7 +408,39 @@ __global__ __launch_bounds__(256) void k_attn_decode(const XtrlDecodeDesc D, con
 #pragma unroll
       for (int i = 0; i < 4; ++i) o4[i] *= sigmoidf_(gate4[i]);
     }
-    *reinterpret_cast<float4*>(D.att + (int64_t)r * I + h * DH + 4 * cq) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+    if constexpr (FUSE) *reinterpret_cast<float4*>(qs + 4 * cq) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+    else *reinterpret_cast<float4*>(D.att + (int64_t)r * I + h * DH + 4 * cq) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+  }
+  if constexpr (FUSE) {
+    wave_sync();
+    float* part = smem + nw * (D.Tmax + 3 * DH);   // [H][d] partial output rows
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) {
+      const int n = 4 * lane + 256 * j;
+      float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        const float o = qs[c];
+        y.x += o * wt[j][c].x;
+        y.y += o * wt[j][c].y;
+        y.z += o * wt[j][c].z;
+        y.w += o * wt[j][c].w;
+      }
+      if (n < d) *reinterpret_cast<float4*>(part + h * d + n) = y;
+    }
+    __syncthreads();
+    const int n = 4 * threadIdx.x;
+    if (n < d) {
+      float4 y = xres;
+      for (int hh = 0; hh < H; ++hh) {
+        const float4 p = *reinterpret_cast<const float4*>(part + hh * d + n);
+        y.x += p.x;
+        y.y += p.y;
+        y.z += p.z;
+        y.w += p.w;
+      }
+      *reinterpret_cast<float4*>(D.x + (int64_t)r * d + n) = y;
+    }
   }
 }
 
@@ -662,17 +712,33 @@ int launch_embed(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   return XTRL_OK;
 }
 
+// whether layer l's attention launch applies its out-projection + residual (k_attn_decode FUSE)
+bool attn_fused(const XtrlDecodeDesc* D, int l) {
+  const size_t lds = ((size_t)D->H * (D->Tmax + 3 * D->dh) + (size_t)D->H * D->d) * sizeof(float);
+  // (dh = 16 only: the dh = 32 forms would spill the prefetched W_out^T rows)
+  return D->layers[l].w_out_t && D->dh == 16 && D->H <= 8 && D->d % 4 == 0 && D->d <= 512 &&
+         D->d <= 4 * 64 * D->H && lds <= 160 * 1024;
+}
+
 int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
+  if (attn_fused(D, l)) {   // one workgroup of H waves per live row
+    const size_t lds = ((size_t)D->H * (D->Tmax + 3 * D->dh) + (size_t)D->H * D->d) * sizeof(float);
+    const dim3 grid(D->E), blk(64 * D->H);
+    if (D->d > 256) hipLaunchKernelGGL((k_attn_decode<16, 2>), grid, blk, lds, s, *D, D->layers[l], l, t);
+    else hipLaunchKernelGGL((k_attn_decode<16, 1>), grid, blk, lds, s, *D, D->layers[l], l, t);
+    XTRL_LAUNCHED("attn_decode");
+    return XTRL_OK;
+  }
   const int waves = D->E * D->H;
   const size_t lds = 4 * (size_t)(D->Tmax + 3 * D->dh) * sizeof(float);
   XTRL_REQUIRE(lds <= 160 * 1024, "attn_decode: Tmax %d too large for LDS", D->Tmax);
   dim3 grid((waves + 3) / 4);
   if (D->dh == 16)
-    hipLaunchKernelGGL(k_attn_decode<16>, grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<16, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
   else if (D->dh == 32)
-    hipLaunchKernelGGL(k_attn_decode<32>, grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<32, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
   else
-    hipLaunchKernelGGL(k_attn_decode<64>, grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<64, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
   XTRL_LAUNCHED("attn_decode");
   return XTRL_OK;
 }
@@ -740,7 +806,9 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
-    if ((rc = dproj(D, t, D->att, I, Ly.w_out, I, nullptr, nullptr, 0, D->x, d, D->x, d, d, EPI_NONE, s))) return rc;
+    if (!attn_fused(D, l) &&
+        (rc = dproj(D, t, D->att, I, Ly.w_out, I, nullptr, nullptr, 0, D->x, d, D->x, d, d, EPI_NONE, s)))
+      return rc;
     if ((rc = dproj(D, t, D->x, d, Ly.w_ff1, d, Ly.b_ff1, Ly.ln_ff, d, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
       return rc;
     // the last layer's output goes straight into the heads' input row (final norm in their prologue)
@@ -755,6 +823,8 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
 int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(F && F->level && F->levels == D->L && F->levels > 0, "fractal_decode: levels mismatch");
+  for (int l = 0; l < D->L; ++l)
+    XTRL_REQUIRE(!D->layers[l].w_out_t, "fractal_decode: the attention output feeds a LayerNorm (w_out_t must be NULL)");
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "fractal_decode: t=%d outside [0, %d)", t, D->Tmax);
   XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs &&
                    D->n_qkv == 3 * D->H * D->dh && D->d <= 512,

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -28,7 +28,7 @@ LOSS_TOK, LOSS_STATS = 30, 32
 
 class DecodeLayer(C.Structure):
     _fields_ = [(n, P) for n in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2',
-                                 'k_cache', 'v_cache')]
+                                 'k_cache', 'v_cache', 'w_out_t')]
 
 
 class RngState(C.Structure):

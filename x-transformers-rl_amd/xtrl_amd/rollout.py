@@ -77,8 +77,9 @@ class RolloutEngine:
         """Per-layer decoder weights (self.wl) and their packed GEMM operands."""
         c = self.c
         d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
-        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), ln_ff=z(d),
-                        w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+        # w_out_t: to_out transposed for the attention kernel's fused out-projection
+        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), w_out_t=z(I, d),
+                        ln_ff=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
         self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
 
     def _wv(self, src, k):
@@ -93,7 +94,8 @@ class RolloutEngine:
         layers = (L.DecodeLayer * c.depth)()
         for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
             layers[i] = L.DecodeLayer(*(self._wv(w, k) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
-                                                                 'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc))
+                                                                 'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc),
+                                      self._wv(w, 'w_out_t'))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -152,6 +154,7 @@ class RolloutEngine:
             torch.cat(rows, out=wl['w_qkv'])
             torch.cat(bias, out=wl['b_qkv'])
             wl['w_out'].copy_(blk.to_out.weight)
+            wl['w_out_t'].copy_(blk.to_out.weight.t())
             wl['ln_ff'].copy_(ln_f.gamma)
             wl['w_ff1'].copy_(ffb.ff[0][0].weight)
             wl['b_ff1'].copy_(ffb.ff[0][0].bias)
