@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 7
+#define XTRL_ABI_VERSION 8
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -154,6 +154,9 @@ typedef struct XtrlDecodeDesc {
   float* ac_in;  /* [E][in_dim]  (final-normed embed | state embed | latent embed) */
   float* logits; /* [E][A or 2A] */
   float* v1;     /* [E][I] first layer's values (value residual) */
+  float* xn;     /* [E][d] or NULL: LayerNorm(x) * gain of the next projection, written by the kernel
+                    that completes the row (the embedding for layer 0's q|k|v, the fused attention
+                    for FF1), so that projection runs without a LayerNorm prologue */
   /* live-row compaction: the step-t kernels run over rows 0..live_count[t & 1]-1 only; row r is
    * episode slot live_rows[(t & 1) * E + r] (written by the step's embedding kernel) */
   int32_t* live_rows;        /* [2][E] */

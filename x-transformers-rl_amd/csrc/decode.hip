@@ -87,7 +87,7 @@ constexpr int EMB_MAX_E = 8192;        // E up to this: the compaction runs insi
 // workgroup 0 stores live_count[t & 1].  No separate compaction launch, and the embedding's
 // first dependent load (the live count) is gone.  Otherwise k_compact ran before.
 template <int NC, bool CMP>   // columns per lane: lane + 64 k, k < NC (d <= 64 NC)
-__global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
+__global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, const float* g_ln0) {
   __shared__ float wsh[EMB_LDS_FLOATS];
   __shared__ float ns_sh[EMB_ROWS][64];
   __shared__ int rows_sh[CMP ? EMB_MAX_E : 1];
@@ -137,13 +137,14 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
     n_live = base;
   }
   // per-column constants of this lane
-  float remb[NC], bse[NC], bpin[NC];
+  float remb[NC], bse[NC], bpin[NC], gln[NC];
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
     const int c = min(lane + 64 * k, d - 1);
     remb[k] = D.reward_embed[c];
     bse[k] = D.b_se[c];
     bpin[k] = D.b_pin ? D.b_pin[c] : 0.f;
+    gln[k] = g_ln0 ? g_ln0[c] : 0.f;
   }
   const int n = CMP ? n_live : D.live_count[t & 1];
   const int r0 = blockIdx.x * EMB_ROWS;
@@ -193,9 +194,11 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
   }
   wave_sync();
   const float nr = ns[S];
+  float xo[NC];
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
     const int c = lane + 64 * k;
+    xo[k] = 0.f;
     if (c >= d) break;
     float p = 0.f, se = 0.f;
     for (int sidx = 0; sidx < S; ++sidx) {
@@ -207,9 +210,28 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t) {
     p += bpin[k];
     const float ak = D.state_only ? 0.f : ((D.continuous || a >= 0) ? act[k] : 0.f);   // SafeEmbedding: -1 -> 0
     const float rew = (D.no_reward_cond || D.state_only) ? 0.f : nr * remb[k];
-    D.x[(int64_t)r * d + c] = p + (ak + rew);
+    xo[k] = p + (ak + rew);
+    D.x[(int64_t)r * d + c] = xo[k];
     D.ac_in[(int64_t)r * D.in_dim + d + c] = se + bse[k];
     if (D.evolutionary && D.lat_embed) D.ac_in[(int64_t)r * D.in_dim + 2 * d + c] = lat[k];
+  }
+  if (g_ln0 && D.xn) {   // layer 0's pre-attention LayerNorm (two-pass, as the GEMM prologue)
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) sm += lane + 64 * k < d ? xo[k] : 0.f;
+    const float mean = wave_sum_dpp(sm) / (float)d;
+    float qq = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const float dl = xo[k] - mean;
+      qq += lane + 64 * k < d ? dl * dl : 0.f;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < d) D.xn[(int64_t)r * d + c] = ((xo[k] - mean) * rstd) * gln[k];
+    }
   }
 }
 
@@ -252,15 +274,19 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
   const int e = rows_of(D, t)[r];
   // fused out-projection operands: this head's rows of W_out^T and the residual row
   float4 wt[FUSE ? FJ : 1][FUSE ? DH : 1];
-  float4 xres = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 xres[FUSE ? FJ : 1], gff[FUSE ? FJ : 1];   // wave 0: the residual row and FF1's LayerNorm gain
   if constexpr (FUSE) {
 #pragma unroll
-    for (int j = 0; j < FJ; ++j)
+    for (int j = 0; j < FJ; ++j) {
+      const int n = min(4 * lane + 256 * j, d - 4);
 #pragma unroll
       for (int c = 0; c < DH; ++c)
-        wt[j][c] = *reinterpret_cast<const float4*>(Ly.w_out_t + (int64_t)(h * DH + c) * d +
-                                                    min(4 * lane + 256 * j, d - 4));
-    if (4 * (int)threadIdx.x < d) xres = *reinterpret_cast<const float4*>(D.x + (int64_t)r * d + 4 * threadIdx.x);
+        wt[j][c] = *reinterpret_cast<const float4*>(Ly.w_out_t + (int64_t)(h * DH + c) * d + n);
+      if (w == 0) {
+        xres[j] = *reinterpret_cast<const float4*>(D.x + (int64_t)r * d + n);
+        gff[j] = *reinterpret_cast<const float4*>(Ly.ln_ff + n);
+      }
+    }
   }
   float* sc = smem + w * (D.Tmax + 3 * DH);   // scores / probabilities [Tmax] | q | k_new | v_new
   float* qs = sc + D.Tmax;
@@ -429,17 +455,45 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
       if (n < d) *reinterpret_cast<float4*>(part + h * d + n) = y;
     }
     __syncthreads();
-    const int n = 4 * threadIdx.x;
-    if (n < d) {
-      float4 y = xres;
-      for (int hh = 0; hh < H; ++hh) {
-        const float4 p = *reinterpret_cast<const float4*>(part + hh * d + n);
-        y.x += p.x;
-        y.y += p.y;
-        y.z += p.z;
-        y.w += p.w;
+    if (w == 0) {   // the row: residual + the head partials in head order; then FF1's LayerNorm
+      float4 y[FJ];
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int n = 4 * lane + 256 * j;
+        y[j] = xres[j];
+        if (n < d) {
+          for (int hh = 0; hh < H; ++hh) {
+            const float4 p = *reinterpret_cast<const float4*>(part + hh * d + n);
+            y[j].x += p.x;
+            y[j].y += p.y;
+            y[j].z += p.z;
+            y[j].w += p.w;
+          }
+          *reinterpret_cast<float4*>(D.x + (int64_t)r * d + n) = y[j];
+          sm += (y[j].x + y[j].y) + (y[j].z + y[j].w);
+        }
       }
-      *reinterpret_cast<float4*>(D.x + (int64_t)r * d + n) = y;
+      if (D.xn) {
+        const float mean = wave_sum_dpp(sm) / (float)d;
+        float qq = 0.f;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          if (4 * lane + 256 * j < d) {
+            const float4 dl = make_float4(y[j].x - mean, y[j].y - mean, y[j].z - mean, y[j].w - mean);
+            qq += (dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w);
+          }
+        }
+        const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          const int n = 4 * lane + 256 * j;
+          if (n < d)
+            *reinterpret_cast<float4*>(D.xn + (int64_t)r * d + n) =
+                make_float4(((y[j].x - mean) * rstd) * gff[j].x, ((y[j].y - mean) * rstd) * gff[j].y,
+                            ((y[j].z - mean) * rstd) * gff[j].z, ((y[j].w - mean) * rstd) * gff[j].w);
+        }
+      }
     }
   }
 }
@@ -690,23 +744,24 @@ int check_desc(const XtrlDecodeDesc* D) {
 
 // compaction (inside the embedding for E <= EMB_MAX_E) + embeddings of step t
 template <bool CMP>
-void launch_embed_t(const XtrlDecodeDesc* D, int t, hipStream_t s) {
+void launch_embed_t(const XtrlDecodeDesc* D, int t, const float* g, hipStream_t s) {
   const dim3 grid((D->E + EMB_ROWS - 1) / EMB_ROWS), blk(1024);
   switch ((D->d + 63) / 64) {
-    case 1: hipLaunchKernelGGL((k_embed<1, CMP>), grid, blk, 0, s, *D, t); break;
-    case 2: hipLaunchKernelGGL((k_embed<2, CMP>), grid, blk, 0, s, *D, t); break;
-    case 3: hipLaunchKernelGGL((k_embed<3, CMP>), grid, blk, 0, s, *D, t); break;
-    case 4: hipLaunchKernelGGL((k_embed<4, CMP>), grid, blk, 0, s, *D, t); break;
-    default: hipLaunchKernelGGL((k_embed<8, CMP>), grid, blk, 0, s, *D, t); break;
+    case 1: hipLaunchKernelGGL((k_embed<1, CMP>), grid, blk, 0, s, *D, t, g); break;
+    case 2: hipLaunchKernelGGL((k_embed<2, CMP>), grid, blk, 0, s, *D, t, g); break;
+    case 3: hipLaunchKernelGGL((k_embed<3, CMP>), grid, blk, 0, s, *D, t, g); break;
+    case 4: hipLaunchKernelGGL((k_embed<4, CMP>), grid, blk, 0, s, *D, t, g); break;
+    default: hipLaunchKernelGGL((k_embed<8, CMP>), grid, blk, 0, s, *D, t, g); break;
   }
 }
-int launch_embed(const XtrlDecodeDesc* D, int t, hipStream_t s) {
+// g_ln0: the gain of layer 0's pre-attention LayerNorm when the embedding also writes xn, else NULL
+int launch_embed(const XtrlDecodeDesc* D, int t, const float* g_ln0, hipStream_t s) {
   if (D->E <= EMB_MAX_E) {
-    launch_embed_t<true>(D, t, s);
+    launch_embed_t<true>(D, t, g_ln0, s);
   } else {
     hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, *D, t);
     XTRL_LAUNCHED("compact");
-    launch_embed_t<false>(D, t, s);
+    launch_embed_t<false>(D, t, g_ln0, s);
   }
   XTRL_LAUNCHED("embed");
   return XTRL_OK;
@@ -797,11 +852,15 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode: t=%d outside [0, %d)", t, D->Tmax);
   const int d = D->d, I = D->H * D->dh, ff = D->ff;
   int rc;
-  if ((rc = launch_embed(D, t, s))) return rc;
+  // xn: the LayerNorm of a row computed by the kernel that completes it (embedding -> layer 0's
+  // q|k|v, fused attention -> FF1); the other pre-norms run in the GEMM prologue
+  const bool xn = D->xn != nullptr;
+  if ((rc = launch_embed(D, t, xn ? D->layers[0].ln_attn : nullptr, s))) return rc;
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
-    if ((rc = dproj(D, t, D->x, d, Ly.w_qkv, d, Ly.b_qkv, Ly.ln_attn, d, nullptr, 0, D->qkv, D->n_qkv, D->n_qkv,
-                    EPI_NONE, s)))
+    const bool xn_qkv = xn && l == 0, xn_ff = xn && attn_fused(D, l);
+    if ((rc = dproj(D, t, xn_qkv ? D->xn : D->x, d, Ly.w_qkv, d, Ly.b_qkv, xn_qkv ? nullptr : Ly.ln_attn,
+                    xn_qkv ? 0 : d, nullptr, 0, D->qkv, D->n_qkv, D->n_qkv, EPI_NONE, s)))
       return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
@@ -809,7 +868,8 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
     if (!attn_fused(D, l) &&
         (rc = dproj(D, t, D->att, I, Ly.w_out, I, nullptr, nullptr, 0, D->x, d, D->x, d, d, EPI_NONE, s)))
       return rc;
-    if ((rc = dproj(D, t, D->x, d, Ly.w_ff1, d, Ly.b_ff1, Ly.ln_ff, d, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
+    if ((rc = dproj(D, t, xn_ff ? D->xn : D->x, d, Ly.w_ff1, d, Ly.b_ff1, xn_ff ? nullptr : Ly.ln_ff, xn_ff ? 0 : d,
+                    nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
       return rc;
     // the last layer's output goes straight into the heads' input row (final norm in their prologue)
     const bool last = l == D->L - 1;
@@ -831,7 +891,7 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
                "fractal_decode: the descriptor must describe plain attention (n_qkv = 3 I) with state_only = 1");
   const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels;
   const int64_t Ed = (int64_t)E * d;
-  if (int rc = launch_embed(D, t, s)) return rc;   // x = W_in s + b_in + le_0
+  if (int rc = launch_embed(D, t, nullptr, s)) return rc;   // x = W_in s + b_in + le_0
   rows_add_launch(nullptr, 0, F->g_init, F->g, d, E, d, s);   // per-step global state of every row starts at init
   XTRL_LAUNCHED("rows_add");
   int rc;

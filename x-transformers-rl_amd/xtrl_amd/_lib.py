@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -47,7 +47,7 @@ class DecodeDesc(C.Structure):
                 + [(n, P) for n in ('rs_mean', 'rs_var', 'state', 'prev_action', 'prev_action_f', 'prev_reward',
                                     'alive', 'lens', 'cum_reward', 'episode_of_slot', 'slot_of_row', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
-                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'live_rows', 'live_count',
+                                    'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count',
                                     'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
 

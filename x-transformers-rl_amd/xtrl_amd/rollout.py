@@ -58,6 +58,7 @@ class RolloutEngine:
         # scratch
         self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
         self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
+        self.xn = z(E, d)
         self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
         # decode weights (nn.Linear layouts; the GEMM operands are packed from them, self.wpk)
         self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
@@ -118,7 +119,7 @@ class RolloutEngine:
         D.rng = self.rng.data_ptr()
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
-        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'live_rows', 'live_count', 'lat_embed'):
+        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count', 'lat_embed'):
             setattr(D, k, rows(getattr(self, k)))
         self.desc, self._layers = D, layers
 
