@@ -657,11 +657,12 @@ struct SampleHook {
   }
 };
 
+template <int KS>
 __global__ __launch_bounds__(256) void k_heads_sample(const DGemmArgs a, const XtrlDecodeDesc D, int t) {
   extern __shared__ float As[];
   __shared__ float lg_sh[16][64];
   SampleHook hook{D, t, D.continuous ? 2 * D.A : D.A, blockIdx.x == 0, lg_sh};
-  dgemm_body<1, 1, EPI_NONE, false, false>(a, As, hook);
+  dgemm_body<1, 1, KS, EPI_NONE, false, false>(a, As, hook);
 }
 
 // host env results of step t (xtrl.py:1297-1336): the memory stores is_boundary = terminated;
@@ -823,16 +824,20 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
                   final_norm ? d : 0, nullptr, 0, D->hff, 4 * d, 4 * d, EPI_SILU, s)))
     return rc;
   const int n_act = D->continuous ? 2 * D->A : D->A;
-  if (n_act <= 64) {   // block-diagonal projection + sampling in one launch
+  const int ks = dg_ks(n_act + D->B, 4 * d);
+  if (n_act <= 64 / ks) {   // block-diagonal projection + sampling in one launch (actor columns in block 0)
     DGemmArgs g;
     g.A = D->hff; g.lda = 4 * d; g.W = D->w_h2; g.ldw = 4 * d; g.bias = D->b_h2;
     g.C = D->logits; g.ldc = n_act; g.n_split = n_act;
     g.C2 = D->traj_values + (int64_t)t * D->B; g.ldc2 = D->Tmax * D->B; g.row_map2 = D->live_rows + (t & 1) * E;
     g.m_dev = D->live_count + (t & 1); g.M = E; g.N = n_act + D->B; g.K = 4 * d;
     XTRL_REQUIRE(g.K % 4 == 0 && g.K <= 2048, "decode heads: 4 d must be a multiple of 4, at most 2048");
-    const dim3 grid((g.N + 63) / 64, (E + 15) / 16);
-    const size_t lds = (size_t)16 * (dg_kp(g.K) + 4) * sizeof(float);
-    hipLaunchKernelGGL(k_heads_sample, grid, dim3(256), lds, s, g, *D, t);
+    const int bn = 64 / ks;
+    const dim3 grid((g.N + bn - 1) / bn, (E + 15) / 16);
+    const size_t lds = dg_lds_floats(1, 1, ks, false, g.K) * sizeof(float);
+    if (ks == 4) hipLaunchKernelGGL(k_heads_sample<4>, grid, dim3(256), lds, s, g, *D, t);
+    else if (ks == 2) hipLaunchKernelGGL(k_heads_sample<2>, grid, dim3(256), lds, s, g, *D, t);
+    else hipLaunchKernelGGL(k_heads_sample<1>, grid, dim3(256), lds, s, g, *D, t);
     XTRL_LAUNCHED("heads_sample");
     return XTRL_OK;
   }

@@ -28,6 +28,7 @@
 //    Linear: actor logits to a row buffer, critic logits straight into the trajectory rows of their
 //    episodes).
 #include <algorithm>
+#include <cstdlib>
 
 #include "dgemm_body.h"
 
@@ -35,11 +36,11 @@ namespace xtrl {
 
 namespace {
 
-template <int MT, int NT, int EPI, bool LN, bool RES>
+template <int MT, int NT, int KS, int EPI, bool LN, bool RES>
 __global__ __launch_bounds__(256) void k_dgemm(const DGemmArgs a) {
   extern __shared__ float As[];
   DgNoHook hook;
-  dgemm_body<MT, NT, EPI, LN, RES>(a, As, hook);
+  dgemm_body<MT, NT, KS, EPI, LN, RES>(a, As, hook);
 }
 
 // fragment packing of an nn.Linear weight [N][K] (one thread per float4 slot)
@@ -58,24 +59,41 @@ __global__ void k_dg_pack(const float* W, int ldw, int N, int K, float* Wp) {
   reinterpret_cast<float4*>(Wp)[s] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-template <int MT, int NT, int EPI, bool LN, bool RES>
+template <int MT, int NT, int KS, int EPI, bool LN, bool RES>
 void launch_dg(const DGemmArgs& a, int rows, hipStream_t s) {
-  constexpr int BM = 16 * MT, BN = 64 * NT;
+  constexpr int BM = 16 * MT, BN = 64 * NT / KS;
   dim3 grid((a.N + BN - 1) / BN, (rows + BM - 1) / BM);
-  const size_t lds = ((size_t)BM * (dg_kp(a.K) + 4) + (LN ? 512 : 0)) * sizeof(float);
-  hipLaunchKernelGGL((k_dgemm<MT, NT, EPI, LN, RES>), grid, dim3(256), lds, s, a);
+  const size_t lds = dg_lds_floats(MT, NT, KS, LN, a.K) * sizeof(float);
+  hipLaunchKernelGGL((k_dgemm<MT, NT, KS, EPI, LN, RES>), grid, dim3(256), lds, s, a);
 }
 
 template <int EPI, bool LN, bool RES>
 void dispatch_dg(const DGemmArgs& a, int rows, hipStream_t s) {
   // 32-row panels where N is wide and the panel stays small (FF1, the head hidden layer: twice
   // the weight reuse, half the workgroups); 16-row panels otherwise (long K, narrow N)
+  // (long K over narrow N: the K split across the 4 waves, see dgemm_body)
   const size_t lds32 = (size_t)32 * (dg_kp(a.K) + 4) * sizeof(float);
-  if (a.N >= 512 && lds32 <= 80 * 1024) launch_dg<2, 1, EPI, LN, RES>(a, rows, s);
-  else launch_dg<1, 1, EPI, LN, RES>(a, rows, s);
+  const int ks = dg_ks(a.N, a.K);
+  if (a.N >= 512 && lds32 <= 80 * 1024) launch_dg<2, 1, 1, EPI, LN, RES>(a, rows, s);
+  else if (ks == 2) launch_dg<1, 1, 2, EPI, LN, RES>(a, rows, s);
+  else if (ks == 4) launch_dg<1, 1, 4, EPI, LN, RES>(a, rows, s);
+  else launch_dg<1, 1, 1, EPI, LN, RES>(a, rows, s);
 }
 
 }  // namespace
+
+// the K split of a 16-row-panel projection: 2 for K >= 768 over N < 512 (FF2 at 440 live rows:
+// 9.7 -> 7.3 us; 4: 7.3 us at 440 rows but 14.0 vs 10.0 us at 1024, every column block re-reading
+// the A panel); XTRL_DG_KS overrides (1, 2, 4; experiments)
+int dg_ks(int N, int K) {
+  static const int ks_env = [] {
+    const char* e = getenv("XTRL_DG_KS");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  if (!dg_split_k(N, K)) return 1;
+  return ks_env ? ks_env : 2;
+}
 
 int64_t dgemm_packed_floats(int N, int K) { return (int64_t)((N + 15) / 16) * 16 * dg_kp(K); }
 

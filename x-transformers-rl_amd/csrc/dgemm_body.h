@@ -21,6 +21,13 @@ constexpr int DG_JB = 16;   // float4 weight loads per lane per block (per colum
 // padded K (a multiple of 16: four lane quarters of whole float4s) and the LDS row stride
 __host__ __device__ __forceinline__ int dg_kp(int K) { return (K + 15) & ~15; }
 
+// LDS floats of a dgemm_body launch: the A panel, the LayerNorm gains, the K-split partial tiles
+__host__ __device__ __forceinline__ size_t dg_lds_floats(int MT, int NT, int KS, bool LN, int K) {
+  return (size_t)16 * MT * (dg_kp(K) + 4) + (LN ? 512 : 0) + (size_t)(KS - 1) * (4 / KS) * MT * NT * 256;
+}
+// the 4-way K split for projections with K >= 768 over N <= 512 (16-row panels)
+__host__ __device__ __forceinline__ bool dg_split_k(int N, int K) { return K >= 768 && N < 512; }
+
 struct DgNoHook {
   __device__ __forceinline__ void prefetch(int, int) {}
   __device__ __forceinline__ void landed() {}
@@ -28,9 +35,15 @@ struct DgNoHook {
   __device__ __forceinline__ void finish(int, int) {}
 };
 
-template <int MT, int NT, int EPI, bool LN, bool RES, class Hook>
+// KS: waves per column group that split K (KS = 1: each of the 4 waves owns 16 NT columns over
+// all of K; KS = 4: the 4 waves share 16 NT columns, each a quarter of the k steps, and their
+// partial tiles meet in LDS, summed in wave order before the epilogue of wave 0).  A long-K,
+// narrow-N projection over few live rows (FF2, the heads' last Linear) otherwise runs a 4x
+// longer MFMA chain per wave on a quarter of the chip.
+template <int MT, int NT, int KS, int EPI, bool LN, bool RES, class Hook>
 __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& hook) {
-  constexpr int BM = 16 * MT, BNW = 16 * NT, BN = 4 * BNW, JB = DG_JB / NT;
+  constexpr int CG = 4 / KS;   // column groups per workgroup
+  constexpr int BM = 16 * MT, BNW = 16 * NT, BN = CG * BNW, JB = DG_JB / NT;
   const int M = a.m_dev ? *a.m_dev : a.M;
   const int m0 = blockIdx.y * BM;
   if (m0 >= M) return;
@@ -38,7 +51,10 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
   const int K = a.K, Kp = dg_kp(K), LDA = Kp + 4, KQ = Kp >> 2, JN = KQ >> 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, q = lane >> 4;
-  const int n0 = blockIdx.x * BN + w * BNW;
+  const int cg = w / KS, ks = w - cg * KS;
+  const int n0 = blockIdx.x * BN + cg * BNW;
+  // this wave's k steps [j_lo, j_hi) of the JN per lane quarter (JN >= KS: see dgemm_run)
+  const int j_lo = ks * JN / KS, j_hi = (ks + 1) * JN / KS;
 
   // ---- weights of this wave: fragment-packed (xtrl_dgemm_pack), so one load instruction reads
   //      1 KiB contiguous — float4 slot ((n / 16 * JN + j) * 4 + q) * 16 + n % 16 holds
@@ -56,7 +72,7 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int j = 0; j < JB; ++j) {
-        const int jj = min(blk * JB + j, JN - 1);   // (steps past JN: tail block, unused)
+        const int jj = min(j_lo + blk * JB + j, j_hi - 1);   // (steps past the range: tail block, unused)
         b[nt][j] = *reinterpret_cast<const f32x4v*>(wp[nt] + 256 * jj);
       }
   };
@@ -174,12 +190,12 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
   };
   // whole blocks of JB float4 steps (K a multiple of 16 JB / ... : no per-step condition), then
   // the tail block
-  const int NBF = JN / JB, JT = JN - NBF * JB;
+  const int NJ = j_hi - j_lo, NBF = NJ / JB, JT = NJ - NBF * JB;
   for (int blk = 0; blk < NBF; ++blk) {
     const bool more = blk + 1 < NBF || JT > 0;
     if (more) load_b(bnext, blk + 1);
 #pragma unroll
-    for (int j = 0; j < JB; ++j) step(blk * JB + j, bcur, j);
+    for (int j = 0; j < JB; ++j) step(j_lo + blk * JB + j, bcur, j);
     if (more) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
@@ -190,10 +206,33 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
   if (JT > 0) {
 #pragma unroll
     for (int j = 0; j < JB; ++j)
-      if (j < JT) step(NBF * JB + j, bcur, j);
+      if (j < JT) step(j_lo + NBF * JB + j, bcur, j);
+  }
+  if constexpr (KS > 1) {   // partial tiles of waves 1 .. KS-1 of each column group -> wave 0
+    f32x4v* red = reinterpret_cast<f32x4v*>(As + BM * LDA + (LN ? 512 : 0));
+    auto slot = [&](int k, int mt, int nt) { return ((cg * (KS - 1) + k - 1) * MT * NT + mt * NT + nt) * 64 + lane; };
+    if (ks > 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) red[slot(ks, mt, nt)] = acc[mt][nt][0] + acc[mt][nt][1];
+    }
+    __syncthreads();
+    if (ks == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          f32x4v v = acc[mt][nt][0] + acc[mt][nt][1];
+          for (int k = 1; k < KS; ++k) v += red[slot(k, mt, nt)];
+          acc[mt][nt][0] = v;
+          acc[mt][nt][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+    }
   }
 
-  // ---- epilogue: element i of a tile is (row 4 q + i, column lr) ----
+  // ---- epilogue (wave 0 of each column group): element i of a tile is (row 4 q + i, column lr) ----
+  if (ks == 0)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

@@ -99,6 +99,8 @@ struct DGemmArgs {
 // `rows` bounds the live-row count (sizes the grid); epi: EPI_NONE / EPI_GELU / EPI_SILU;
 // W fragment-packed by dgemm_pack (dgemm_packed_floats(N, K) floats)
 int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s);
+// waves splitting K per column group (dgemm_body KS) of a 16-row-panel projection of this shape
+int dg_ks(int N, int K);
 int64_t dgemm_packed_floats(int N, int K);
 int dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s);
 
