@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Benchmark: env-steps/s of the Learner hot path (rollout + learn) on N MI355X, weak scaling.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5|c1]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One "step" = one learning update of the reference Learner loop (xtrl.py:1204-1373): a rollout of
@@ -49,6 +49,13 @@ CONFIGS = {
     'c2': dict(workload='C2: LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 steps, depth-2 d=128 EPO',
                S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,
                batch=32, hazard_log2=6, dropout=0.25, mode='lander'),
+    # configs[4] — EPO population 8, one gene per GPU at 8 GPUs, the fractal policy body (causal per
+    # timestep, x-transformers-rl_amd/xtrl_amd/fractal.py); per GPU 1024 (episode, gene) pairs
+    'c5': dict(workload='C5 (per GPU): LunarLander-shaped VecSim, EPO population 8 gene-sharded (gene g on GPU g at '
+                        '8 GPUs), 1024 episodes x 128 steps per GPU, fractal policy body (4 levels, d=256, 4x16 '
+                        'heads, causal per timestep), batch 128 episodes, 4 epochs, dropout 0.25',
+               S=8, A=4, episodes=128, genes=8, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=False, evo=True,
+               fractal=4, batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
     # configs[0] — README Sim plumbing case
     'c1': dict(workload='C1: README Sim (S=5, A=2, T=10), depth 1, d=48, 64 episodes, batch 8',
                S=5, A=2, episodes=64, T=10, depth=1, dim=48, heads=4, dim_head=16, gates=False, evo=False,
@@ -61,14 +68,17 @@ def build_learner(cfg, seed, use_graph=True, world=1):
     wm = dict(attn_dim_head=cfg['dim_head'], heads=cfg['heads'], depth=cfg['depth'])
     if cfg['gates']:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
+    extra = dict(policy_body='fractal', fractal_levels=cfg['fractal']) if cfg.get('fractal') else {}
     learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
                       max_timesteps=cfg['T'], batch_size=cfg['batch'],
                       num_episodes_per_update=cfg['episodes'] * world,   # weak scaling: episodes per GPU fixed
                       evolutionary=cfg['evo'], evolve_every=5, evolve_after_step=10,
-                      latent_gene_pool=dict(dim=32, num_genes_per_island=3, num_selected=2, tournament_size=2),
+                      latent_gene_pool=dict(dim=32, num_genes_per_island=cfg.get('genes', 3), num_selected=2,
+                                            tournament_size=2),
                       agent_kwargs=dict(hidden_dim=cfg['dim'], dropout=cfg['dropout'], seed=seed,
-                                        save_path='/tmp/xtrl_bench_ppo.pt'),
-                      use_graph=use_graph)
+                                        save_path='/tmp/xtrl_bench_ppo.pt', **extra),
+                      use_graph=use_graph, shard_by_gene=bool(cfg.get('fractal')))
+    # (C5: episodes per update = 128 x world over 8 genes, gene-sharded: 1024 pairs per GPU at any N)
     env = SynthVecSim(cfg['S'], cfg['A'], cfg['mode'], cfg['hazard_log2'])
     return learner, env
 
@@ -245,14 +255,18 @@ def cpu_baseline(cfg, seed, budget_s, threads=None, episodes=None):
     from oracle import ref_port as R
     threads = threads or int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    episodes = episodes or (96 if cfg['T'] >= 100 else 512)
+    episodes = episodes or (32 if cfg.get('fractal') else 96 if cfg['T'] >= 100 else 512)
     batch = min(8, episodes)
     c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
                         dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],
                         learned_mix=cfg['gates'], evolutionary=False, max_timesteps=cfg['T'], batch_size=batch,
                         num_episodes_per_update=episodes, sim_mode=cfg['mode'], hazard_log2=cfg['hazard_log2'],
                         seed=seed, dropout=cfg['dropout'])
-    oracle = R.OracleLearner(c)
+    factory = None
+    if cfg.get('fractal'):
+        from oracle import fractal_ref as FR
+        factory = lambda mc: FR.OracleFractalPolicy(mc, cfg['fractal'])   # noqa: E731
+    oracle = R.OracleLearner(c, model_factory=factory)
     t0 = time.perf_counter()
     eps, fit = oracle.rollout(0)
     t1 = time.perf_counter()
@@ -280,7 +294,11 @@ def ppo_loss_delta(learner, env, cfg):
                        c.num_bins, c.continuous, c.squash, c.evolutionary, c.dim_gene, c.frac_head_grad,
                        c.entropy_weight, c.eps_clip, c.value_clip, 0., c.reward_dropout, True, c.gate_values,
                        c.value_residual, c.learned_mix)
-    model = R.OracleWMAC(mc)
+    if cfg.get('fractal'):
+        from oracle import fractal_ref as FR
+        model = FR.OracleFractalPolicy(mc, cfg['fractal'])
+    else:
+        model = R.OracleWMAC(mc)
 
     def probe(epoch, mbi, idx, loss, stats):
         if out:
@@ -351,7 +369,8 @@ def main():
 
     for _ in range(args.warmup):
         one_update(learner, env, T)
-    timer = None if args.no_roofline else DecodeAttnTimer(learner, env, T)
+    # (the roofline timers instrument the decoder's decode step and fused learn step: C3 / C2 / C1)
+    timer = None if args.no_roofline or cfg.get('fractal') else DecodeAttnTimer(learner, env, T)
     gtimer = None
     if timer is not None:
         # untimed: capture the rollout graph with the event records inside, and count the
@@ -441,7 +460,8 @@ def main():
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, args.seed, 20.)
             phys, share = host_cores()
-            one = cpu_baseline(cfg, args.seed, 20., threads=1, episodes=32 if cfg['T'] >= 100 else 128)
+            one = cpu_baseline(cfg, args.seed, 20., threads=1,
+                               episodes=8 if cfg.get('fractal') else 32 if cfg['T'] >= 100 else 128)
             cpu.update(host_physical_cores=phys, host_cpu_share=share,
                        single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
@@ -449,7 +469,8 @@ def main():
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
                     higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
                     data='synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)',
-                    config=dict(workload=cfg['workload'], global_batch=cfg['episodes'] * (3 if cfg['evo'] else 1) * world,
+                    config=dict(workload=cfg['workload'],
+                                global_batch=cfg['episodes'] * (cfg.get('genes', 3) if cfg['evo'] else 1) * world,
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
                     roofline=roofline, attention_roofline=attn_roofline, cpu_baseline=cpu, ppo_loss=loss_delta,
                     phase_ms=phase_ms)
