@@ -269,9 +269,11 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
   const int idx = blockIdx.x * nw + w;
   const int H = D.H, I = H * DH, d = D.d;
   const int r = idx / H, h = idx - r * H;
-  if (r >= D.live_count[t & 1]) return;   // wave-uniform (FUSE: workgroup-uniform)
   constexpr bool FUSE = FJ > 0;
-  const int e = rows_of(D, t)[r];
+  // the live count and the row's slot in one round trip (live_rows past the count: a stale slot)
+  const int n_live = D.live_count[t & 1];
+  const int e = rows_of(D, t)[min(r, D.E - 1)];
+  if (r >= n_live) return;   // wave-uniform (FUSE: workgroup-uniform)
   // fused out-projection operands: this head's rows of W_out^T and the residual row
   float4 wt[FUSE ? FJ : 1][FUSE ? DH : 1];
   float4 xres[FUSE ? FJ : 1], gff[FUSE ? FJ : 1];   // wave 0: the residual row and FF1's LayerNorm gain
@@ -639,10 +641,10 @@ struct SampleHook {
   SampleIn in;
   // the row's slot first (its load lands with the GEMM operands), the loads that depend on it
   // once they have landed (in flight during the MFMA loop)
-  __device__ __forceinline__ void prefetch(int m0, int M) {
+  __device__ __forceinline__ void prefetch(int m0, int rows) {
     row = threadIdx.x / SAMPLE_L;
     sub = threadIdx.x % SAMPLE_L;
-    if (on && row < 16) e = rows_of(D, t)[min(m0 + row, M - 1)];
+    if (on && row < 16) e = rows_of(D, t)[min(m0 + row, rows - 1)];   // (stale past the live count: unused)
   }
   __device__ __forceinline__ void landed() {
     if (on && row < 16) in = sample_load(D, e);
