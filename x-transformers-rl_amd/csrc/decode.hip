@@ -641,10 +641,10 @@ struct SampleHook {
   SampleIn in;
   // the row's slot first (its load lands with the GEMM operands), the loads that depend on it
   // once they have landed (in flight during the MFMA loop)
-  __device__ __forceinline__ void prefetch(int m0, int rows) {
+  __device__ __forceinline__ void prefetch(int m0, int M) {
     row = threadIdx.x / SAMPLE_L;
     sub = threadIdx.x % SAMPLE_L;
-    if (on && row < 16) e = rows_of(D, t)[min(m0 + row, rows - 1)];   // (stale past the live count: unused)
+    if (on && row < 16) e = rows_of(D, t)[min(m0 + row, M - 1)];
   }
   __device__ __forceinline__ void landed() {
     if (on && row < 16) in = sample_load(D, e);

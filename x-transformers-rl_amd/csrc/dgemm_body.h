@@ -1,6 +1,6 @@
 // Decode-step GEMM body (dgemm.hip), shared with the fused head + sampling kernel of decode.hip.
-// See dgemm.hip for the design.  A Hook adds work to the body: prefetch(m0, rows) runs before the
-// operand loads are issued (rows: the buffer's row count, the live count is not known yet), landed() once they have landed (the first workgroup barrier passed),
+// See dgemm.hip for the design.  A Hook adds work to the body: prefetch(m0, M) runs before the
+// operand loads are issued, landed() once they have landed (the first workgroup barrier passed),
 // value(row_in_tile, n, v) for every output element (also the discarded ones past M / N),
 // finish(m0, M) after the epilogue.
 #pragma once
@@ -44,12 +44,12 @@ template <int MT, int NT, int KS, int EPI, bool LN, bool RES, class Hook>
 __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& hook) {
   constexpr int CG = 4 / KS;   // column groups per workgroup
   constexpr int BM = 16 * MT, BNW = 16 * NT, BN = CG * BNW, JB = DG_JB / NT;
-  // the live row count M is loaded with the operands, not before them: rows are clamped to the
-  // buffer (a.M rows), rows past M computed on stale data and discarded, and a workgroup past M
-  // exits once its loads have landed — one dependent round trip less per launch
+  // (loading M together with the operands — rows clamped to the buffer, a workgroup past M exiting
+  // after its loads — measured slower: the dead row panels' loads cost more than the round trip)
   const int M = a.m_dev ? *a.m_dev : a.M;
-  const int m0 = blockIdx.y * BM, mlast = a.M - 1;
-  hook.prefetch(m0, a.M);
+  const int m0 = blockIdx.y * BM, mlast = M - 1;
+  if (m0 >= M) return;
+  hook.prefetch(m0, M);
   const int K = a.K, Kp = dg_kp(K), LDA = Kp + 4, KQ = Kp >> 2, JN = KQ >> 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, q = lane >> 4;
@@ -128,8 +128,7 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
       dst[mt][i] = a.row_map ? (int64_t)a.row_map[m] : (int64_t)m;
       dst2[mt][i] = a.row_map2 ? (int64_t)a.row_map2[m] : (int64_t)m;
     }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (also before an exit: no LDS-DMA may outlive the workgroup)
-  if (m0 >= M) return;   // (workgroup-uniform)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   hook.landed();
 
