@@ -82,6 +82,7 @@ __global__ __launch_bounds__(1024) void k_compact(const XtrlDecodeDesc D, int t)
 constexpr int EMB_ROWS = 16;
 constexpr int EMB_LDS_FLOATS = 8192;   // 2 d S <= 8192 (C3: 4096); larger: weights read from global
 constexpr int EMB_MAX_E = 8192;        // E up to this: the compaction runs inside k_embed (CMP)
+constexpr int EMB_AREG = 8;            // discrete A up to this: action embeddings held in registers
 // CMP: every workgroup ranks the live slots itself (one load of the alive bytes, ballots, an LDS
 // scan — the same slot order as k_compact) and stores its own rows' entries of live_rows[t & 1];
 // workgroup 0 stores live_count[t & 1].  No separate compaction launch, and the embedding's
@@ -146,6 +147,17 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, c
     bpin[k] = D.b_pin ? D.b_pin[c] : 0.f;
     gln[k] = g_ln0 ? g_ln0[c] : 0.f;
   }
+  // discrete actions, A <= EMB_AREG: every action's embedding columns of this lane, loaded up front
+  // (the row's action then selects among registers: no dependent load after the previous action)
+  constexpr int AR = NC <= 4 ? EMB_AREG : 1;   // (d > 256: the table stays in memory, registers are short)
+  const bool areg = NC <= 4 && !D.continuous && D.A <= EMB_AREG;
+  float emb_a[AR][NC];
+  if (areg) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+#pragma unroll
+      for (int k = 0; k < NC; ++k) emb_a[i][k] = D.act_emb[min(i, D.A - 1) * d + min(lane + 64 * k, d - 1)];
+  }
   const int n = CMP ? n_live : D.live_count[t & 1];
   const int r0 = blockIdx.x * EMB_ROWS;
   if (r0 >= n) return;   // (whole workgroup)
@@ -188,6 +200,11 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, c
       float acc = 0.f;
       for (int i = 0; i < D.A; ++i) acc += D.prev_action_f[e * D.A + i] * D.act_emb[c * D.A + i];
       act[k] = acc + D.act_emb_b[c];
+    } else if (areg) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) v = (i == max(a, 0)) ? emb_a[i][k] : v;
+      act[k] = v;
     } else {
       act[k] = D.act_emb[max(a, 0) * d + c];
     }
