@@ -79,6 +79,15 @@ def show(path):
         lw = (int(rows[seg[-1]]['End_Timestamp']) - int(rows[seg[0]]['Start_Timestamp'])) / 1e3
         print(f'learn busy per {qkey} (wall {lw / 1e3:.2f} ms): ' +
               ', '.join(f'{q}: {us / 1e3:.2f} ms' for q, us in sorted(per_q.items(), key=lambda kv: -kv[1])))
+        # per stream: the learn kernels by time (the input-gradient chain's stream is the critical path)
+        for q in sorted(per_q, key=lambda k: -per_q[k]):
+            agg = defaultdict(lambda: [0, 0.0])
+            for i in seg:
+                if rows[i].get(qkey) == q:
+                    a = agg[short(names[i])]; a[0] += 1; a[1] += dur[i]
+            print(f'  {qkey} {q}:')
+            for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:12]:
+                print(f'    {us / 1e3:8.2f} ms {n:6d} {us / n:8.1f} us  {k}')
         by_next = defaultdict(float)
         for g_us, i in gaps:
             by_next[short(names[i])] += g_us
@@ -94,12 +103,12 @@ def show(path):
             for i in range(a, b):
                 gap = (int(rows[i]['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp'])) / 1e3
                 print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  {short(names[i])}')
-        # one decode step: the kernels between two consecutive k_sample launches in the rollout
-        samples = [i for i in roll if 'k_sample' in names[i]]
+        # one decode step: the kernels between two consecutive sampling launches in the rollout
+        samples = [i for i in roll if 'k_sample' in names[i] or 'k_heads_sample' in names[i]]
         if len(samples) > 12:
             a, b = samples[10], samples[11]
             ts = int(rows[a]['End_Timestamp']); te = int(rows[b]['End_Timestamp'])
-            print(f'\ndecode step (k_sample #10..#11): {b - a} kernels, wall {(te - ts) / 1e3:.1f} us')
+            print(f'\ndecode step (sampling launch #10..#11): {b - a} kernels, wall {(te - ts) / 1e3:.1f} us')
             for i in range(a + 1, b + 1):
                 gap = (int(rows[i]['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp'])) / 1e3
                 print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  {short(names[i])}')
