@@ -63,6 +63,10 @@ int xtrl_gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float*
  * 512 / tiles splits) and summed in fixed order — deterministic. */
 int xtrl_gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K,
                     float beta, float* ws, int64_t ws_floats, void* stream);
+/* the same with the bias gradient folded in: db[n - db_n0] += sum_m dY[m][n] for n >= db_n0 (from
+ * the staged dY slabs of the GEMM; beta must be 1).  nn.Linear.bias.grad (xtrl.py:981 backward) */
+int xtrl_gemm_wgrad_db(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K,
+                       float beta, float* ws, int64_t ws_floats, float* db, int db_n0, void* stream);
 
 /* Y[m, :] = layer_norm(X[m, :]) * gamma  (x-transformers LayerNorm, final norm of the Decoder) */
 int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D, void* stream);

@@ -1386,6 +1386,12 @@ extern "C" int xtrl_gemm_wgrad(const float* dY, int ldy, const float* X, int ldx
   return xtrl::gemm_wgrad(dY, ldy, X, ldx, dW, ldw, M, N, K, beta, ws, ws_floats, xtrl::as_stream(stream), nullptr, 0);
 }
 
+extern "C" int xtrl_gemm_wgrad_db(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M,
+                                  int N, int K, float beta, float* ws, int64_t ws_floats, float* db, int db_n0,
+                                  void* stream) {
+  return xtrl::gemm_wgrad(dY, ldy, X, ldx, dW, ldw, M, N, K, beta, ws, ws_floats, xtrl::as_stream(stream), db, db_n0);
+}
+
 extern "C" int xtrl_layernorm_f32(const float* X, int ldx, const float* gamma, float* Y, int ldy, int M, int D,
                                   void* stream) {
   return xtrl::layernorm_f32(X, ldx, gamma, Y, ldy, M, D, xtrl::as_stream(stream));

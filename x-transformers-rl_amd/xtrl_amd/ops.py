@@ -59,32 +59,48 @@ def wgrad(dy, x, dw, ws, beta=1.):
 
 
 class XLinearFn(torch.autograd.Function):
-    """nn.Linear whose parameter gradients are accumulated straight into the flat gradient
-    buffer (the weight gradient by the split-K HIP GEMM, so no per-parameter accumulation pass);
-    forward and input-gradient GEMMs stay on hipBLASLt."""
+    """nn.Linear on the library GEMMs (the reference-mode learn step; the fractal policy body's
+    product path): forward y = x W^T + b and input gradient dx = dy W on gemm_run (split-bf16
+    products on the large-tile geometry), the weight gradient by the split-K HIP GEMM with the bias
+    gradient folded into it, both accumulated straight into the flat gradient buffer (no
+    per-parameter accumulation pass, no separate column-sum launch)."""
 
     @staticmethod
     def forward(ctx, x, w, b, wg, bg, bg_off, ws):
         K = x.shape[-1]
+        N = w.shape[0]
         x2 = x.reshape(-1, K)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        M = x2.shape[0]
+        assert w.is_contiguous() and (b is None or b.is_contiguous())
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        if M:
+            gemm_ex(x2, w, 0, 0, M, N, K, y, bias=b)
         ctx.save_for_backward(x2, w)
         ctx.extra = (wg, bg, bg_off, ws, x.shape)
-        return y.view(*x.shape[:-1], w.shape[0])
+        return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         wg, bg, bg_off, ws, xshape = ctx.extra
-        dy2 = dy.reshape(-1, w.shape[0])
+        N, K = w.shape
+        dy2 = dy.reshape(-1, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dx = torch.mm(dy2, w).view(xshape) if ctx.needs_input_grad[0] else None
-        if wg is not None:
-            wgrad(dy2, x2, wg, ws, beta=1.)
-        if bg is not None:
+        M = dy2.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, device=dy.device, dtype=torch.float32)
+            if M:
+                gemm_ex(dy2, w, 0, 1, M, K, N, dx)
+            dx = dx.view(xshape)
+        if wg is not None and M:
+            L.check(L.lib().xtrl_gemm_wgrad_db(L.ptr(dy2), dy2.stride(0), L.ptr(x2), x2.stride(0), L.ptr(wg), K, M, N,
+                                               K, 1., L.ptr(ws), ws.numel(), L.ptr(bg), int(bg_off), L.stream()),
+                    'gemm_wgrad_db')
+        elif bg is not None:
             bg.add_(dy2[:, bg_off:].sum(0))
         return dx, None, None, None, None, None, None
 
