@@ -384,6 +384,12 @@ typedef struct XtrlTrainDesc {
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
 int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream);
+/* Y = drop(gelu(X W^T + b)) and deriv = drop(gelu'(X W^T + b)) (x-transformers FeedForward's first
+ * Linear + GELU + Dropout, xtrl.py Decoder ff; fractal_rl.py FeedForward), dropout keep bits the
+ * stream of xtrl_ff_dropout_mask(seed, offset, layer) and of the fused learn step */
+int xtrl_linear_gelu_drop(const float* X, int ldx, const float* W, const float* bias, float* Y, int ldy, float* deriv,
+                          int ld_deriv, int M, int N, int K, float p, uint64_t seed, uint32_t offset, uint32_t layer,
+                          void* stream);
 /* the feed-forward dropout keep mask of layer `layer` as uint8 [M][N] (tests / reference mode) */
 int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, uint32_t layer,
                          void* stream);

@@ -905,6 +905,24 @@ extern "C" int64_t xtrl_train_part_floats(int T, int b, int d, int A) {
   return std::max(std::max(ln, cs), std::max(lat, emb));
 }
 
+extern "C" int xtrl_linear_gelu_drop(const float* X, int ldx, const float* W, const float* bias, float* Y, int ldy,
+                                     float* deriv, int ld_deriv, int M, int N, int K, float p, uint64_t seed,
+                                     uint32_t offset, uint32_t layer, void* stream) {
+  XTRL_REQUIRE(layer < (1u << 22), "linear_gelu_drop: layer %u out of range", layer);
+  XTRL_REQUIRE(X && W && Y && deriv && M >= 0 && N > 0 && K > 0 && p >= 0.f && p < 1.f && ldx >= K && ldy >= N &&
+                   ld_deriv >= N,
+               "linear_gelu_drop: bad arguments");
+  if (M == 0) return XTRL_OK;
+  xtrl::GemmArgs g;
+  g.A = X; g.lda = ldx; g.B = W; g.ldb = K; g.bias = bias; g.C = Y; g.ldc = ldy; g.M = M; g.N = N; g.K = K;
+  g.aux_out = deriv; g.ld_aux_out = ld_deriv;
+  g.seed = seed; g.drop_off = offset; g.drop_layer = layer;
+  g.drop_thresh = xtrl::dropout_thresh(p);
+  g.drop_thresh8 = xtrl::dropout_thresh8(p);
+  g.inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  return xtrl::gemm_run(g, 0, 0, xtrl::EPI_GELU_DROP, xtrl::as_stream(stream));
+}
+
 extern "C" int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset,
                                     uint32_t layer, void* stream) {
   XTRL_REQUIRE(layer < (1u << 22), "ff_dropout_mask: layer %u out of range", layer);

@@ -113,6 +113,7 @@ SIGNATURES = {
     'xtrl_gemm_ex': (I32, [I32, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, F32, P]),
     'xtrl_gemm_wgrad': (I32, [P, I32, P, I32, P, I32, I32, I32, I32, F32, P, I64, P]),
     'xtrl_gemm_wgrad_db': (I32, [P, I32, P, I32, P, I32, I32, I32, I32, F32, P, I64, P, I32, P]),
+    'xtrl_linear_gelu_drop': (I32, [P, I32, P, P, P, I32, P, I32, I32, I32, I32, F32, U64, U32, U32, P]),
     'xtrl_layernorm_f32': (I32, [P, I32, P, P, I32, I32, I32, P]),
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),

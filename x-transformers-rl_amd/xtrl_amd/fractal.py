@@ -377,11 +377,8 @@ class FractalPolicyActorCritic(FractalWorldModelActorCritic):
             x1 = blk.norm1(x + self._lin(o, sa.to_out))
             x2 = blk.norm2(x1 + self._lin(self._lin(g, ga.to_v), ga.to_out))
             ff0, ff2 = blk.ff.ff[0][0], blk.ff.ff[2]
-            h = F.gelu(self._lin(x2, ff0))
-            if p_drop > 0:
-                from .train import ff_dropout_mask
-                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset, h.device, layer=li)
-                h = h * keep.view(b, n, -1).to(h.dtype) * (1.0 / (1.0 - p_drop))
+            h = ops.linear_gelu_drop(x2, ff0.weight, ff0.bias, ff0.weight.grad, ff0.bias.grad, self._ws, p_drop,
+                                     attn_seed, ff_offset, li)   # Linear + GELU + Dropout in one epilogue
             x3 = blk.norm3(x2 + self._lin(h, ff2))
             mean = x3.cumsum(dim=1) / cnt
             projs.append(self._lin(mean, enc.level_projections[li]))

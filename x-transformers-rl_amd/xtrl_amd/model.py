@@ -278,11 +278,9 @@ class WorldModelActorCritic(nn.Module):
                 o = o * gate_pre.sigmoid()
             x = self._lin(o, blk.to_out) + x
             (ln_f, _, _), ffb, _ = ff_l
-            h = F.gelu(self._lin(ln_f(x), ffb.ff[0][0]))
-            if p_drop > 0:
-                from .train import ff_dropout_mask
-                keep = ff_dropout_mask(b * n, h.shape[-1], p_drop, attn_seed, ff_offset, h.device, layer=li)
-                h = h * keep.view(b, n, -1).to(h.dtype) * (1.0 / (1.0 - p_drop))
+            f0 = ffb.ff[0][0]   # Linear + GELU + Dropout in one GEMM epilogue (the fused step's mask stream)
+            h = ops.linear_gelu_drop(ln_f(x), f0.weight, f0.bias, f0.weight.grad, f0.bias.grad, self._ws, p_drop,
+                                     attn_seed, ff_offset, li)
             x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)
         ewa = torch.cat((embed, self.embed_actions(next_actions)), dim=-1)

@@ -109,6 +109,54 @@ def xlinear(x, w, b, wg, bg, ws, bg_off=0):
     return XLinearFn.apply(x, w, b, wg, bg, bg_off, ws)
 
 
+class LinearGeluDropFn(torch.autograd.Function):
+    """h = drop(gelu(x W^T + b)) in one GEMM epilogue that also saves drop(gelu'(.)) (the feed-forward
+    first Linear + GELU + Dropout); backward: one multiply by the saved derivative, then the linear
+    backward of XLinearFn.  The dropout keep bits are the xtrl_ff_dropout_mask / fused-step stream."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, wg, bg, ws, p, seed, offset, layer):
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M = x2.shape[0]
+        assert w.is_contiguous() and b.is_contiguous()
+        y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        deriv = torch.empty(M, N, device=x.device, dtype=torch.float32)
+        L.check(L.lib().xtrl_linear_gelu_drop(L.ptr(x2), K, L.ptr(w), L.ptr(b), L.ptr(y), N, L.ptr(deriv), N, M, N, K,
+                                              float(p), int(seed) & (2 ** 64 - 1), int(offset) & 0xFFFFFFFF,
+                                              int(layer), L.stream()), 'linear_gelu_drop')
+        ctx.save_for_backward(x2, w, deriv)
+        ctx.extra = (wg, bg, ws, x.shape)
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, w, deriv = ctx.saved_tensors
+        wg, bg, ws, xshape = ctx.extra
+        N, K = w.shape
+        g = (dh.reshape(-1, N) * deriv).contiguous()
+        M = g.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, device=g.device, dtype=torch.float32)
+            if M:
+                gemm_ex(g, w, 0, 1, M, K, N, dx)
+            dx = dx.view(xshape)
+        if wg is not None and M:
+            L.check(L.lib().xtrl_gemm_wgrad_db(L.ptr(g), N, L.ptr(x2), K, L.ptr(wg), K, M, N, K, 1., L.ptr(ws), ws.numel(),
+                                               L.ptr(bg), 0, L.stream()), 'gemm_wgrad_db')
+        elif bg is not None:
+            bg.add_(g.sum(0))
+        return dx, None, None, None, None, None, None, None, None, None
+
+
+def linear_gelu_drop(x, w, b, wg, bg, ws, p, seed, offset, layer):
+    return LinearGeluDropFn.apply(x, w, b, wg, bg, ws, p, seed, offset, layer)
+
+
 def layernorm(x, gamma, out=None):
     lib = L.lib()
     M, D = x.shape
