@@ -849,13 +849,14 @@ def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, d
 # ----------------------------------------------------------------------------------------------
 
 
-def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_minibatches=2):
+def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_minibatches=2, fractal=None):
     """Rollout of the device Learner vs the oracle's batch-1 loop (actions / lengths / rewards /
     done masks bit-exact, log-probs and critic logits within 1e-4), then the first
     ``max_minibatches`` minibatches of Agent.learn: loss within 1e-4 relative and every gradient
     within 1e-4 of the gradient scale against the oracle on the GPU's weights and minibatch."""
-    learner, env, oracle = make_learner(depth=depth, gates=True, evo=evo, T=T, episodes=episodes, batch=batch, seed=4,
-                                        hazard=hazard, dim=dim, gene_dim=gene_dim)
+    learner, env, oracle = make_learner(depth=depth, gates=fractal is None, evo=evo, T=T, episodes=episodes,
+                                        batch=batch, seed=4, hazard=hazard, dim=dim, gene_dim=gene_dim,
+                                        fractal_levels=fractal)
     agent = learner.agent
     c = oracle.c
     traj, lens, genes, cum = learner.rollout_device(env, 0, T)
@@ -905,6 +906,13 @@ def test_c3_shape_rollout_and_learn_match_oracle():
     sequence length (T = 128, termination hazard 1/64), 16 episodes in minibatches of 8."""
     seen, lens = _config_parity(depth=4, dim=256, T=128, hazard=6, evo=False, episodes=16, batch=8)
     assert len(seen) == 2 and int(lens.max()) > 64     # multi-tile training attention
+
+
+def test_c5_shape_fractal_rollout_and_learn_match_oracle():
+    """C5 policy (the fractal body: 4 levels, d 256, 4 x 16 heads, causal per timestep) with EPO
+    genes at T = 128: the fractal decode step and the learn step against the streaming oracle."""
+    seen, lens = _config_parity(depth=4, dim=256, T=128, hazard=6, evo=True, episodes=4, batch=4, fractal=4)
+    assert len(seen) == 2 and int(lens.max()) > 64
 
 
 def test_c2_shape_rollout_and_learn_match_oracle():
