@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 8
+#define XTRL_ABI_VERSION 9
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -94,6 +94,10 @@ typedef struct XtrlDecodeLayer {
   const float* w_out_t;  /* [I][d]  to_out transposed (plain fp32), or NULL: when set (and the shape
                             allows) the attention kernel applies the out-projection + residual
                             itself, x += W_out o, and no out-projection GEMM runs */
+  const uint16_t* w_ff1x; /* split-bf16 images (xtrl_dgemm_pack_x6) of the unpacked [ff][d] FF1 and */
+  const uint16_t* w_ff2x; /* [d][ff] FF2 weights, or NULL: when both are set (with xn, mlp_part and
+                             mlp_cnt) FF1 + GELU + FF2 + residual + the next pre-norm run as one launch
+                             on the bf16 matrix cores (fp32 products as six piece products) */
 } XtrlDecodeLayer;
 
 typedef struct XtrlRngState {   /* device memory; read by the sampling / sim kernels */
@@ -165,6 +169,11 @@ typedef struct XtrlDecodeDesc {
    * episode slot live_rows[(t & 1) * E + r] (written by the step's embedding kernel) */
   int32_t* live_rows;        /* [2][E] */
   int32_t* live_count;       /* [2] */
+  /* the one-launch feed-forward block: partial outputs of the hidden chunks [ceil(E / 32)][ff / 128]
+   * [32][d] and one arrival counter per 16-row panel [ceil(E / 16)] (zero-initialised; every launch
+   * leaves them zero), or NULL */
+  float* mlp_part;
+  uint32_t* mlp_cnt;
   const float* lat_embed;    /* [E][d] latent_to_embed(gene) per episode slot (evolutionary) or NULL */
   /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
    * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
@@ -202,6 +211,12 @@ int xtrl_dgemm(const float* A, int lda, const float* Wp, const float* bias, cons
  * decode GEMM reads 1 KiB contiguous.  Done once per rollout (the EMA weights are fixed for it). */
 int64_t xtrl_dgemm_packed_floats(int N, int K);
 int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, void* stream);
+/* Split-bf16 fragment packing of W [N][K] (K a multiple of 32) for the v_mfma_f32_16x16x32_bf16
+ * operand: every value w = hi + mid + lo exactly (bf16 pieces); three planes (hi, mid, lo) of
+ * xtrl_dgemm_packed_x6_elems(N, K) / 3 bf16 each, the 16-byte slot (n / 16 * K / 32 + s) * 64 + lane
+ * of a plane holding W[16 (n / 16) + lane % 16][32 s + 8 (lane / 16) .. + 7], zero past N. */
+int64_t xtrl_dgemm_packed_x6_elems(int N, int K);
+int xtrl_dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fractal policy body, one decode step (fractal_rl.py:37-346, 510-619 restated per timestep and

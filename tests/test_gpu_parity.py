@@ -121,6 +121,27 @@ def test_dgemm_decode_projection(M, N, K, live, mode):
     tol(got, ref[:live], 2e-5, 2e-5)
 
 
+@pytest.mark.parametrize('N,K', [(1024, 256), (256, 1024), (20, 64)])
+def test_dgemm_pack_x6_pieces_are_exact(N, K):
+    """xtrl_dgemm_pack_x6: hi + mid + lo reproduce every fp32 weight exactly, each piece sits in the
+    16x16x32 bf16 fragment slot the fused feed-forward kernel reads, zero past N."""
+    from xtrl_amd import _lib as L
+    g = torch.Generator().manual_seed(N + K)
+    w = (torch.randn(N, K, generator=g) * torch.exp(torch.randn(N, K, generator=g))).to(DEV)
+    out = torch.zeros(int(L.lib().xtrl_dgemm_packed_x6_elems(N, K)), dtype=torch.int16, device=DEV)
+    L.check(L.lib().xtrl_dgemm_pack_x6(L.ptr(w), K, N, K, L.ptr(out), L.stream()), 'dgemm_pack_x6')
+    torch.cuda.synchronize()
+    Np = (N + 15) // 16 * 16
+    bits = out.view(3, Np // 16, K // 32, 4, 16, 8).cpu().to(torch.int32) & 0xFFFF   # piece, tile, step, q, row, j
+    f = (bits << 16).view(torch.float32)
+    pieces = f.permute(0, 1, 4, 2, 3, 5).reshape(3, Np, K)   # [piece][n][k = 32 step + 8 q + j]
+    # the smallest piece first, as the kernel's products: exact because the pieces do not overlap
+    total = (pieces[2] + pieces[1]) + pieces[0]
+    assert torch.equal(total[:N], w.cpu())
+    assert float(total[N:].abs().sum()) == 0.
+    assert bool((pieces[0][:N].abs() >= pieces[1][:N].abs()).all())
+
+
 def _dot_scale(a, b):
     """sum_k |a[m, k] b[k, n]| (the scale of an fp32 dot product's rounding error)."""
     return a.abs() @ b.abs()
@@ -405,8 +426,10 @@ def test_rollout_continuous_matches_oracle():
     compare_rollout(traj, lens, episodes, cont=True)
 
 
-def test_rollout_graph_replay_equals_eager():
-    learner, env, _ = make_learner(depth=2, T=16, episodes=16)
+@pytest.mark.parametrize('dim', [48, 256])
+def test_rollout_graph_replay_equals_eager(dim):
+    """dim 256: the one-launch feed-forward kernel (its per-panel arrival counters reset in-graph)."""
+    learner, env, _ = make_learner(depth=2, T=16, episodes=40, dim=dim)
     traj, lens, _, _ = learner.rollout_device(env, 0, 16)
     eager = {k: v.clone() for k, v in traj.items() if v is not None}
     learner.use_graph = True

@@ -29,6 +29,7 @@
 // [E][Tmax][.] so the learner reads whole episodes contiguously.
 #include "dgemm_body.h"
 #include "kernels.h"
+#include "x6.h"
 #include "philox.h"
 
 namespace xtrl {
@@ -795,6 +796,250 @@ bool attn_fused(const XtrlDecodeDesc* D, int l) {
          D->d <= 4 * 64 * D->H && lds <= 160 * 1024;
 }
 
+// ---------------------------------------------------------------------------------------------
+// the feed-forward block of a decode layer in ONE launch (replaces the FF1 and FF2 projections):
+// workgroup (hidden chunk c, 16-row panel p) computes h_c = GELU(xn W1[c]^T + b1[c]) for its 16
+// live rows and 128 hidden units (kept in LDS) and the partial output h_c W2[:, c]^T (16 x d).  The
+// ff / 128 partials of a panel meet through the cross-workgroup hand-off of the MI355X guide (sc1
+// stores and loads, no fences): every workgroup stores its partial tile with sc1 stores, every wave
+// waits for them, and behind a workgroup barrier one lane adds to the panel's arrival counter
+// (agent scope); the workgroup whose add returned ff/128 - 1 sums the partials in chunk order
+// (sc1 loads) onto the residual row and b2, stores the layer output and the next pre-norm of it,
+// and zeroes the counter.  Every chunk workgroup of a live panel is live, so the count always
+// completes; nothing waits or polls.  Both products run on the bf16 matrix cores as split-bf16
+// ("X6", x6.h: fp32-accurate): the weights pre-split at pack time (xtrl_dgemm_pack_x6), the
+// activations split as their fragments are read from LDS (6 x 16 cycles per 32-deep step instead
+// of 8 x 32 for the f32 MFMA: at E = 1024 the fp32 feed-forward was matrix-core bound).
+// ---------------------------------------------------------------------------------------------
+constexpr int MLP_HW = 128;   // hidden units per workgroup
+
+// fp32 operands as split-bf16 pieces: 8 consecutive values -> hi / mid / lo bf16x8 fragments
+__device__ __forceinline__ void split3x8(const f32x4v a, const f32x4v b, bf16x8& h, bf16x8& m, bf16x8& l) {
+  uint32_t hh[4], mm[4], ll[4];
+  split3_pair(a[0], a[1], hh[0], mm[0], ll[0]);
+  split3_pair(a[2], a[3], hh[1], mm[1], ll[1]);
+  split3_pair(b[0], b[1], hh[2], mm[2], ll[2]);
+  split3_pair(b[2], b[3], hh[3], mm[3], ll[3]);
+  h = __builtin_bit_cast(bf16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+  m = __builtin_bit_cast(bf16x8, make_uint4(mm[0], mm[1], mm[2], mm[3]));
+  l = __builtin_bit_cast(bf16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+}
+// acc += a . b over 32 k as the six largest piece products, smallest first (x6.h)
+__device__ __forceinline__ f32x4v mfma_x6(const bf16x8 (&a)[3], const uint4 (&b)[3], f32x4v c) {
+  const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]), bm = __builtin_bit_cast(bf16x8, b[1]),
+               bl = __builtin_bit_cast(bf16x8, b[2]);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bh, c, 0, 0, 0);
+}
+
+template <int NT2, int MT>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
+__global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, float* C,
+                                             int ldc, const float* g_next, float* Y, int ldy) {
+  constexpr int d = 64 * NT2, NT1 = MLP_HW / 64, BM = 16 * MT;
+  constexpr int LDA = d + 4, JS1 = d / 32;              // FF1: K = d, 32-deep k steps
+  constexpr int LDH = MLP_HW + 4, JSC = MLP_HW / 32;    // FF2: the chunk's 128 k
+  __shared__ __attribute__((aligned(16))) float A1[BM * LDA];
+  __shared__ __attribute__((aligned(16))) float Hs[BM * LDH];
+  __shared__ int last_sh;
+  const int HC = D.ff / MLP_HW, JS2 = D.ff / 32;
+  const int c = blockIdx.x, p = blockIdx.y, m0 = p * BM;
+  const int M = D.live_count[t & 1];
+  if (m0 >= M) return;   // (workgroup-uniform)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, q = lane >> 4;
+  // ---- operands: the panel's xn rows (LDS-DMA, one 1 KiB piece per row; the destination is the
+  //      wave's row base, lane i lands 16 i bytes further), this wave's W1 piece fragments of the
+  //      chunk (all of K in one batch), b1
+  if (4 * lane < d)
+    for (int r = w; r < BM; r += 4)
+      __builtin_amdgcn_global_load_lds((const void*)(D.xn + (int64_t)min(m0 + r, M - 1) * d + 4 * lane),
+                                       (lds_void*)(A1 + r * LDA), 16, 0, 0);
+  const uint4* w1 = reinterpret_cast<const uint4*>(Ly.w_ff1x);
+  const int64_t P1 = (int64_t)D.ff / 16 * JS1 * 64;   // slots per piece plane
+  uint4 bw[NT1][JS1][3];
+  float b1v[NT1];
+#pragma unroll
+  for (int nt = 0; nt < NT1; ++nt) {
+    const int t16 = c * (MLP_HW / 16) + w * NT1 + nt;
+    const uint4* wp = w1 + (int64_t)t16 * JS1 * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < JS1; ++s)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) bw[nt][s][pc] = wp[pc * P1 + 64 * s];
+    b1v[nt] = Ly.b_ff1[t16 * 16 + lr];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // ---- FF1 chunk + GELU -> Hs
+  {
+    f32x4v acc[MT][NT1][2];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt) acc[mt][nt][0] = acc[mt][nt][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < JS1; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float* ap = A1 + (16 * mt + lr) * LDA + 32 * s + 8 * q;
+        bf16x8 a[3];
+        split3x8(*reinterpret_cast<const f32x4v*>(ap), *reinterpret_cast<const f32x4v*>(ap + 4), a[0], a[1], a[2]);
+#pragma unroll
+        for (int nt = 0; nt < NT1; ++nt) acc[mt][nt][s & 1] = mfma_x6(a, bw[nt][s], acc[mt][nt][s & 1]);
+      }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT1; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          Hs[(16 * mt + 4 * q + i) * LDH + w * 16 * NT1 + 16 * nt + lr] =
+              geluf_((acc[mt][nt][0][i] + acc[mt][nt][1][i]) + b1v[nt]);
+  }
+  // ---- this wave's W2 piece fragments: tiles w NT2 + nt, k steps of chunk c (issued after FF1:
+  //      with the first batch they would double the registers)
+  const uint4* w2 = reinterpret_cast<const uint4*>(Ly.w_ff2x);
+  const int64_t P2 = (int64_t)(d / 16) * JS2 * 64;
+  uint4 b2w[NT2][JSC][3];
+#pragma unroll
+  for (int nt = 0; nt < NT2; ++nt) {
+    const uint4* wp = w2 + ((int64_t)(w * NT2 + nt) * JS2 + c * JSC) * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < JSC; ++s)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) b2w[nt][s][pc] = wp[pc * P2 + 64 * s];
+  }
+  __syncthreads();   // (Hs complete)
+  // ---- FF2 partial of the chunk -> sc1 stores
+  {
+    f32x4v acc[MT][NT2][2];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT2; ++nt) acc[mt][nt][0] = acc[mt][nt][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < JSC; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float* ap = Hs + (16 * mt + lr) * LDH + 32 * s + 8 * q;
+        bf16x8 a[3];
+        split3x8(*reinterpret_cast<const f32x4v*>(ap), *reinterpret_cast<const f32x4v*>(ap + 4), a[0], a[1], a[2]);
+#pragma unroll
+        for (int nt = 0; nt < NT2; ++nt) acc[mt][nt][s & 1] = mfma_x6(a, b2w[nt][s], acc[mt][nt][s & 1]);
+      }
+    float* part = D.mlp_part + ((int64_t)p * HC + c) * BM * d;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT2; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          __hip_atomic_store(part + (16 * mt + 4 * q + i) * d + w * 16 * NT2 + 16 * nt + lr,
+                             acc[mt][nt][0][i] + acc[mt][nt][1][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its partial stores have completed
+  __syncthreads();
+  if (tid == 0)
+    last_sh = __hip_atomic_fetch_add(D.mlp_cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(HC - 1);
+  __syncthreads();
+  if (!last_sh) return;   // (workgroup-uniform)
+  // ---- the last chunk workgroup of the panel: residual + b2 + the partials in chunk order (every
+  //      load issued before the first store: C may be the residual row itself)
+  constexpr int EPT = BM * d / 256;   // elements per thread
+  const float* part0 = D.mlp_part + (int64_t)p * HC * BM * d;
+  float v[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = tid + 256 * k, r = e / d, col = e - r * d;
+    v[k] = D.x[(int64_t)min(m0 + r, M - 1) * d + col] + Ly.b_ff2[col];
+  }
+  for (int cc = 0; cc < HC; ++cc)
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = tid + 256 * k, r = e / d, col = e - r * d;
+      v[k] += __hip_atomic_load(part0 + ((int64_t)cc * BM + r) * d + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  if (tid == 0) __hip_atomic_store(D.mlp_cnt + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = tid + 256 * k, r = e / d, col = e - r * d, m = m0 + r;
+    if (C && m < M) C[(int64_t)m * ldc + col] = v[k];
+    A1[r * LDA + col] = v[k];   // (A1 is free: every wave is past its FF1)
+  }
+  // the next pre-norm of the completed rows (the next layer's attention LayerNorm, or the final norm
+  // in the heads' input row), two-pass as the GEMM prologue: one wave per BM / 4 rows
+  __syncthreads();
+#pragma unroll
+  for (int rr = 0; rr < BM / 4; ++rr) {
+    const int r = (BM / 4) * w + rr, m = m0 + r;
+    float xv[NT2], sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT2; ++j) {
+      xv[j] = A1[r * LDA + lane + 64 * j];
+      sm += xv[j];
+    }
+    const float mean = wave_sum_dpp(sm) / (float)d;
+    float qq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT2; ++j) {
+      const float dl = xv[j] - mean;
+      qq += dl * dl;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+    if (m < M)
+#pragma unroll
+      for (int j = 0; j < NT2; ++j)
+        Y[(int64_t)m * ldy + lane + 64 * j] = ((xv[j] - mean) * rstd) * g_next[lane + 64 * j];
+  }
+}
+
+// panel rows of the fused feed-forward: 16; XTRL_MLP_ROWS=32 (experiments) feeds every weight
+// fragment to twice the rows on half the workgroups — measured slower at C3 (26.2 vs 19.7 us a
+// launch, rollout 26.5 vs 23.2 ms: the per-wave MFMA chain doubles and one workgroup per CU is left)
+int mlp_rows() {
+  static const int r = [] {
+    const char* e = getenv("XTRL_MLP_ROWS");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return r;
+}
+
+bool mlp_fused(const XtrlDecodeDesc* D, int l) {
+  return D->xn && D->mlp_part && D->mlp_cnt && D->layers[l].w_ff1x && D->layers[l].w_ff2x && attn_fused(D, l) &&
+         D->d % 64 == 0 &&
+         D->d <= 256 && D->ff % MLP_HW == 0;
+}
+
+// layer l's feed-forward: x += FF(xn), then the next pre-norm of the rows — the last layer writes only
+// the final-normed row into the heads' input (nothing reads its raw output), the others x and xn
+int launch_mlp(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
+  const int bm = mlp_rows();
+  const dim3 grid(D->ff / MLP_HW, (D->E + bm - 1) / bm);
+  const XtrlDecodeLayer& Ly = D->layers[l];
+  const bool last = l == D->L - 1;
+  float* C = last ? nullptr : D->x;
+  const float* g = last ? D->ln_final : D->layers[l + 1].ln_attn;
+  float* Y = last ? D->ac_in : D->xn;
+  const int ldc = D->d, ldy = last ? D->in_dim : D->d;
+#define XTRL_MLP(NT2)                                                                              \
+  do {                                                                                             \
+    if (bm == 32) hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, C, ldc, g, Y, ldy); \
+    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, C, ldc, g, Y, ldy);          \
+  } while (0)
+  switch (D->d / 64) {
+    case 1: XTRL_MLP(1); break;
+    case 2: XTRL_MLP(2); break;
+    case 3: XTRL_MLP(3); break;
+    default: XTRL_MLP(4); break;
+  }
+#undef XTRL_MLP
+  XTRL_LAUNCHED("mlp");
+  return XTRL_OK;
+}
+
 int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
   if (attn_fused(D, l)) {   // one workgroup of H waves per live row
     const size_t lds = ((size_t)D->H * (D->Tmax + 3 * D->dh) + (size_t)D->H * D->d) * sizeof(float);
@@ -877,12 +1122,13 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
   const int d = D->d, I = D->H * D->dh, ff = D->ff;
   int rc;
   // xn: the LayerNorm of a row computed by the kernel that completes it (embedding -> layer 0's
-  // q|k|v, fused attention -> FF1); the other pre-norms run in the GEMM prologue
+  // q|k|v, fused attention -> FF1, fused feed-forward -> the next q|k|v or the heads); the other
+  // pre-norms run in the GEMM prologue
   const bool xn = D->xn != nullptr;
   if ((rc = launch_embed(D, t, xn ? D->layers[0].ln_attn : nullptr, s))) return rc;
   for (int l = 0; l < D->L; ++l) {
     const XtrlDecodeLayer& Ly = D->layers[l];
-    const bool xn_qkv = xn && l == 0, xn_ff = xn && attn_fused(D, l);
+    const bool xn_qkv = xn && (l == 0 || mlp_fused(D, l - 1)), xn_ff = xn && attn_fused(D, l);
     if ((rc = dproj(D, t, xn_qkv ? D->xn : D->x, d, Ly.w_qkv, d, Ly.b_qkv, xn_qkv ? nullptr : Ly.ln_attn,
                     xn_qkv ? 0 : d, nullptr, 0, D->qkv, D->n_qkv, D->n_qkv, EPI_NONE, s)))
       return rc;
@@ -892,16 +1138,20 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
     if (!attn_fused(D, l) &&
         (rc = dproj(D, t, D->att, I, Ly.w_out, I, nullptr, nullptr, 0, D->x, d, D->x, d, d, EPI_NONE, s)))
       return rc;
+    // the last layer's output goes straight into the heads' input row (final norm in their prologue)
+    const bool last = l == D->L - 1;
+    if (mlp_fused(D, l)) {   // FF1 + GELU + FF2 + residual + the next pre-norm: one launch
+      if ((rc = launch_mlp(D, l, t, s))) return rc;
+      continue;
+    }
     if ((rc = dproj(D, t, xn_ff ? D->xn : D->x, d, Ly.w_ff1, d, Ly.b_ff1, xn_ff ? nullptr : Ly.ln_ff, xn_ff ? 0 : d,
                     nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
       return rc;
-    // the last layer's output goes straight into the heads' input row (final norm in their prologue)
-    const bool last = l == D->L - 1;
     if ((rc = dproj(D, t, D->hff, ff, Ly.w_ff2, ff, Ly.b_ff2, nullptr, 0, D->x, d, last ? D->ac_in : D->x,
                     last ? D->in_dim : d, d, EPI_NONE, s)))
       return rc;
   }
-  return decode_heads(D, t, true, s);
+  return decode_heads(D, t, !mlp_fused(D, D->L - 1), s);
 }
 
 int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t, hipStream_t s) {

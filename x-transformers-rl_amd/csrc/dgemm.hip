@@ -31,6 +31,7 @@
 #include <cstdlib>
 
 #include "dgemm_body.h"
+#include "x6.h"
 
 namespace xtrl {
 
@@ -57,6 +58,27 @@ __global__ void k_dg_pack(const float* W, int ldw, int N, int K, float* Wp) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] = (n < N && k0 + i < K) ? W[(int64_t)n * ldw + k0 + i] : 0.f;
   reinterpret_cast<float4*>(Wp)[s] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// split-bf16 fragment packing for the 16x16x32 bf16 operand (one thread per 16-byte slot of each plane)
+__global__ void k_dg_pack_x6(const float* W, int ldw, int N, int K, uint4* Wp) {
+  const int JS = K >> 5;
+  const int64_t slots = (int64_t)((N + 15) >> 4) * JS * 64;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= slots) return;
+  const int lane = (int)(s & 63);
+  const int64_t rest = s >> 6;
+  const int sk = (int)(rest % JS), t16 = (int)(rest / JS);
+  const int n = 16 * t16 + (lane & 15), k0 = 32 * sk + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = n < N ? W[(int64_t)n * ldw + k0 + i] : 0.f;
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split3_pair(v[2 * i], v[2 * i + 1], h[i], m[i], l[i]);
+  Wp[s] = make_uint4(h[0], h[1], h[2], h[3]);
+  Wp[slots + s] = make_uint4(m[0], m[1], m[2], m[3]);
+  Wp[2 * slots + s] = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
 template <int MT, int NT, int KS, int EPI, bool LN, bool RES>
@@ -105,6 +127,18 @@ int dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s) 
   return XTRL_OK;
 }
 
+int64_t dgemm_packed_x6_elems(int N, int K) { return (int64_t)3 * ((N + 15) / 16) * 16 * K; }
+
+int dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, hipStream_t s) {
+  XTRL_REQUIRE(W && Wp && N > 0 && K > 0 && K % 32 == 0 && ldw >= K && ((uintptr_t)Wp & 15u) == 0,
+               "dgemm_pack_x6: bad arguments (K a multiple of 32, Wp 16-byte aligned)");
+  const int64_t slots = dgemm_packed_x6_elems(N, K) / 24;
+  hipLaunchKernelGGL(k_dg_pack_x6, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, W, ldw, N, K,
+                     reinterpret_cast<uint4*>(Wp));
+  XTRL_LAUNCHED("dgemm_pack_x6");
+  return XTRL_OK;
+}
+
 int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s) {
   XTRL_REQUIRE(a.A && a.W && a.C && a.K > 0 && a.N > 0 && rows >= 0, "dgemm: bad operands");
   XTRL_REQUIRE(a.K % 4 == 0 && a.lda % 4 == 0 && ((uintptr_t)a.A & 15u) == 0 && ((uintptr_t)a.W & 15u) == 0,
@@ -141,6 +175,10 @@ int dgemm_run(const DGemmArgs& a, int rows, int epi, hipStream_t s) {
 extern "C" int64_t xtrl_dgemm_packed_floats(int N, int K) { return xtrl::dgemm_packed_floats(N, K); }
 extern "C" int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, void* stream) {
   return xtrl::dgemm_pack(W, ldw, N, K, Wp, xtrl::as_stream(stream));
+}
+extern "C" int64_t xtrl_dgemm_packed_x6_elems(int N, int K) { return xtrl::dgemm_packed_x6_elems(N, K); }
+extern "C" int xtrl_dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, void* stream) {
+  return xtrl::dgemm_pack_x6(W, ldw, N, K, Wp, xtrl::as_stream(stream));
 }
 extern "C" int xtrl_dgemm(const float* A, int lda, const float* Wp, const float* bias, const float* ln_gamma, int ln_k,
                           const float* R, int ldr, float* C, int ldc, const int32_t* row_map, const int32_t* m_dev,

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -28,7 +28,7 @@ LOSS_TOK, LOSS_STATS = 30, 32
 
 class DecodeLayer(C.Structure):
     _fields_ = [(n, P) for n in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2',
-                                 'k_cache', 'v_cache', 'w_out_t')]
+                                 'k_cache', 'v_cache', 'w_out_t', 'w_ff1x', 'w_ff2x')]
 
 
 class RngState(C.Structure):
@@ -48,7 +48,7 @@ class DecodeDesc(C.Structure):
                                     'alive', 'lens', 'cum_reward', 'episode_of_slot', 'slot_of_row', 'rng', 'traj_states',
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
                                     'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count',
-                                    'lat_embed')]
+                                    'mlp_part', 'mlp_cnt', 'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))])
 
 
@@ -122,6 +122,8 @@ SIGNATURES = {
     'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),
     'xtrl_fractal_decode_step': (I32, [C.POINTER(DecodeDesc), C.POINTER(FractalDesc), I32, P]),
     'xtrl_dgemm_packed_floats': (I64, [I32, I32]),
+    'xtrl_dgemm_pack_x6': (I32, [P, I32, I32, I32, P, P]),
+    'xtrl_dgemm_packed_x6_elems': (I64, [I32, I32]),
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P, P, P]),
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),

@@ -17,6 +17,7 @@ sync and terminated episodes cost nothing.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import dataclasses
 
 import torch
@@ -59,6 +60,11 @@ class RolloutEngine:
         self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
         self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
         self.xn = z(E, d)
+        # one-launch feed-forward (k_mlp): per 16-row panel, one FF2 partial per 128-wide hidden chunk
+        # and the panel's arrival counter (the last chunk workgroup sums the partials and resets it)
+        n_chunk = ff // 128 if (ff % 128 == 0 and d % 64 == 0 and d <= 256) else 0
+        self.mlp_part = z(((E + 31) // 32) * 32 * n_chunk * d) if n_chunk else None   # (16- or 32-row panels)
+        self.mlp_cnt = z((E + 15) // 16, dt=i32) if n_chunk else None
         self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
         # decode weights (nn.Linear layouts; the GEMM operands are packed from them, self.wpk)
         self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
@@ -81,6 +87,11 @@ class RolloutEngine:
         # w_out_t: to_out transposed for the attention kernel's fused out-projection
         self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), w_out_t=z(I, d),
                         ln_ff=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+        # w_ff1x / w_ff2x: split-bf16 images of FF1 / FF2 for the one-launch feed-forward kernel
+        if ff % 128 == 0 and d % 64 == 0 and d <= 256:
+            n1, n2 = (int(L.lib().xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
+            for wl in self.wl:
+                wl['w_ff1x'], wl['w_ff2x'] = z(n1, dt=torch.int16), z(n2, dt=torch.int16)
         self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
 
     def _wv(self, src, k):
@@ -96,7 +107,7 @@ class RolloutEngine:
         for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
             layers[i] = L.DecodeLayer(*(self._wv(w, k) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
                                                                  'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc),
-                                      self._wv(w, 'w_out_t'))
+                                      self._wv(w, 'w_out_t'), self._wv(w, 'w_ff1x'), self._wv(w, 'w_ff2x'))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -119,8 +130,11 @@ class RolloutEngine:
         D.rng = self.rng.data_ptr()
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
-        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count', 'lat_embed'):
+        for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count', 'lat_embed',
+                  'mlp_part', 'mlp_cnt'):
             setattr(D, k, rows(getattr(self, k)))
+        if os.environ.get('XTRL_DECODE_MLP', '1') == '0':   # A/B switch: the two-GEMM feed-forward
+            D.mlp_part = None
         self.desc, self._layers = D, layers
 
     # ------------------------------------------------------------------------------------------
@@ -194,6 +208,12 @@ class RolloutEngine:
             t = src[k]
             L.check(lib.xtrl_dgemm_pack(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(self.wpk[(id(src), k)]),
                                         L.stream()), f'dgemm_pack({k})')
+        for wl in getattr(self, 'wl', ()):
+            for src, dst in (('w_ff1', 'w_ff1x'), ('w_ff2', 'w_ff2x')):
+                if dst in wl:
+                    t = wl[src]
+                    L.check(lib.xtrl_dgemm_pack_x6(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(wl[dst]),
+                                                   L.stream()), f'dgemm_pack_x6({src})')
 
     # ------------------------------------------------------------------------------------------
     def _begin(self, seed, update, slot_offset, episode_of_slot, latent, slots=None):
