@@ -784,11 +784,11 @@ def test_e2e_reference_contract(evolutionary, continuous_actions, tmp_path):
     assert (tmp_path / 'ppo.pt').exists()
 
 
-@pytest.mark.parametrize('frac', [None, 2])
-def test_deploy_forward_matches_oracle_cached_decode(frac):
+@pytest.mark.parametrize('frac,dim', [(None, 48), (2, 48), (None, 256)])
+def test_deploy_forward_matches_oracle_cached_decode(frac, dim):
     """Agent.forward (online model, KV cache — and for the fractal body the level running sums —
-    threaded through hiddens) vs the oracle module."""
-    learner, env, oracle = make_learner(depth=2, gates=frac is None, fractal_levels=frac)
+    threaded through hiddens) vs the oracle module; dim 256: the one-launch feed-forward at E = 1."""
+    learner, env, oracle = make_learner(depth=2, gates=frac is None, fractal_levels=frac, dim=dim)
     agent = learner.agent
     agent.rs_mean.copy_(torch.linspace(-0.5, 0.5, 9))
     agent.rs_var.copy_(torch.linspace(0.5, 2., 9))
@@ -1081,13 +1081,14 @@ def test_host_env_scalar_contract_matches_oracle(ret, limit):
         assert any(ep['boot'] is not None for ep in episodes)     # some episodes truncated
 
 
-@pytest.mark.parametrize('frac', [None, 2])
-def test_host_env_vectorised_waves_match_oracle(frac):
+@pytest.mark.parametrize('frac,dim', [(None, 48), (2, 48), (None, 256)])
+def test_host_env_vectorised_waves_match_oracle(frac, dim):
     """A vectorised env of 4 sub-envs over 2 genes x 5 episodes (10 pairs: waves of 4, 4, 2 — the
     last one partial), evolutionary with per-episode reset seeds, truncation at 6 steps (the
-    truncation bootstrap step included); decoder and fractal policy bodies."""
+    truncation bootstrap step included); decoder and fractal policy bodies (dim 256: the decoder's
+    one-launch feed-forward writing the final norm into the 3d-wide heads' input row)."""
     learner, _, oracle = make_learner(depth=2, gates=frac is None, evo=True, T=8, episodes=5, batch=5,
-                                      fractal_levels=frac)
+                                      fractal_levels=frac, dim=dim)
     seeds = torch.randint(0, 10 ** 7, (5,), generator=torch.Generator().manual_seed(3))
     _, _, genes, cum, episodes, fitness = _compare_host(learner, oracle, HostLanderVec(4, limit=6),
                                                         HostLander(limit=6), 8, seeds)
