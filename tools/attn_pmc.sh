@@ -17,7 +17,7 @@ from collections import defaultdict
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob('gpurun_out/attn_pmc/**/*counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'].split('(')[0].replace('void xtrl::', '').replace('(anonymous namespace)::', '')
+        k = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0].replace('void xtrl::', '')
         acc[k][r['Counter_Name']].append(float(r['Counter_Value']))
 for k, d in acc.items():
     print(k)
