@@ -151,33 +151,94 @@ __global__ __launch_bounds__(64 * LT_W) void k_loss_tokens(const XtrlLossDesc D)
   const bool valid = tk0 < N;   // (waves past N evaluate the last token and store nothing)
   const int tk = valid ? tk0 : N - 1;
   const int bi = tk / D.n, ti = tk - bi * D.n;
+  // every operand of the token in one batch of loads (the terms below are chains of wave
+  // reductions; loading inside them cost one memory round trip per stage): value and old-value
+  // logits, bin centres and edges of lanes k and k + 64, the prediction and next real row (c = lane),
+  // the action logits (lane < A) and the token's scalars.  Same arithmetic, same order, as loading
+  // on use.
+  const int B = D.B;
+  const float* vals = D.values + (int64_t)tk * B;
+  const float* ovals = D.old_values + (int64_t)tk * B;
+  const bool k0 = lane < B, k1 = lane + 64 < B;
+  const float x0 = k0 ? vals[lane] : 0.f, x1 = k1 ? vals[lane + 64] : 0.f;
+  const float y0 = k0 ? ovals[lane] : 0.f, y1 = k1 ? ovals[lane + 64] : 0.f;
+  const float c0 = k0 ? D.centers[lane] : 0.f, c1 = k1 ? D.centers[lane + 64] : 0.f;
+  const float e0 = lane <= B ? D.support[lane] : 0.f, e1 = lane + 64 <= B ? D.support[lane + 64] : 0.f;
+  const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
+  const bool c_in = lane < D.S1;
+  const float pm = c_in ? pr[2 * lane] : 0.f, plv = c_in ? pr[2 * lane + 1] : 0.f;
+  const float yr = c_in ? D.real[((int64_t)min(tk + 1, N - 1)) * D.S1 + lane] : 0.f;
+  const float rawv = (!D.continuous && lane < D.A) ? D.raw_actions[(int64_t)tk * D.A + lane] : 0.f;
+  const int act = D.continuous ? 0 : D.actions[tk];
+  const float ret = D.returns[tk], zlog = D.done_logit[tk];
+  const bool dn = D.dones[tk] != 0;
   const bool mask = ti < D.lens[bi];
   float* tok = D.tok + (int64_t)tk * NT;
-  const float* vals = D.values + (int64_t)tk * D.B;
-  const float* ovals = D.old_values + (int64_t)tk * D.B;
-  const RowStats rn = row_stats(vals, D.centers, D.B, lane);
-  const RowStats ro = row_stats(ovals, D.centers, D.B, lane);
-  const float ret = D.returns[tk];
-  const float ceu = hl_ce(D, vals, rn.lse, ret, lane);
-  const float cec = hl_ce(D, vals, rn.lse, fminf(fmaxf(ret, -D.value_clip), D.value_clip), lane);
+  // softmax statistics of the value and old-value rows (row_stats on registers)
+  auto stats = [&](float a0, float a1) -> RowStats {
+    float mx = -INFINITY;
+    if (k0) mx = fmaxf(mx, a0);
+    if (k1) mx = fmaxf(mx, a1);
+    mx = wave_max(mx);
+    float sm = 0.f, sc = 0.f;
+    if (k0) {
+      const float e = expf(a0 - mx);
+      sm += e;
+      sc += e * c0;
+    }
+    if (k1) {
+      const float e = expf(a1 - mx);
+      sm += e;
+      sc += e * c1;
+    }
+    sm = wave_sum(sm);
+    sc = wave_sum(sc);
+    return {mx, mx + logf(sm), sc / sm};
+  };
+  const RowStats rn = stats(x0, x1);
+  const RowStats ro = stats(y0, y1);
+  // HL-Gauss cross entropy (hl_targets / hl_ce on the edges in registers)
+  const float inv = 1.0f / (1.41421356237309505f * D.sigma);
+  auto ce = [&](float y) -> float {
+    y = fminf(fmaxf(y, D.lo), D.hi);
+    const float f0 = lane <= B ? erff((e0 - y) * inv) : 0.f;
+    const float f1 = lane + 64 <= B ? erff((e1 - y) * inv) : 0.f;
+    const int nb = (lane + 1) & 63;
+    const float n0s = __shfl(f0, nb, 64), n1 = __shfl(f1, nb, 64), f64 = __shfl(f1, 0, 64);
+    const float n0 = lane == 63 ? f64 : n0s;
+    const float cB = B < 64 ? __shfl(f0, B, 64) : __shfl(f1, B - 64, 64);
+    const float z = cB - __shfl(f0, 0, 64);
+    const float t0 = k0 ? (n0 - f0) / z : 0.f, t1 = k1 ? (n1 - f1) / z : 0.f;
+    float acc = 0.f;
+    if (k0) acc += t0 * (x0 - rn.lse);
+    if (k1) acc += t1 * (x1 - rn.lse);
+    return -wave_sum(acc);
+  };
+  const float ceu = ce(ret);
+  const float cec = ce(fminf(fmaxf(ret, -D.value_clip), D.value_clip));
   // world model: predictions at t predict the normalised state-with-reward at t + 1
   const bool wm_on = mask && ti < D.n - 1;
   float wm = 0.f;
   if (wm_on) {
     for (int c = lane; c < D.S1; c += 64) {
-      const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
-      const float mean = pr[2 * c];
-      const float var = expf(tanhf(pr[2 * c + 1] / 3.f) * 3.f);
+      const float mean = c == lane ? pm : pr[2 * c];
+      const float var = expf(tanhf((c == lane ? plv : pr[2 * c + 1]) / 3.f) * 3.f);
       const float vv = fmaxf(var, 1e-6f);
-      const float y = D.real[((int64_t)tk + 1) * D.S1 + c];
+      const float y = c == lane ? yr : D.real[((int64_t)tk + 1) * D.S1 + c];
       wm += 0.5f * (logf(vv) + (mean - y) * (mean - y) / vv);
     }
     wm = wave_sum(wm);
   }
+  // the action logits to every lane (lane 0 evaluates the discrete terms)
+  float rawa[32];
+  if (!D.continuous) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) rawa[i] = __shfl(rawv, i, 64);
+  }
   if (lane == 0) {
     const float adv = ret - ro.dot_centers;
-    const float pd = sigmoidf_(D.done_logit[tk]);
-    const float y = D.dones[tk] ? 1.f : 0.f;
+    const float pd = sigmoidf_(zlog);
+    const float y = dn ? 1.f : 0.f;
     const float l1 = fmaxf(logf(pd), -100.f), l0 = fmaxf(logf(1.f - pd), -100.f);
     const float bce = -(y * l1 + (1.f - y) * l0);
     if (valid) {
@@ -189,7 +250,7 @@ __global__ __launch_bounds__(64 * LT_W) void k_loss_tokens(const XtrlLossDesc D)
       tok[T_CEC] = cec;
       if (!D.continuous) {
         DiscreteTerms T;
-        discrete_terms(D.raw_actions + (int64_t)tk * D.A, D.A, D.actions[tk], T);
+        discrete_terms(rawa, D.A, act, T);
         tok[T_LP] = T.lp;
         tok[T_ENT] = T.ent;
       }
@@ -373,68 +434,95 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
   const int N = D.b * D.n;
   if (tk >= N) return;
   const int bi = tk / D.n, ti = tk - bi * D.n;
-  const bool mask = ti < D.lens[bi];
+  // every operand of the token in one batch of loads (as k_loss_tokens; same arithmetic and order
+  // as loading on use): the forward's per-token terms and the loss statistics, value logits and bin
+  // edges of lanes k and k + 64, the prediction and next real row (c = lane), the token's scalars
+  const int B = D.B;
+  const bool k0 = lane < B, k1 = lane + 64 < B;
+  const float* x = D.values + (int64_t)tk * B;
+  const float x0 = k0 ? x[lane] : 0.f, x1 = k1 ? x[lane + 64] : 0.f;
+  const float e0 = lane <= B ? D.support[lane] : 0.f, e1 = lane + 64 <= B ? D.support[lane + 64] : 0.f;
+  const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
+  const bool c_in = lane < D.S1;
+  const float pm = c_in ? pr[2 * lane] : 0.f, plv = c_in ? pr[2 * lane + 1] : 0.f;
+  const float yr = c_in ? D.real[((int64_t)min(tk + 1, N - 1)) * D.S1 + lane] : 0.f;
   const float* st = D.stats;
   const float* tok = D.tok + (int64_t)tk * NT;
-  const float n_mask = st[XTRL_LS_NMASK];
+  const float t_adv = tok[T_ADV], t_v = tok[T_V], t_vold = tok[T_VOLD], t_ceu = tok[T_CEU], t_cec = tok[T_CEC],
+              t_lse = tok[T_LSE];
+  const float s_nmask = st[XTRL_LS_NMASK], s_mean = st[XTRL_LS_ADV_MEAN], s_den = st[XTRL_LS_ADV_DEN],
+              s_dl = st[XTRL_LS_DL], s_dlc = st[XTRL_LS_DLC], s_nwm = st[XTRL_LS_NWM];
+  const float ret = D.returns[tk], zlog = D.done_logit[tk];
+  const bool dn = D.dones[tk] != 0;
+  const bool mask = ti < D.lens[bi];
+  const float n_mask = s_nmask;
   const float coef_ac = mask ? g / n_mask : 0.f;
-  const float advn = (tok[T_ADV] - st[XTRL_LS_ADV_MEAN]) / st[XTRL_LS_ADV_DEN];
+  const float advn = (t_adv - s_mean) / s_den;
   const float lo = 1.f - D.eps_clip, hi = 1.f + D.eps_clip;
 
   // ---- critic: d/dvalues
   {
-    const float* x = D.values + (int64_t)tk * D.B;
     float du, dc;   // weights of the unclipped / clipped CE gradients
     if (D.hl_reduction_mean) {
-      du = g * st[XTRL_LS_DL] / (float)N;
-      dc = g * st[XTRL_LS_DLC] / (float)N;
+      du = g * s_dl / (float)N;
+      dc = g * s_dlc / (float)N;
     } else {
-      const bool zero = critic_zeroed(tok[T_V], D.returns[tk], tok[T_VOLD], D.value_clip);
+      const bool zero = critic_zeroed(t_v, ret, t_vold, D.value_clip);
       const float w = zero ? 0.f : coef_ac * D.w_critic;
-      const float a = tok[T_CEU], b = tok[T_CEC];
+      const float a = t_ceu, b = t_cec;
       du = a < b ? w : (a > b ? 0.f : 0.5f * w);
       dc = b < a ? w : (b > a ? 0.f : 0.5f * w);
     }
-    const float lse = tok[T_LSE];   // the forward's softmax statistics of this token's value logits
+    const float lse = t_lse;   // the forward's softmax statistics of this token's value logits
     const float inv = 1.0f / (1.41421356237309505f * D.sigma);
-    const float yu = fminf(fmaxf(D.returns[tk], D.lo), D.hi);
-    const float yc = fminf(fmaxf(fminf(fmaxf(D.returns[tk], -D.value_clip), D.value_clip), D.lo), D.hi);
-    const HlTargets tu = hl_targets(D.support, D.B, yu, inv, lane);
-    const HlTargets tc = hl_targets(D.support, D.B, yc, inv, lane);
+    const float yu = fminf(fmaxf(ret, D.lo), D.hi);
+    const float yc = fminf(fmaxf(fminf(fmaxf(ret, -D.value_clip), D.value_clip), D.lo), D.hi);
+    // hl_targets on the edges in registers
+    auto targets = [&](float y) -> HlTargets {
+      const float f0 = lane <= B ? erff((e0 - y) * inv) : 0.f;
+      const float f1 = lane + 64 <= B ? erff((e1 - y) * inv) : 0.f;
+      const int nb = (lane + 1) & 63;
+      const float n0s = __shfl(f0, nb, 64), n1 = __shfl(f1, nb, 64), f64 = __shfl(f1, 0, 64);
+      const float n0 = lane == 63 ? f64 : n0s;
+      const float cB = B < 64 ? __shfl(f0, B, 64) : __shfl(f1, B - 64, 64);
+      const float z = cB - __shfl(f0, 0, 64);
+      return {k0 ? (n0 - f0) / z : 0.f, k1 ? (n1 - f1) / z : 0.f};
+    };
+    const HlTargets tu = targets(yu);
+    const HlTargets tc = targets(yc);
     // sum_k t_k (= 1 up to rounding) for the exact softmax * sum(t) - t gradient
     float su = 0.f, sc = 0.f;
-    if (lane < D.B) {
+    if (k0) {
       su += tu.t0;
       sc += tc.t0;
     }
-    if (lane + 64 < D.B) {
+    if (k1) {
       su += tu.t1;
       sc += tc.t1;
     }
     su = wave_sum(su);
     sc = wave_sum(sc);
-    if (lane < D.B) {
-      const float p = expf(x[lane] - lse);
-      D.d_values[(int64_t)tk * D.B + lane] = du * (p * su - tu.t0) + dc * (p * sc - tc.t0);
+    if (k0) {
+      const float p = expf(x0 - lse);
+      D.d_values[(int64_t)tk * B + lane] = du * (p * su - tu.t0) + dc * (p * sc - tc.t0);
     }
-    if (lane + 64 < D.B) {
-      const float p = expf(x[lane + 64] - lse);
-      D.d_values[(int64_t)tk * D.B + lane + 64] = du * (p * su - tu.t1) + dc * (p * sc - tc.t1);
+    if (k1) {
+      const float p = expf(x1 - lse);
+      D.d_values[(int64_t)tk * B + lane + 64] = du * (p * su - tu.t1) + dc * (p * sc - tc.t1);
     }
   }
 
   // ---- world model: d/dpred_raw (interleaved mean / log-var)
   {
-    const float coef = (mask && ti < D.n - 1) ? g * D.w_autoreg / st[XTRL_LS_NWM] : 0.f;
-    const float* pr = D.pred_raw + (int64_t)tk * 2 * D.S1;
+    const float coef = (mask && ti < D.n - 1) ? g * D.w_autoreg / s_nwm : 0.f;
     for (int c = lane; c < D.S1; c += 64) {
       float dm = 0.f, dlv = 0.f;
       if (coef != 0.f) {
-        const float mean = pr[2 * c], lv = pr[2 * c + 1];
+        const float mean = c == lane ? pm : pr[2 * c], lv = c == lane ? plv : pr[2 * c + 1];
         const float th = tanhf(lv / 3.f);
         const float var = expf(th * 3.f);
         const float vv = fmaxf(var, 1e-6f);
-        const float y = D.real[((int64_t)tk + 1) * D.S1 + c];
+        const float y = c == lane ? yr : D.real[((int64_t)tk + 1) * D.S1 + c];
         const float df = mean - y;
         dm = coef * df / vv;
         const float dvar = coef * 0.5f * (1.f / vv - df * df / (vv * vv));
@@ -445,12 +533,23 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
     }
   }
 
+  // the action logits to every lane (lane 0 evaluates the discrete terms)
+  float rawa[32];
+  int act = 0;
+  float olp = 0.f;
+  if (!D.continuous) {
+    const float rawv = lane < D.A ? D.raw_actions[(int64_t)tk * D.A + lane] : 0.f;
+    act = D.actions[tk];
+    olp = D.old_logp[tk];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) rawa[i] = __shfl(rawv, i, 64);
+  }
   if (lane != 0) return;
   // ---- done: BCE(sigmoid(z), y)
   {
     const float coef = mask ? g * D.w_autoreg / n_mask : 0.f;
-    const float p = sigmoidf_(D.done_logit[tk]);
-    const float y = D.dones[tk] ? 1.f : 0.f;
+    const float p = sigmoidf_(zlog);
+    const float y = dn ? 1.f : 0.f;
     const float dp = coef * (p - y) / fmaxf((1.f - p) * p, 1e-12f);
     D.d_done_logit[tk] = dp * (1.f - p) * p;
   }
@@ -464,9 +563,9 @@ __global__ __launch_bounds__(256) void k_loss_bwd(const XtrlLossDesc D, float g)
       return;
     }
     DiscreteTerms T;
-    const int a = D.actions[tk];
-    discrete_terms(D.raw_actions + (int64_t)tk * A, A, a, T);
-    const float r = expf(T.lp - D.old_logp[tk]);
+    const int a = act;
+    discrete_terms(rawa, A, a, T);
+    const float r = expf(T.lp - olp);
     const float dlp = -dmin_dr(r, advn, lo, hi) * r * ca;   // d tok / d logp
     const float dent = -D.entropy_weight * ca;               // d tok / d entropy
     float gq[32];
