@@ -719,6 +719,9 @@ __global__ void k_rollout_begin(const XtrlDecodeDesc D) {
   D.alive[e] = 1;
   D.lens[e] = 0;
   D.cum_reward[e] = 0.0;
+  // the fused feed-forward's panel arrival counters (every launch leaves them zero; reset here so an
+  // interrupted rollout cannot leave one behind)
+  if (D.mlp_cnt && e < (D.E + 15) / 16) D.mlp_cnt[e] = 0u;
 }
 
 __global__ void k_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const int32_t* ep_of_slot) {
