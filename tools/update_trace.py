@@ -14,10 +14,10 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
 
 
-def run():
+def run(name='c3'):
     import torch
     import bench
-    cfg = bench.CONFIGS['c3']
+    cfg = bench.CONFIGS[name]
     learner, env = bench.build_learner(cfg, 0)
     bench.one_update(learner, env, cfg['T'])
     torch.cuda.synchronize()
@@ -116,6 +116,6 @@ def show(path):
 
 if __name__ == '__main__':
     if sys.argv[1] == 'run':
-        run()
+        run(sys.argv[2] if len(sys.argv) > 2 else 'c3')
     else:
         show(sys.argv[2])

@@ -422,14 +422,38 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld
     if (a < A) out[(int64_t)a * d + c] = acc[a];
 }
 
-// latent gradient of the evolutionary conditioning: dlat[e][c] = sum_steps dac[e*n + s][2d + c]
-__global__ void k_latent_grad(const float* dac, int ld, int off, int b, int n, int d, float* dlat) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= b * d) return;
-  const int e = i / d, c = i - e * d;
+// latent gradient of the evolutionary conditioning: dlat[e][c] = sum_steps dac[e*n + s][2d + c].
+// Block (episode e, 64 columns): LG_G groups of 64 threads each sum a contiguous range of steps
+// in order (8 loads in flight per thread), then the group partials are added in group order (a
+// thread per column summing all n steps in turn took 107 us a launch at C2's n = 500)
+constexpr int LG_G = 16;
+__global__ __launch_bounds__(64 * LG_G) void k_latent_grad(const float* dac, int ld, int off, int b, int n, int d,
+                                                           float* dlat) {
+  __shared__ float red[LG_G][64];
+  const int e = blockIdx.x, cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int per = (n + LG_G - 1) / LG_G, t0 = grp * per, t1 = min(n, t0 + per);
   float s = 0.f;
-  for (int t = 0; t < n; ++t) s += dac[((int64_t)e * n + t) * ld + off + c];
-  dlat[i] = s;
+  if (c < d) {
+    const float* col = dac + (int64_t)e * n * ld + off + c;
+    int t = t0;
+    for (; t + 8 <= t1; t += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = col[(int64_t)(t + u) * ld];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; t < t1; ++t) s += col[(int64_t)t * ld];
+  }
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < d) {
+    float tot = 0.f;
+#pragma unroll
+    for (int g2 = 0; g2 < LG_G; ++g2) tot += red[g2][cl];
+    dlat[(int64_t)e * d + c] = tot;
+  }
 }
 
 // dW[c][g] += sum_e dlat[e][c] latent[e][g];  db[c] += sum_e dlat[e][c]
@@ -437,14 +461,22 @@ __global__ void k_latent_wgrad(const float* dlat, const float* latent, int b, in
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d * (G + 1)) return;
   const int c = i / (G + 1), g = i - c * (G + 1);
+  // (episodes 8 at a time, their loads issued together; the sum in episode order)
   float s = 0.f;
-  if (g < G) {
-    for (int e = 0; e < b; ++e) s += dlat[(int64_t)e * d + c] * latent[(int64_t)e * G + g];
-    dw[(int64_t)c * G + g] += s;
-  } else {
-    for (int e = 0; e < b; ++e) s += dlat[(int64_t)e * d + c];
-    db[c] += s;
+  for (int e0 = 0; e0 < b; e0 += 8) {
+    float x[8], y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = min(e0 + u, b - 1);
+      x[u] = dlat[(int64_t)e * d + c];
+      y[u] = g < G ? latent[(int64_t)e * G + g] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (e0 + u < b) s += g < G ? x[u] * y[u] : x[u];
   }
+  if (g < G) dw[(int64_t)c * G + g] += s;
+  else db[c] += s;
 }
 
 __global__ void k_copy_col(const float* src, int ld, float* dst, int lddst, int rows) {
@@ -770,8 +802,8 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   if ((rc = wgrad(cw, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
   if (D->evolutionary) {
     XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
-    hipLaunchKernelGGL(k_latent_grad, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->dac, D->in_dim, 2 * d, D->b,
-                       D->n, d, D->part);
+    hipLaunchKernelGGL(k_latent_grad, dim3(D->b, (d + 63) / 64), dim3(64 * LG_G), 0, s, D->dac, D->in_dim, 2 * d,
+                       D->b, D->n, d, D->part);
     hipLaunchKernelGGL(k_latent_wgrad, dim3(blocks(d * (D->G + 1), 256)), dim3(256), 0, s, D->part, D->latent, D->b,
                        d, D->G, c.G(D->w_lat), c.G(D->b_lat));
     XTRL_LAUNCHED("train latent grad");
