@@ -162,12 +162,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 template <int DH>
-__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(const AttnArgs a) {
+__global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const AttnArgs a) {
   constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
   __shared__ float Qs[TQ][KST], dOs[TQ][KST];
   __shared__ float Ls[TQ], Dls[TQ];
   // one per-wave tile image, used for P~ (dV) and then for dS (dK): 26.6 KB of LDS per workgroup,
-  // six resident per CU, so the C3 grid is one round
+  // six resident per CU; at dh = 16 the register budget is held to 128 (4 waves per SIMD: 168 gave
+  // 3, and a quarter of the C3 grid ran as a second round), so the C3 grid is one round
   __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
