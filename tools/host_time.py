@@ -11,7 +11,7 @@ sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
 import torch  # noqa: E402
 import bench  # noqa: E402
 
-cfg = bench.CONFIGS['c3']
+cfg = bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else 'c3']
 learner, env = bench.build_learner(cfg, 0)
 for _ in range(2):
     bench.one_update(learner, env, cfg['T'])
