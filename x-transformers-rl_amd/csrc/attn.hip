@@ -48,15 +48,11 @@ struct AttnArgs {
 };
 
 // ---------------------------------------------------------------------------------------------
-// (fragment reads are float4: lane group lg takes the k range [lg KS, lg KS + KS) of Q K^T and the
-// keys [16 lg, 16 lg + 16) of P V — each MFMA's k slice is one value per lane group — so one
-// ds_read_b128 feeds four MFMAs; V is staged transposed for that)
 template <int DH>
 __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
-  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 4, PSF = TK + 4;
-  __shared__ __attribute__((aligned(16))) float Ks[TK][KST];
-  __shared__ __attribute__((aligned(16))) float Vt[DH][PSF];
-  __shared__ __attribute__((aligned(16))) float Ps[4][16][PSF];
+  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
+  __shared__ float Ks[TK][KST], Vs[TK][KST];
+  __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
   const int bh = blockIdx.y, b = bh / a.H, n = a.n;
   const int q0 = blockIdx.x * TQ;
@@ -71,7 +67,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
   {
     const int i = q0 + 16 * w + lr;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) qa[s] = (i < n) ? a.Q[ib + (int64_t)i * isi + lg * KS + s] : 0.f;
+    for (int s = 0; s < KS; ++s) qa[s] = (i < n) ? a.Q[ib + (int64_t)i * isi + 4 * s + lg] : 0.f;
   }
   float m[4], l[4];
   f32x4v o[ND];
@@ -89,7 +85,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     for (int x = tid; x < TK * DH; x += 256) {
       const int j = x / DH, c = x - j * DH, jj = kt * TK + j;
       Ks[j][c] = jj < n ? a.K[ib + (int64_t)jj * isi + c] : 0.f;
-      Vt[c][j] = jj < n ? a.V[ib + (int64_t)jj * isi + c] : 0.f;
+      Vs[j][c] = jj < n ? a.V[ib + (int64_t)jj * isi + c] : 0.f;
     }
     __syncthreads();
     f32x4v sacc[4];
@@ -97,11 +93,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     for (int sub = 0; sub < 4; ++sub) {
       sacc[sub] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s4 = 0; s4 < KS / 4; ++s4) {
-        const f32x4v kf = *reinterpret_cast<const f32x4v*>(&Ks[16 * sub + lr][lg * KS + 4 * s4]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sacc[sub] = mfma16(qa[4 * s4 + u], kf[u], sacc[sub]);
-      }
+      for (int s = 0; s < KS; ++s) sacc[sub] = mfma16(qa[s], Ks[16 * sub + lr][4 * s + lg], sacc[sub]);
     }
     // keep words: this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block per key column
     // (word = row & 3), so one block per column instead of one per element
@@ -146,15 +138,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     }
     wave_sync();
 #pragma unroll
-    for (int s4 = 0; s4 < TK / 16; ++s4) {
-      const f32x4v pf = *reinterpret_cast<const f32x4v*>(&Ps[w][lr][16 * lg + 4 * s4]);
+    for (int d = 0; d < ND; ++d)
 #pragma unroll
-      for (int d = 0; d < ND; ++d) {
-        const f32x4v vf = *reinterpret_cast<const f32x4v*>(&Vt[16 * d + lr][16 * lg + 4 * s4]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[d] = mfma16(pf[u], vf[u], o[d]);
-      }
-    }
+      for (int s = 0; s < TK / 4; ++s) o[d] = mfma16(Ps[w][lr][4 * s + lg], Vs[4 * s + lg][16 * d + lr], o[d]);
     wave_sync();
   }
 #pragma unroll
