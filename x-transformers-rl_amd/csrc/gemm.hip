@@ -189,14 +189,16 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
 
 // scalar epilogue: acc[r] -> row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col lane & 31 of the wave's 32 x 32
 // tile (i, j); bias / activation / saved derivative / gate / residual / beta, then the stores
-template <int TM, int TN, int EPI, bool RES>
+// V4ONLY: the launch guarantees the row-vector form (epi_v4_host): the scalar form is not compiled
+// in (for the split-bf16 GELU + dropout kernels it cost 46 spilled registers)
+template <int TM, int TN, int EPI, bool RES, bool V4ONLY = false>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
                                               int wn, int lane, int bz) {
   const int M = a.M, N = a.N;
   float* C = a.C;
   if (a.t_dev) C += (int64_t)(*a.t_dev) * a.c_t_stride;
   if (a.kspan > 0) C += bz * a.c_split;
-  if (epi_v4_ok<EPI, RES>(a, C)) {
+  if (V4ONLY || epi_v4_ok<EPI, RES>(a, C)) {
     gemm_epilogue_v4<TM, TN, EPI, RES>(a, acc, C, m0, n0, wm, wn, lane);
     return;
   }
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
     }
   }
 
-  gemm_epilogue<TM, TN, EPI, RES>(a, acc, m0, n0, wm, wn, lane, bz);
+  gemm_epilogue<TM, TN, EPI, RES, X6 && EPI == EPI_GELU_DROP>(a, acc, m0, n0, wm, wn, lane, bz);
 }
 
 #ifdef XTRL_WS_DIAG   // tools/ws_lab.hip: per-step s_memtime stamps of waves 0 and 4 of every workgroup
@@ -993,7 +995,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
     __syncthreads();
   }
   WS_STAMP(nsteps, 0);
-  gemm_epilogue<TM, TN, EPI, RES>(a, acc, m0, n0, wm, wn, lane, bz);
+  gemm_epilogue<TM, TN, EPI, RES, EPI == EPI_GELU_DROP>(a, acc, m0, n0, wm, wn, lane, bz);
 }
 
 __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, const float* gamma, float* Y, int ldy,
@@ -1217,6 +1219,13 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// host restatement of epi_v4_ok for the GELU + dropout epilogue (C and aux_out; no split-K / t_dev
+// offset on this epilogue's launches): the split-bf16 kernels compile only the row-vector form of it
+bool gelu_drop_v4_host(const GemmArgs& a) {
+  return (a.N & 3) == 0 && (a.ldc & 3) == 0 && aligned16(a.C) && (a.ld_aux_out & 3) == 0 && aligned16(a.aux_out) &&
+         !a.t_dev && a.kspan == 0;
+}
 int round4(int x) { return (x + 3) & ~3; }
 
 }  // namespace
@@ -1239,9 +1248,12 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   const bool vec = aligned16(a.A) && aligned16(a.B) && (a.lda % 4 == 0) && (a.ldb % 4 == 0) &&
                    a.lda >= round4(trans_a ? a.M : a.K) && a.ldb >= round4(trans_b ? a.N : a.K);
   const bool ln = a.gamma != nullptr, res = a.R != nullptr;
+  // (the split-bf16 GELU + dropout kernels have only the row-vector epilogue: other layouts take the
+  // scalar-load kernel)
+  const bool vec_k = vec && (epi != EPI_GELU_DROP || gelu_drop_v4_host(a));
 #define XG(TA_, TB_, E_, L_, R_)                                                                   \
   if (trans_a == TA_ && trans_b == TB_ && epi == E_ && ln == L_ && res == R_) {                    \
-    dispatch_geom<TA_, TB_, E_, L_, R_>(a, vec, s);                                                \
+    dispatch_geom<TA_, TB_, E_, L_, R_>(a, vec_k, s);                                              \
     XTRL_LAUNCHED("gemm_f32");                                                                     \
     return XTRL_OK;                                                                                \
   }
