@@ -1107,12 +1107,14 @@ void launch(const GemmArgs& a, hipStream_t s) {
                      a);
 }
 
-// XTRL_GEMM_X6_SMALL=1: split-bf16 products on the 64 x 64 geometry too (off: the decode-sized
-// GEMMs are latency bound, C3 rollout 38.7 vs 38.1 ms with it on)
+// split-bf16 products on the 64 x 64 geometry too (XTRL_GEMM_X6_SMALL=0: f32 products there).  On
+// since the rollout's projections moved to the decode GEMM (dgemm.hip): the learn step's mid-sized
+// GEMMs gain (C3 learn -0.2 ... -0.5 ms in 5 of 5 A/B rounds); round 1 had it off for the decode
+// shapes (rollout 38.7 vs 38.1 ms)
 bool use_x6_small() {
   static const bool on = [] {
     const char* e = getenv("XTRL_GEMM_X6_SMALL");
-    return e && atoi(e) != 0;
+    return !(e && atoi(e) == 0);
   }();
   return on;
 }
