@@ -47,9 +47,12 @@ def show(path):
     t1 = int(rows[upd[-1]]['End_Timestamp'])
     print(f'update: {len(upd)} kernels, wall {(t1 - t0) / 1e6:.2f} ms, busy {sum(dur[i] for i in upd) / 1e3:.2f} ms')
     gathers = [i for i in upd if 'k_gather' in names[i]]
-    if gathers:
-        roll = [i for i in upd if i < gathers[0]]
-        learn = [i for i in upd if i >= gathers[0]]
+    # (the reference-mode learn step of the fractal body has no device gather: the learn phase then
+    # starts at the GAE launch)
+    first = gathers[:1] or [i for i in upd if 'k_hlgauss_gae' in names[i]][:1]
+    if first:
+        roll = [i for i in upd if i < first[0]]
+        learn = [i for i in upd if i >= first[0]]
         for label, seg in (('rollout', roll), ('learn', learn)):
             ts = int(rows[seg[0]]['Start_Timestamp']); te = int(rows[seg[-1]]['End_Timestamp'])
             print(f'{label}: {len(seg)} kernels, wall {(te - ts) / 1e6:.2f} ms, busy {sum(dur[i] for i in seg) / 1e3:.2f} ms')
