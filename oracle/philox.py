@@ -128,3 +128,46 @@ class SynthSim:
             terminated = bool((int(x) & ((1 << self.hazard_log2) - 1)) == 0)
         self.t = t + 1
         return self._state(t + 1), reward, terminated
+
+
+# --------------------------------------------------------------------------------------------
+# learn-step dropout keep masks (the streams csrc/attn.hip and the GELU + dropout GEMM epilogue
+# of csrc/gemm.hip draw; include/xtrl_hip.h "dropout streams"), so that the oracle's training
+# forward can apply the GPU's masks in place of torch.nn.Dropout (x-transformers attn_dropout /
+# FeedForward Dropout, xtrl.py:729-730) and be compared with dropout ON
+# --------------------------------------------------------------------------------------------
+
+
+def _thresh32(p):
+    return np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
+
+
+def attn_dropout_keep(b, H, n, p, seed, offset, layer):
+    """bool [b][H][n][n]: keep(e, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + e H + h,
+    FIELD_DROPOUT << 24 | layer; seed) >= p 2^32 (one Philox block per 4 query rows)."""
+    n4 = (n + 3) // 4
+    c2 = (np.uint64(offset) + np.arange(b * H, dtype=np.uint64))[:, None, None]
+    words = philox4x32(np.arange(n4)[None, :, None], np.arange(n)[None, None, :], c2,
+                       _c3(FIELD_DROPOUT, layer), seed)
+    w = np.stack(words, axis=2).reshape(b * H, 4 * n4, n)[:, :n]     # row i = 4 (i >> 2) + (i & 3)
+    return (w >= _thresh32(p)).reshape(b, H, n, n)
+
+
+def ff_dropout_keep(M, N, p, seed, offset, layer):
+    """bool [M][N] feed-forward keep mask over token-major rows m (= episode * n + step) and hidden
+    columns.  p a multiple of 1/256 (byte mode): byte (m & 3) of word ((m >> 3) & 3) of
+    philox4x32(col, 2 (m >> 5) + ((m >> 2) & 1), offset, FIELD_FF_DROPOUT << 24 | 2 layer + 1; seed)
+    >= 256 p (one block per 16 rows); otherwise word (m & 3) of philox4x32(col, m >> 2, offset,
+    FIELD_FF_DROPOUT << 24 | 2 layer; seed) >= p 2^32."""
+    m = np.arange(M)
+    cols = np.arange(N)[None, :]
+    if float(p * 256).is_integer():
+        G2 = 2 * ((M + 31) // 32)
+        words = np.stack(philox4x32(cols, np.arange(G2)[:, None], offset, _c3(FIELD_FF_DROPOUT, 2 * layer + 1),
+                                    seed))                            # [word][c1][col]
+        c1 = ((m >> 5) << 1) | ((m >> 2) & 1)
+        w = words[(m >> 3) & 3, c1]                                   # [M][N]
+        return ((w >> (8 * (m & 3))[:, None].astype(np.uint32)) & np.uint32(0xFF)) >= np.uint32(int(p * 256))
+    M4 = (M + 3) // 4
+    words = np.stack(philox4x32(cols, np.arange(M4)[:, None], offset, _c3(FIELD_FF_DROPOUT, 2 * layer), seed))
+    return words[m & 3, m >> 2] >= _thresh32(p)

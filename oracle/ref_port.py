@@ -23,8 +23,8 @@ from torch import nn
 from torch.nn.utils.rnn import pad_sequence
 
 from . import thirdparty as tp
-from .philox import (FIELD_COIN, FIELD_SAMPLE, SynthSim, epoch_permutation, evolve_seed, philox_uniform,
-                     reward_coin)
+from .philox import (FIELD_COIN, FIELD_SAMPLE, SynthSim, attn_dropout_keep, epoch_permutation, evolve_seed,
+                     ff_dropout_keep, philox_uniform, reward_coin)
 
 F32_EPS = float(torch.finfo(torch.float32).eps)
 
@@ -375,6 +375,57 @@ def minibatch_loss(model: OracleWMAC, rsnorm: RSNormState, mb: Minibatch, latent
     return loss, logs, swr, mask
 
 
+class PhiloxAttnDropout(nn.Module):
+    """x-transformers' attention-probability dropout (xtrl.py:729 attn_dropout) with the keep mask of
+    the shared counter-based stream (philox.attn_dropout_keep) in place of torch's RNG: the same
+    probabilities are dropped as in the HIP training attention, so the two can be compared with
+    dropout on.  Applies only in training mode, like nn.Dropout."""
+
+    def __init__(self, layer, p=0., seed=0, offset=0):
+        super().__init__()
+        self.layer, self.p, self.seed, self.offset = layer, p, seed, offset
+
+    def forward(self, attn):
+        if not self.training or self.p <= 0.:
+            return attn
+        b, h, n, j = attn.shape
+        assert n == j, 'training attention (no cache)'
+        keep = torch.from_numpy(attn_dropout_keep(b, h, n, self.p, self.seed, self.offset, self.layer))
+        return attn * keep.to(attn.dtype) / (1. - self.p)
+
+
+class PhiloxFFDropout(nn.Module):
+    """FeedForward's Dropout after GELU (xtrl.py:730 ff_dropout) with philox.ff_dropout_keep over the
+    minibatch's token-major rows (episode * n + step) — the GPU's GELU + dropout GEMM epilogue mask."""
+
+    def __init__(self, layer, p=0., seed=0, offset=0):
+        super().__init__()
+        self.layer, self.p, self.seed, self.offset = layer, p, seed, offset
+
+    def forward(self, h):
+        if not self.training or self.p <= 0.:
+            return h
+        b, n, f = h.shape
+        keep = torch.from_numpy(ff_dropout_keep(b * n, f, self.p, self.seed, self.offset, self.layer))
+        return h * keep.reshape(b, n, f).to(h.dtype) / (1. - self.p)
+
+
+def install_philox_dropout(model, p, seed, attn_offset, ff_offset):
+    """Point every attention / feed-forward dropout of an OracleWMAC decoder at the learn step's
+    counter-based streams for one minibatch (seed = agent seed * 1000003 + update, attention counters
+    from ``attn_offset``, FF counter ``ff_offset``; the layer index in the Philox sub-index, as
+    xtrl_amd.learner.Agent.learn draws them)."""
+    layers = model.transformer.attn_layers.layers
+    for li in range(len(layers) // 2):
+        attn, ff = layers[2 * li][1], layers[2 * li + 1][1]
+        if not isinstance(attn.attn_dropout, PhiloxAttnDropout):
+            attn.attn_dropout = PhiloxAttnDropout(li)
+            ff.ff[1] = PhiloxFFDropout(li)
+        for m, off in ((attn.attn_dropout, attn_offset), (ff.ff[1], ff_offset)):
+            m.p, m.seed, m.offset = float(p), int(seed), int(off)
+            m.train(model.training)
+
+
 # --------------------------------------------------------------------------------------------
 # LatentGenePool.evolve_  (evo.py:28-184) — same torch RNG call order as the reference
 # --------------------------------------------------------------------------------------------
@@ -513,15 +564,19 @@ class OracleLearner:
         return l2norm(self.genes[gene_ids])
 
     @torch.no_grad()
-    def rollout(self, update, max_timesteps=None, sim_seed=None):
-        """xtrl.py:1204-1356 for one learning update; env slot i = i-th (episode, gene) pair."""
+    def rollout(self, update, max_timesteps=None, sim_seed=None, slots=None):
+        """xtrl.py:1204-1356 for one learning update; env slot i = i-th (episode, gene) pair.
+        ``slots``: replay only these pairs (a sample of a wide rollout; episodes come back in that order)."""
         c = self.c
         T = max_timesteps or c.max_timesteps
         model = self.ema.ema_model
         model.eval()
         episodes = []
         fitness = torch.zeros(len(self.genes) if c.evolutionary else 1)
-        for slot, (episode, gene) in enumerate(self.episode_genes):
+        pairs = list(enumerate(self.episode_genes))
+        if slots is not None:
+            pairs = [pairs[int(s)] for s in slots]
+        for slot, (episode, gene) in pairs:
             sim = SynthSim(sim_seed if sim_seed is not None else c.seed, update, episode, c.state_dim,
                            c.num_actions, c.sim_mode, c.hazard_log2)
             state = torch.from_numpy(sim.reset()).float()

@@ -404,17 +404,18 @@ class EMA(nn.Module):
     def update(self):
         step = self.step.item()
         self.step += 1
-        if step % self.update_every != 0:
-            return
-        if step <= self.update_after_step:
+        should_update = step % self.update_every == 0
+        if should_update and step <= self.update_after_step:
             self.copy_params_from_model_to_ema()
             return
-        if not self.initted.item():
-            self.copy_params_from_model_to_ema()
-            self.initted.fill_(True)
-        decay = self.current_decay()
-        for pe, pm in zip(self.ema_model.parameters(), self.model.parameters()):
-            pe.lerp_(pm, 1. - decay)
+        if should_update:
+            if not self.initted.item():
+                self.copy_params_from_model_to_ema()
+                self.initted.fill_(True)
+            decay = self.current_decay()
+            for pe, pm in zip(self.ema_model.parameters(), self.model.parameters()):
+                pe.lerp_(pm, 1. - decay)
+        # the online-model copy-back is checked on every step, outside should_update (ema-pytorch)
         if self.update_model_with_ema_every is not None and step % self.update_model_with_ema_every == 0:
             for pe, pm in zip(self.ema_model.parameters(), self.model.parameters()):
                 pm.lerp_(pe, 1. - self.update_model_with_ema_beta)

@@ -373,10 +373,20 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
     return learner, env, oracle
 
 
-def compare_rollout(traj, lens, episodes, cont=False):
+def compare_rollout(traj, lens, episodes, cont=False, rows=None, prefix=None):
+    """Device trajectory rows vs the oracle's episodes (rows[i] <-> episodes[i]; default row i).
+    ``prefix``: the oracle ran at most ``prefix`` steps — compare the first min(len, prefix) steps."""
     lens = lens.cpu().numpy()
+    if rows is not None:
+        traj = {k: (v[torch.as_tensor(rows, device=v.device)] if v is not None else None) for k, v in traj.items()}
+        lens = lens[np.asarray(rows)]
     for i, ep in enumerate(episodes):
         n = ep['len']
+        if prefix is not None:
+            assert min(int(lens[i]), prefix) == n, (i, lens[i], n)
+            traj_i = {k: (v[i:i + 1, :n] if v is not None else None) for k, v in traj.items()}
+            compare_rollout(traj_i, torch.tensor([n]), [ep], cont)
+            continue
         assert lens[i] == n, (i, lens[i], n)
         mem = ep['mem']
         states = torch.stack([m[0] for m in mem])
@@ -880,8 +890,6 @@ def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_
     learner, env, oracle = make_learner(depth=depth, gates=fractal is None, evo=evo, T=T, episodes=episodes,
                                         batch=batch, seed=4, hazard=hazard, dim=dim, gene_dim=gene_dim,
                                         fractal_levels=fractal)
-    agent = learner.agent
-    c = oracle.c
     traj, lens, genes, cum = learner.rollout_device(env, 0, T)
     torch.cuda.synchronize()
     episodes_o, fitness = oracle.rollout(0)
@@ -889,11 +897,29 @@ def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_
     fit = learner.fitness(cum, genes)
     if evo:
         tol(fit, fitness, 1e-5, 1e-5)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches)
+    return seen, lens
+
+
+def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, dropout=0.):
+    """The first ``max_minibatches`` minibatches of Agent.learn against the oracle on the GPU's
+    current weights, RSNorm, genes and minibatch (rebuilt from the device trajectory as
+    xtrl.py:822-852 does): loss within 1e-4 relative, every gradient within 1e-4 of the gradient
+    scale.  ``dropout`` > 0: the learn step runs with attention / FF dropout and the oracle applies
+    the same keep masks (oracle.philox.attn_dropout_keep / ff_dropout_keep) in its training forward."""
+    agent = learner.agent
+    c = oracle.c
+    evo = agent.evolutionary
+    agent.cfg.dropout = dropout
+    agent.model.cfg.dropout = dropout
+    gene_list = genes.cpu().tolist()
     states, actions, old_lp, rewards, bounds, values, elens, egenes = oracle_minibatch_tensors(
-        gpu_episodes(traj, lens, [ep['gene'] for ep in episodes_o]))
+        gpu_episodes(traj, lens, gene_list))
     returns = R.calc_gae(rewards, oracle.model.hl(values), (~bounds).float(), c.gamma, c.lam)
     rs = R.RSNormState(c.state_dim + 1)
     rs.mean, rs.var = agent.rs_mean.cpu().clone(), agent.rs_var.cpu().clone()
+    N = len(gene_list)
+    n_mb_epoch = (N + agent.batch_size - 1) // agent.batch_size
     seen = []
 
     def probe(epoch, mbi, idx, loss, stats):
@@ -901,6 +927,9 @@ def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_
         oracle.model.load_state_dict({k: v.detach().cpu() for k, v in agent.model.state_dict().items()})
         oracle.model.train()
         oracle.model.zero_grad()
+        ordinal = epoch * n_mb_epoch + mbi        # Agent.learn's dropout counters for this minibatch
+        R.install_philox_dropout(oracle.model, dropout, agent.seed * 1000003 + 0,
+                                 ordinal * agent.batch_size * agent.cfg.heads, ordinal)
         mb = R.Minibatch(states[idx], actions[idx], rewards[idx], old_lp[idx], returns[idx], values[idx], bounds[idx],
                          egenes[idx], elens[idx])
         latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if evo else None
@@ -911,17 +940,20 @@ def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_
         assert abs(l_gpu - l_ref) <= 1e-4 * abs(l_ref) + 1e-6, (epoch, mbi, l_gpu, l_ref)
         gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
         scale = max(float(p.grad.abs().max()) for p in oracle.model.parameters() if p.grad is not None)
+        worst = 0.
         for name, p in oracle.model.named_parameters():
             if p.grad is not None:
                 err = float((gpu_g[name] - p.grad).abs().max())
+                worst = max(worst, err / scale)
                 assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
-        seen.append((int(elens[idx].max()), l_gpu))
+        seen.append((int(states.shape[1]), l_gpu, worst, int(idx.numel())))   # padded n = the learn step's width
         if len(seen) >= max_minibatches:
             raise _Captured()
 
     with pytest.raises(_Captured):
         agent.learn(traj, lens, genes, fit, update=0, probe=probe)
-    return seen, lens
+    print('minibatches (n, loss, worst grad err / scale, episodes):', seen)
+    return seen
 
 
 def test_c3_shape_rollout_and_learn_match_oracle():
@@ -929,6 +961,65 @@ def test_c3_shape_rollout_and_learn_match_oracle():
     sequence length (T = 128, termination hazard 1/64), 16 episodes in minibatches of 8."""
     seen, lens = _config_parity(depth=4, dim=256, T=128, hazard=6, evo=False, episodes=16, batch=8)
     assert len(seen) == 2 and int(lens.max()) > 64     # multi-tile training attention
+
+
+# ---- the bench's own geometry (bench.py CONFIGS): the kernels and grids the timed run uses ------------
+
+
+def _bench_learner(cfg):
+    """make_learner at a bench.py configuration (model, episodes per update, minibatch, T, hazard)."""
+    from bench import CONFIGS
+    c = CONFIGS[cfg]
+    return make_learner(depth=c['depth'], gates=c['gates'], evo=c['evo'], T=c['T'], episodes=c['episodes'],
+                        batch=c['batch'], seed=4, hazard=c['hazard_log2'], dim=c['dim'], gene_dim=32)
+
+
+def test_c3_full_width_rollout_matches_oracle():
+    """The C3 bench rollout at full width — 1024 episodes x 128 steps through the captured
+    hipGraph: 64 k_mlp panels meeting through the counter hand-off and the fused attention /
+    out-projection at up to 1024 live rows — against the oracle's batch-1 loop: every episode's
+    first 4 steps, and 16 whole episodes (the longest ones and a spread of slots) over the full
+    KV-cache length."""
+    learner, env, oracle = _bench_learner('c3')
+    learner.use_graph = True
+    learner._engine = None
+    traj, lens, _, _ = learner.rollout_device(env, 0, 128)
+    torch.cuda.synchronize()
+    assert len(learner.episode_genes) == 1024
+    episodes, _ = oracle.rollout(0, max_timesteps=4)
+    compare_rollout(traj, lens, episodes, prefix=4)
+    lens_c = lens.cpu()
+    longest = torch.argsort(lens_c, descending=True, stable=True)[:8].tolist()
+    spread = [int(x) for x in torch.linspace(5, 1019, 8).round().long().tolist()]
+    rows = sorted(set(longest + spread))
+    episodes, _ = oracle.rollout(0, slots=rows)
+    compare_rollout(traj, lens, episodes, rows=rows)
+    assert int(lens_c.max()) == 128 and int((lens_c == 128).sum()) > 50
+
+
+@pytest.mark.parametrize('dropout', [0., 0.25])
+def test_c3_bench_minibatch_learn_matches_oracle(dropout):
+    """The C3 learn step exactly as the bench runs it — 1024 episodes per update, minibatches of
+    128 episodes x 128 steps = 16384 tokens, depth 4, d 256, gated values + value residual, the
+    fused step (X6 large-tile / warp-specialised GEMMs, split-K weight gradients on the side
+    stream) — against the oracle on identical weights and minibatch: loss at 1e-4 relative and
+    every gradient at 1e-4 of the gradient scale, for two minibatches (the second after one
+    optimiser step).  Dropout 0.25: the oracle draws the GPU's attention / FF keep masks from the
+    host Philox stream."""
+    learner, env, oracle = _bench_learner('c3')
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 128)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2, dropout=dropout)
+    assert [s[0] for s in seen] == [128, 128] and all(s[3] == 128 for s in seen)
+
+
+def test_c2_bench_minibatch_learn_matches_oracle():
+    """C2 as the bench runs it: 256 episodes x 3 genes (EPO, 32-dim genes) at T = 500, minibatches
+    of 32 episodes x ~430 steps, depth 2, d 128, dropout 0.25 — loss and every gradient against
+    the oracle with the GPU's dropout masks, two minibatches."""
+    learner, env, oracle = _bench_learner('c2')
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 500)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2, dropout=0.25)
+    assert len(seen) == 2 and seen[0][0] > 300 and all(s[3] == 32 for s in seen)
 
 
 def test_c5_shape_fractal_rollout_and_learn_match_oracle():
@@ -959,7 +1050,9 @@ def test_ema_schedule_and_model_copy_back_match_oracle():
     online weights: copies before ``update_after_step``, the lerp with the warm-up decay after it
     (k_ema on the flat buffer), and the online-model copy-back every ``update_model_with_ema_every``
     steps — with ema_kwargs small enough that 40 optimiser steps cover all three."""
-    ek = dict(update_after_step=6, update_every=2, update_model_with_ema_every=14)
+    # update_model_with_ema_every not a multiple of update_every: the copy-back also runs on steps
+    # where the EMA itself does not update (ema-pytorch order)
+    ek = dict(update_after_step=6, update_every=2, update_model_with_ema_every=15)
     learner, _, _ = make_learner(depth=1, gates=False, agent_extra=dict(ema_kwargs=ek))
     agent = learner.agent
     online = torch.nn.Module()
@@ -1069,11 +1162,12 @@ def _compare_host(learner, oracle, env_gpu, env_cpu, T, seeds=None):
     return traj, lens, genes, cum, episodes, fitness
 
 
-@pytest.mark.parametrize('ret,limit', [(3, None), (4, 5), (5, 5), (5, None)])
+@pytest.mark.parametrize('ret,limit', [(3, None), (4, 5), (5, 5), (5, None), (5, 9), (4, 9)])
 def test_host_env_scalar_contract_matches_oracle(ret, limit):
     """The reference's scalar env (batch 1, pairs one by one) through the device decode: states,
     actions, log-probs, rewards, is_boundary = terminated, critic logits and lengths as the
-    oracle's reference loop; truncated episodes carry the next state's value (bootstrap)."""
+    oracle's reference loop; truncated episodes carry the next state's value (bootstrap) — limit 9 =
+    max_timesteps: the truncation lands on the last allowed step and still bootstraps."""
     learner, _, oracle = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2)
     _, lens, _, _, episodes, _ = _compare_host(learner, oracle, HostLander(ret=ret, limit=limit),
                                                HostLander(ret=ret, limit=limit), 9)
@@ -1093,6 +1187,18 @@ def test_host_env_vectorised_waves_match_oracle(frac, dim):
     _, _, genes, cum, episodes, fitness = _compare_host(learner, oracle, HostLanderVec(4, limit=6),
                                                         HostLander(limit=6), 8, seeds)
     tol(learner.fitness(cum, genes), fitness, 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize('frac', [None, 2])
+def test_host_env_vectorised_truncation_at_max_timesteps(frac):
+    """TimeLimit equal to max_timesteps on a vectorised env: every episode that reaches the last
+    step is truncated there and bootstraps from the next state's value (xtrl.py:1323-1336 take
+    the bootstrap on any truncated, not terminated step)."""
+    learner, _, oracle = make_learner(depth=2, gates=frac is None, T=7, episodes=6, batch=3, fractal_levels=frac)
+    traj, lens, _, _, episodes, _ = _compare_host(learner, oracle, HostLanderVec(4, limit=7, hazard=0.05),
+                                                  HostLander(limit=7, hazard=0.05), 7)
+    assert any(ep['boot'] is not None and ep['len'] == 7 for ep in episodes)
+    assert bool(torch.isfinite(traj['boot'].cpu()[lens.cpu() == 7]).all())
 
 
 def test_host_env_learn_with_truncation_bootstrap_matches_oracle():

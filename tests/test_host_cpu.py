@@ -199,3 +199,34 @@ def test_full_checkpoint_roundtrip(tmp_path):
     c = Learner(5, 2, (-1., 1.), **kw).agent
     c.load_checkpoint()
     assert torch.equal(c.flat.flat, a.flat.flat) and c.step == 0
+
+
+def test_vector_env_info_dict_is_read_per_env():
+    """A gym-style vector 4-tuple (obs, rew, done, infos) carries ONE batch-level dict: truncation is
+    read from its per-env keys ('TimeLimit.truncated' with the '_TimeLimit.truncated' presence
+    mask), never as bool(dict) — which would truncate every sub-env whenever infos is non-empty."""
+    from xtrl_amd.learner import _vector_env_fns
+    W = 4
+
+    class VecEnv:
+        num_envs = W
+
+        def __init__(self, info):
+            self.info = info
+
+        def reset(self, seed=None):
+            return np.zeros((W, 3))
+
+        def step(self, actions):
+            return np.zeros((W, 3)), np.ones(W), np.array([False, True, False, False]), self.info
+
+    cases = [({'episode': {'r': np.zeros(W)}}, [False] * 4),
+             ({'TimeLimit.truncated': np.array([True, False, True, False]),
+               '_TimeLimit.truncated': np.array([True, True, False, False])}, [True, False, False, False]),
+             ({'TimeLimit.truncated': np.array([False, False, False, True])}, [False, False, False, True]),
+             ([{}, {'x': 1}, {}, {}], [False, True, False, False])]
+    for info, want in cases:
+        _, step = _vector_env_fns(VecEnv(info), W, None, False)
+        ns, r, term, trunc = step(np.zeros(W, dtype=np.int32), np.ones(W, dtype=bool))
+        assert trunc.tolist() == want, (info, trunc)
+        assert term.tolist() == [False, True, False, False]

@@ -700,8 +700,11 @@ __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_
   D.cum_reward[e] += (double)reward[e];
   D.lens[e] = t + 1;
   for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = next_state[(int64_t)e * D.S + i];
-  if (term || t + 1 >= t_limit) D.alive[e] = 0;
-  else if (trunc) D.alive[e] = (bootstrap && t + 1 < D.Tmax) ? 2 : 0;
+  // the bootstrap is taken on any truncated, not terminated step — the last allowed step included
+  // (an env TimeLimit equal to max_timesteps: the engine holds Tmax = max_timesteps + 1 positions)
+  if (term) D.alive[e] = 0;
+  else if (trunc && bootstrap && t + 1 < D.Tmax) D.alive[e] = 2;
+  else if (trunc || t + 1 >= t_limit) D.alive[e] = 0;
 }
 
 __global__ void k_rollout_begin(const XtrlDecodeDesc D) {

@@ -264,15 +264,17 @@ class Agent(nn.Module):
     def _ema_update(self):
         step = self.ema_step
         self.ema_step += 1
-        if step % self.ema_update_every != 0:
-            return
-        if step <= self.ema_update_after:
+        should_update = step % self.ema_update_every == 0
+        if should_update and step <= self.ema_update_after:
             self.ema_flat.copy_(self.flat.flat)
             return
-        if not self.ema_initted:
-            self.ema_flat.copy_(self.flat.flat)
-            self.ema_initted = True
-        ops.ema_lerp(self.ema_flat, self.flat.flat, 1. - self.ema_decay())
+        if should_update:
+            if not self.ema_initted:
+                self.ema_flat.copy_(self.flat.flat)
+                self.ema_initted = True
+            ops.ema_lerp(self.ema_flat, self.flat.flat, 1. - self.ema_decay())
+        # ema-pytorch checks update_model_with_ema_every on every step, independent of should_update
+        # (parity unpinned: ema-pytorch is not in the container; DESIGN.md decision log)
         if self.ema_model_every is not None and step % self.ema_model_every == 0:
             # the online model takes the EMA weights (ema-pytorch update_model_with_ema)
             ops.ema_lerp(self.flat.flat, self.ema_flat, 1. - self.ema_model_beta)
@@ -682,8 +684,15 @@ def _scalar_env_fns(env, W, seeds, continuous):
 def _vector_env_fns(env, W, seeds, continuous):
     """A vectorised env of W sub-envs: reset(seed=[...]) / step(actions [W] or [W][A])."""
     def flags(x):
-        if isinstance(x, dict):                   # a 4-tuple's info read as truncated (quirk B8)
-            return np.full(W, bool(x))
+        if isinstance(x, dict):
+            # a batch-level info dict (gym vector 4-tuple): per-env truncation keys, never bool(dict)
+            # — a non-empty infos dict would otherwise truncate every sub-env after one step
+            for key in ('TimeLimit.truncated', 'truncated'):
+                if key in x:
+                    v = np.broadcast_to(np.asarray(x[key]).astype(bool), (W,))
+                    has = x.get('_' + key)
+                    return v & np.broadcast_to(np.asarray(has).astype(bool), (W,)) if has is not None else v
+            return np.zeros(W, dtype=bool)
         if isinstance(x, (list, tuple)) and x and isinstance(x[0], dict):
             return np.array([bool(i) for i in x])
         return np.broadcast_to(np.asarray(x).astype(bool), (W,))

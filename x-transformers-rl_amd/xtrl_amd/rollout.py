@@ -326,7 +326,7 @@ class RolloutEngine:
                                                   L.ptr(fl_d[E:2 * E]), T, int(bootstrap), L.stream()),
                     'env_feedback')
             ended = live & (term | trunc | (t + 1 >= T))
-            boot_now = live & trunc & ~term & (t + 1 < T) & bool(bootstrap)
+            boot_now = live & trunc & ~term & bool(bootstrap)     # the last step (t + 1 == T) included
             boot_rows |= boot_now
             pending = boot_now
             live = live & ~ended
