@@ -33,6 +33,9 @@ int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
 int64_t xtrl_struct_size(const char* name);
 const char* xtrl_last_error(void);
+/* content hash of the sources the library was compiled from (x-transformers-rl_amd/xtrl_amd/_srchash.py);
+ * bindings compare it with the sources beside the library and refuse a stale build; host-only */
+const char* xtrl_source_hash(void);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused fp32 MFMA GEMM  (every nn.Linear on the path: x-transformers to_q/k/v/out, FeedForward,

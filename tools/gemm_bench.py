@@ -47,3 +47,11 @@ for tag, N, K, M in [('ff1', 1024, 256, 16384), ('ff2', 256, 1024, 16384), ('pro
     us = timeit(lambda: ops.wgrad(dy, x, dw, ws, beta=0.))
     ut = timeit(lambda: torch.mm(dy.t(), x, out=dw))
     print(f'wgrad {tag:6s} N={N:5d} K={K:5d} M={M}  xtrl {us:8.1f} us {2*M*N*K/us/1e6:6.1f} TF | torch {ut:8.1f} us | err {err:.1e}')
+
+print('--- ceiling reference: hipBLASLt bf16 GEMM with 6x the reduction length (the X6 MFMA work)')
+for tag, M, N, K in [('fwd ff1', 16384, 1024, 256), ('fwd ff2', 16384, 256, 1024), ('dgrad ff1', 16384, 256, 1024),
+                     ('wgrad ff1', 1024, 256, 16384), ('wgrad head1', 1024, 768, 16384)]:
+    a = torch.randn(M, 6 * K, device='cuda', dtype=torch.bfloat16)
+    b = torch.randn(6 * K, N, device='cuda', dtype=torch.bfloat16)
+    ut = timeit(lambda: torch.matmul(a, b))
+    print(f'bf16x6 {tag:12s} M={M:6d} N={N:5d} K={K:6d}: {ut:8.1f} us = {2*M*N*K/ut/1e6:6.1f} TF fp32-equivalent')

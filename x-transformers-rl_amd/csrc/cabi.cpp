@@ -31,6 +31,12 @@ int check_launch(const char* what) {
 
 extern "C" int xtrl_abi_version(void) { return XTRL_ABI_VERSION; }
 
+#ifndef XTRL_SRC_HASH
+#define XTRL_SRC_HASH "unknown"
+#endif
+// content hash of the sources this library was compiled from (xtrl_amd/_srchash.py)
+extern "C" const char* xtrl_source_hash(void) { return XTRL_SRC_HASH; }
+
 // sizeof of a descriptor struct as compiled into the library (bindings check their mirrors)
 extern "C" int64_t xtrl_struct_size(const char* name) {
   static const struct {

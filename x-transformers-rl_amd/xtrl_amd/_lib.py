@@ -148,6 +148,7 @@ SIGNATURES = {
     'xtrl_wm_post': (I32, [P, I32, I32, I32, P, P, I32, P, P]),
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
+    'xtrl_source_hash': (C.c_char_p, []),
 }
 
 STRUCTS = {'XtrlDecodeLayer': DecodeLayer, 'XtrlRngState': RngState, 'XtrlDecodeDesc': DecodeDesc,
@@ -170,6 +171,11 @@ def load():
             fn.restype, fn.argtypes = res, args
         if lib.xtrl_abi_version() != ABI_VERSION:
             raise RuntimeError(f'libxtrl_hip ABI {lib.xtrl_abi_version()} != {ABI_VERSION}')
+        from ._srchash import source_hash
+        built, here = lib.xtrl_source_hash().decode(), source_hash()
+        if built != here:   # a library compiled from other sources than the ones in this tree
+            raise RuntimeError(f'{LIB_PATH} was built from sources {built}, the tree holds {here}: rebuild it '
+                               f'with `make -C x-transformers-rl_amd` or __graft_entry__.build()')
         for cname, py in STRUCTS.items():   # a stale build against an edited header fails here
             got = lib.xtrl_struct_size(cname.encode())
             if got != C.sizeof(py):

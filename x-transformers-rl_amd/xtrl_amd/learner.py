@@ -618,10 +618,13 @@ class Learner(nn.Module):
         agent = self.agent
         if not agent.evolutionary:
             return None
-        fit = torch.zeros(agent.gene_pool.num_genes, dtype=torch.float32)
-        for c_, g in zip(cum_reward.cpu().tolist(), genes.cpu().tolist()):
-            fit[g] += np.float32(c_)
-        return dist_.sum_(fit.to(self.device)).cpu()
+        # per-gene sums on the device (one small GEMV in a fixed order; fp64 episode returns), the
+        # rank sum (xtrl.py:1362) on the device too: one device->host copy per update, for evolve_
+        G = agent.gene_pool.num_genes
+        cum = cum_reward.to(self.device, torch.float64)
+        onehot = (genes.to(self.device)[None, :] == torch.arange(G, device=self.device)[:, None]).to(torch.float64)
+        fit = (onehot @ cum).to(torch.float32)
+        return dist_.sum_(fit).cpu()
 
     def forward(self, env, num_learning_updates: int, seed=None, max_timesteps=None):
         T = max_timesteps or self.max_timesteps
