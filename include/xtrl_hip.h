@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 9
+#define XTRL_ABI_VERSION 10
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -376,6 +376,7 @@ typedef struct XtrlTrainDesc {
   const float* d_done;
   /* backward scratch */
   float* dx;                     /* [T][d] */
+  float* dx2;                    /* [T][d] second residual-gradient buffer (fused LayerNorm backward) */
   float* dxn;                    /* [T][d] */
   float* dff;                    /* [T][ff] */
   float* dproj;                  /* [T][max n_qkv] */

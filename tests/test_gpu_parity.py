@@ -928,8 +928,9 @@ def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, drop
         oracle.model.train()
         oracle.model.zero_grad()
         ordinal = epoch * n_mb_epoch + mbi        # Agent.learn's dropout counters for this minibatch
-        R.install_philox_dropout(oracle.model, dropout, agent.seed * 1000003 + 0,
-                                 ordinal * agent.batch_size * agent.cfg.heads, ordinal)
+        if dropout > 0.:     # (the decoder's dropout streams; the fractal oracle body runs dropout-free)
+            R.install_philox_dropout(oracle.model, dropout, agent.seed * 1000003 + 0,
+                                     ordinal * agent.batch_size * agent.cfg.heads, ordinal)
         mb = R.Minibatch(states[idx], actions[idx], rewards[idx], old_lp[idx], returns[idx], values[idx], bounds[idx],
                          egenes[idx], elens[idx])
         latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if evo else None

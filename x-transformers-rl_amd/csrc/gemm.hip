@@ -736,6 +736,119 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
   gemm_epilogue<TM, TN, EPI, RES, X6 && EPI == EPI_GELU_DROP>(a, acc, m0, n0, wm, wn, lane, bz);
 }
 
+// LayerNorm epilogues of the warp-specialised GEMM (EPI_RES_LN / EPI_LN_BWD; N <= BN, one column
+// tile).  The consumers park the accumulator tile (2 x 2 32 x 32 MFMA tiles per wave) in LDS rows;
+// then each of the 8 waves takes rows w, w + 8, ... with a lane per 4 consecutive columns: every
+// global operand of its rows is loaded before the first reduction, row statistics are wave sums.
+// The same arithmetic per element as k_ln_fwd / k_ln_bwd (train.hip): x-transformers LayerNorm
+// (no affine, eps 1e-5) times gamma, two-pass variance; d gamma partials per BM-row tile summed
+// over the 8 waves in wave order (deterministic).
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][2], float* tile, bool producer,
+                                            int m0, int wm, int wn, int lane, int wave, int row_tile) {
+  constexpr int LDT = BN + 4, RPW = BM / 8;
+  const int M = a.M, N = a.N;
+  if (!producer) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + 32 * i + 4 * (lane >> 5) + 8 * (r >> 2) + (r & 3);
+          tile[row * LDT + wn * 64 + 32 * j + (lane & 31)] = acc[i][j][r];
+        }
+  }
+  __syncthreads();
+  const int c = 4 * lane;
+  const bool cok = c < N;
+  // every global load unconditional at an in-bounds column (a select between a global and a zero
+  // operand compiles to flat loads through a scratch zero), the values selected afterwards
+  const int cc = cok ? c : 0;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto ld4 = [&](const float* base) { return *reinterpret_cast<const float4*>(base + cc); };
+  float4 gam = ld4(a.ln_g);
+  if (!cok) gam = z4;
+  const float inv_n = 1.0f / (float)N;
+  if constexpr (EPI == EPI_RES_LN) {
+    float4 bia = z4;
+    if (a.bias) bia = ld4(a.bias);
+    if (!cok) bia = z4;
+    float4 v[RPW], r[RPW];
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int row = wave + 8 * rr, mc = min(m0 + row, M - 1);
+      v[rr] = *reinterpret_cast<const float4*>(tile + row * LDT + cc);
+      r[rr] = ld4(a.R + (int64_t)mc * a.ldr);
+    }
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int m = m0 + wave + 8 * rr;
+      float4 x;   // (acc + bias) + residual, as the GEMM epilogue forms it
+      x.x = (v[rr].x + bia.x) + r[rr].x; x.y = (v[rr].y + bia.y) + r[rr].y;
+      x.z = (v[rr].z + bia.z) + r[rr].z; x.w = (v[rr].w + bia.w) + r[rr].w;
+      if (!cok) x = z4;
+      const float mean = wave_sum((x.x + x.y) + (x.z + x.w)) * inv_n;
+      float4 dl = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+      if (!cok) dl = z4;
+      const float rstd = 1.0f / sqrtf(wave_sum((dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w)) * inv_n + 1e-5f);
+      const float4 y = make_float4((dl.x * rstd) * gam.x, (dl.y * rstd) * gam.y, (dl.z * rstd) * gam.z,
+                                   (dl.w * rstd) * gam.w);
+      if (m < M) {
+        if (cok) {
+          *reinterpret_cast<float4*>(a.C + (int64_t)m * a.ldc + c) = x;
+          *reinterpret_cast<float4*>(a.ln_y1 + (int64_t)m * a.ln_ld1 + c) = y;
+          if (a.ln_y2) *reinterpret_cast<float4*>(a.ln_y2 + (int64_t)m * a.ln_ld2 + c) = y;
+        }
+        if (lane == 0) *reinterpret_cast<float2*>(a.ln_stats + 2 * (int64_t)m) = make_float2(mean, rstd);
+      }
+    }
+  } else {
+    float4 g[RPW], xv[RPW], dr[RPW];
+    float2 st[RPW];
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int row = wave + 8 * rr, mc = min(m0 + row, M - 1);
+      g[rr] = *reinterpret_cast<const float4*>(tile + row * LDT + cc);
+      xv[rr] = ld4(a.ln_x + (int64_t)mc * N);
+      dr[rr] = a.ln_dres ? ld4(a.ln_dres + (int64_t)mc * N) : z4;
+      st[rr] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (int64_t)mc);
+      if (!cok) g[rr] = z4;
+    }
+    float4 dg = z4;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int m = m0 + wave + 8 * rr;
+      const float mu = st[rr].x, rs = st[rr].y;
+      float4 xh = make_float4((xv[rr].x - mu) * rs, (xv[rr].y - mu) * rs, (xv[rr].z - mu) * rs, (xv[rr].w - mu) * rs);
+      if (!cok) xh = z4;
+      const float4 gm = make_float4(g[rr].x * gam.x, g[rr].y * gam.y, g[rr].z * gam.z, g[rr].w * gam.w);
+      if (m < M) {
+        dg.x += g[rr].x * xh.x; dg.y += g[rr].y * xh.y; dg.z += g[rr].z * xh.z; dg.w += g[rr].w * xh.w;
+      }
+      const float ma = wave_sum((gm.x + gm.y) + (gm.z + gm.w)) * inv_n;
+      const float mb = wave_sum((gm.x * xh.x + gm.y * xh.y) + (gm.z * xh.z + gm.w * xh.w)) * inv_n;
+      float4 o;
+      o.x = rs * (gm.x - ma - xh.x * mb) + dr[rr].x;
+      o.y = rs * (gm.y - ma - xh.y * mb) + dr[rr].y;
+      o.z = rs * (gm.z - ma - xh.z * mb) + dr[rr].z;
+      o.w = rs * (gm.w - ma - xh.w * mb) + dr[rr].w;
+      if (m < M && cok) *reinterpret_cast<float4*>(a.C + (int64_t)m * a.ldc + c) = o;
+    }
+    // d gamma partial of this row tile: the 8 waves' column sums, added in wave order
+    float* red = tile + BM * LDT;
+    if (cok) *reinterpret_cast<float4*>(red + wave * BN + c) = dg;
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += red[w * BN + t];
+      a.ln_part[(int64_t)row_tile * N + t] = sum;
+    }
+  }
+}
+
 #ifdef XTRL_WS_DIAG   // tools/ws_lab.hip: per-step s_memtime stamps of waves 0 and 4 of every workgroup
 __device__ uint64_t* g_ws_diag;
 __device__ int g_ws_mode;   // 1: consumers skip the MFMAs; 2: producers skip loads + splits; 3: skip splits
@@ -749,20 +862,34 @@ __device__ int g_ws_mode;   // 1: consumers skip the MFMAs; 2: producers skip lo
 #define WS_STAMP(step, k) do {} while (0)
 #endif
 
-// ---- X6 warp-specialised GEMM (the 128 x 128 large-tile path) ----------------------------------
+// ---- X6 warp-specialised GEMM (the large-tile path) ---------------------------------------------
 // 8 waves per workgroup, one workgroup per CU.  Waves 0-3 (one per SIMD) are consumers: each owns
 // 64 x 64 of the tile and only reads piece fragments from LDS and issues bf16 MFMAs.  Waves 4-7
 // (their SIMD partners) are producers: they keep two fp32 slabs in flight global -> registers,
 // split each staged value into its hi / mid / lo pieces and write the piece images the consumers
 // read next.  Two piece images (double buffered), one barrier per 32-deep K slab: the consumers
 // never wait on global memory, and the producers' split arithmetic issues in the gaps of their
-// partner's MFMAs.  Requires K (and the split span) to be a multiple of 32 and float4 operands.
-template <bool TA, bool TB, int EPI, bool RES>
+// partner's MFMAs.  Float4 operands; K a multiple of 32, or of 4 with KT (the last slab's k >= K
+// entries are zeroed in both operands, branch-free).
+// Tiles: BM x BN = 128 x 128 (2 x 2 consumer waves) or 64 x 256 (1 x 4: a whole d = 256 row per
+// tile, so the LayerNorm epilogues below see every column of their rows).
+// LayerNorm epilogues (EPI_RES_LN / EPI_LN_BWD, one column tile, N <= BN): the consumers park the
+// tile in LDS (the piece images are free after the last step), then all 8 waves take whole rows —
+// a lane per 4 consecutive columns, every operand of the wave's rows loaded before the first
+// reduction — and finish the residual + LayerNorm forward, or the LayerNorm backward with the
+// incoming residual gradient and the tile's d gamma partial, in the same launch (no normalised /
+// d-normalised intermediate goes through HBM, no separate LayerNorm launch).
+template <bool TA, bool TB, int EPI, bool RES, int BM = 128, int BN = 128, bool KT = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
-  constexpr int BM = 128, BN = 128, BK = 32, XRS = BK + 8, NP = 256, TM = 2, TN = 2;
+  constexpr int BK = 32, XRS = BK + 8, NP = 256, TM = 2, TN = 2, WN = BN / 64;
+  constexpr bool LNE = (EPI == EPI_RES_LN || EPI == EPI_LN_BWD);
   constexpr int A_F4 = BM * BK / 4 / NP, B_F4 = BN * BK / 4 / NP;   // float4 per producer thread per slab
   constexpr int IMG = 3 * (BM + BN) * XRS;                           // bf16 per piece image
-  static_assert(A_F4 == 4 && B_F4 == 4, "one 4 x 4 transposed group per operand per producer thread");
+  static_assert((BM == 128 && BN == 128) || (BM == 64 && BN == 256), "tile 128 x 128 or 64 x 256");
+  static_assert(!TA || A_F4 == 4, "A \"T\": one 4 x 4 transposed group per producer thread");
+  static_assert(!TB || B_F4 % 4 == 0, "B \"T\": whole 4 x 4 transposed groups per producer thread");
+  constexpr int LDT = BN + 4;                                        // LN epilogue: tile rows in LDS (floats)
+  static_assert(!LNE || (BM * LDT + 8 * BN) * 4 <= 2 * IMG * 2, "LN tile exceeds the piece images");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * IMG];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -788,7 +915,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
     Ab += TA ? (int64_t)kb * a.lda : kb;
     Bb += TB ? (int64_t)kb * a.ldb : kb;
   }
-  const int nk = K / BK;
+  const int nk = (K + BK - 1) / BK;
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
 
@@ -798,12 +925,23 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
   const bool do_rs = a.rowsum != nullptr && bx == 0;   // bias gradient (TA only, see gemm_run)
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
   // operand element loads, clamped into the operand (rows / columns past M / N feed only outputs
-  // the epilogue discards; K is whole slabs)
+  // the epilogue discards; k past K: clamped in-bounds, then zeroed with KT)
   auto ld_n = [&](const float* base, int64_t ld, int row, int row_lim, int k) -> float4 {   // [row][k]
-    return *reinterpret_cast<const float4*>(base + (int64_t)min(row, row_lim - 1) * ld + k);
+    float4 f = *reinterpret_cast<const float4*>(base + (int64_t)min(row, row_lim - 1) * ld + (KT ? min(k, K - 4) : k));
+    if constexpr (KT) {
+      const bool ok = k < K;
+      f = make_float4(ok ? f.x : 0.f, ok ? f.y : 0.f, ok ? f.z : 0.f, ok ? f.w : 0.f);
+    }
+    return f;
   };
   auto ld_t = [&](const float* base, int64_t ld, int k, int col, int col_lim) -> float4 {   // [k][col]
-    return *reinterpret_cast<const float4*>(base + (int64_t)k * ld + min(col, ((col_lim + 3) & ~3) - 4));
+    float4 f = *reinterpret_cast<const float4*>(base + (int64_t)(KT ? min(k, K - 1) : k) * ld +
+                                                min(col, ((col_lim + 3) & ~3) - 4));
+    if constexpr (KT) {
+      const bool ok = k < K;
+      f = make_float4(ok ? f.x : 0.f, ok ? f.y : 0.f, ok ? f.z : 0.f, ok ? f.w : 0.f);
+    }
+    return f;
   };
   auto load = [&](auto S, int kt) {
     const int k0 = min(kt, nk - 1) * BK;
@@ -822,9 +960,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
       if constexpr (!TB) {
         const int e = p + i * NP, r = e / (BK / 4), q = e % (BK / 4);
         rb[S][i] = ld_n(Bb, a.ldb, n0 + r, N, k0 + 4 * q);
-      } else {
-        const int kq = p % (BK / 4), q = p / (BK / 4);
-        rb[S][i] = ld_t(Bb, a.ldb, k0 + 4 * kq + i, n0 + 4 * q, N);
+      } else {   // group i / 4 covers column quads 32 (i / 4) + p / 8
+        const int kq = p % (BK / 4), q = p / (BK / 4) + 32 * (i >> 2);
+        rb[S][i] = ld_t(Bb, a.ldb, k0 + 4 * kq + (i & 3), n0 + 4 * q, N);
       }
     }
   };
@@ -870,16 +1008,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
         put(xb, BN, r, 4 * qq, rb[S][i]);
       }
     } else {
-      const float4 k0v = rb[S][0], k1v = rb[S][1], k2v = rb[S][2], k3v = rb[S][3];
-      put(xb, BN, 4 * q + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
-      put(xb, BN, 4 * q + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
-      put(xb, BN, 4 * q + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
-      put(xb, BN, 4 * q + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+#pragma unroll
+      for (int gi = 0; gi < B_F4 / 4; ++gi) {
+        const int qg = q + 32 * gi;
+        const float4 k0v = rb[S][4 * gi], k1v = rb[S][4 * gi + 1], k2v = rb[S][4 * gi + 2], k3v = rb[S][4 * gi + 3];
+        put(xb, BN, 4 * qg + 0, 4 * kq, make_float4(k0v.x, k1v.x, k2v.x, k3v.x));
+        put(xb, BN, 4 * qg + 1, 4 * kq, make_float4(k0v.y, k1v.y, k2v.y, k3v.y));
+        put(xb, BN, 4 * qg + 2, 4 * kq, make_float4(k0v.z, k1v.z, k2v.z, k3v.z));
+        put(xb, BN, 4 * qg + 3, 4 * kq, make_float4(k0v.w, k1v.w, k2v.w, k3v.w));
+      }
     }
   };
 
   // ---- consumer state ----
-  const int wm = (wave & 3) >> 1, wn = wave & 1;
+  const int wm = (wave & 3) / WN, wn = (wave & 3) % WN;
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -955,7 +1097,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
       else if (mode == 3) {   // consume the loads without splitting
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s += ra[decltype(C)::value][i].x + rb[decltype(C)::value][i].y;
+        for (int i = 0; i < 4; ++i) s += ra[decltype(C)::value][i % A_F4].x + rb[decltype(C)::value][i].y;
         if (s == 12345.f) smem[tid] = (__bf16)s;
       }
       WS_STAMP(t, 1);
@@ -981,21 +1123,27 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
         }
       }
     }
-    return;
-  }
-  __syncthreads();
-  for (int t = 0; t < nsteps; ++t) {
-    WS_STAMP(t, 0);
-#ifdef XTRL_WS_DIAG
-    if (t < nk && g_ws_mode != 1) compute(smem + (t & 1) * IMG);
-#else
-    if (t < nk) compute(smem + (t & 1) * IMG);
-#endif
-    WS_STAMP(t, 1);
+    if constexpr (!LNE) return;
+  } else {
     __syncthreads();
+    for (int t = 0; t < nsteps; ++t) {
+      WS_STAMP(t, 0);
+#ifdef XTRL_WS_DIAG
+      if (t < nk && g_ws_mode != 1) compute(smem + (t & 1) * IMG);
+#else
+      if (t < nk) compute(smem + (t & 1) * IMG);
+#endif
+      WS_STAMP(t, 1);
+      __syncthreads();
+    }
+    WS_STAMP(nsteps, 0);
+    if constexpr (!LNE) {
+      gemm_epilogue<TM, TN, EPI, RES, EPI == EPI_GELU_DROP>(a, acc, m0, n0, wm, wn, lane, bz);
+      return;
+    }
   }
-  WS_STAMP(nsteps, 0);
-  gemm_epilogue<TM, TN, EPI, RES, EPI == EPI_GELU_DROP>(a, acc, m0, n0, wm, wn, lane, bz);
+  if constexpr (LNE) ln_epilogue<BM, BN, EPI>(a, acc, reinterpret_cast<float*>(smem), producer, m0, wm, wn, lane, wave,
+                                              by);
 }
 
 __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, const float* gamma, float* Y, int ldy,
@@ -1139,13 +1287,41 @@ bool ws_ok(const GemmArgs& a, bool ta, bool ln) {
   return wgs <= 256 && (a.kspan > 0 ? a.kspan : a.K) >= 512;
 }
 
-template <bool TA, bool TB, int EPI, bool RES>
+template <bool TA, bool TB, int EPI, bool RES, int BM = 128, int BN = 128, bool KT = false>
 void launch_ws(const GemmArgs& a, hipStream_t s) {
   const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
-  dim3 grid((a.N + 127) / 128, (a.M + 127) / 128, splits);
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
   GemmArgs r = a;
   r.xcd_remap = (xcd_env() && (int64_t)grid.x * grid.y * grid.z % 8 == 0) ? 1 : 0;
-  hipLaunchKernelGGL((k_gemm_ws<TA, TB, EPI, RES>), grid, dim3(512), 0, s, r);
+  hipLaunchKernelGGL((k_gemm_ws<TA, TB, EPI, RES, BM, BN, KT>), grid, dim3(512), 0, s, r);
+}
+
+// the LayerNorm-epilogue GEMMs: one column tile per row (N <= 256), 128-row tiles up to N = 128,
+// 64 x 256 above; K a multiple of 4 (KT masks a partial last slab)
+int ln_gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, bool vec, hipStream_t s) {
+  const bool res = a.R != nullptr;
+  XTRL_REQUIRE(!trans_a && vec && a.kspan == 0 && a.N <= 256 && a.N % 4 == 0 && a.K % 4 == 0 && a.ln_g &&
+                   a.ln_stats && a.ldc % 4 == 0 && ((uintptr_t)a.C & 15u) == 0 && ((uintptr_t)a.ln_g & 15u) == 0,
+               "gemm: LayerNorm epilogue needs one row tile (N=%d <= 256), float4 operands, K %% 4 == 0", a.N);
+  const bool kt = a.K % 32 != 0, narrow = a.N <= 128;
+  if (epi == EPI_RES_LN) {
+    XTRL_REQUIRE(!trans_b && res && a.ln_y1 && a.ldr % 4 == 0 && a.ln_ld1 % 4 == 0 && (!a.ln_y2 || a.ln_ld2 % 4 == 0) &&
+                     (!a.bias || ((uintptr_t)a.bias & 15u) == 0),
+                 "gemm: residual + LayerNorm epilogue arguments");
+    if (narrow) {
+      if (kt) launch_ws<false, false, EPI_RES_LN, true, 128, 128, true>(a, s);
+      else launch_ws<false, false, EPI_RES_LN, true, 128, 128, false>(a, s);
+    } else {
+      if (kt) launch_ws<false, false, EPI_RES_LN, true, 64, 256, true>(a, s);
+      else launch_ws<false, false, EPI_RES_LN, true, 64, 256, false>(a, s);
+    }
+  } else {
+    XTRL_REQUIRE(trans_b && !res && a.ln_x && a.ln_part, "gemm: LayerNorm-backward epilogue arguments");
+    if (narrow) launch_ws<false, true, EPI_LN_BWD, false, 128, 128, true>(a, s);
+    else launch_ws<false, true, EPI_LN_BWD, false, 64, 256, true>(a, s);
+  }
+  XTRL_LAUNCHED("gemm_ln");
+  return XTRL_OK;
 }
 
 bool use_x6() {   // XTRL_GEMM_F32=1: native f32 MFMA products everywhere
@@ -1232,6 +1408,8 @@ int round4(int x) { return (x + 3) & ~3; }
 
 }  // namespace
 
+int gemm_ln_rows(int N) { return N <= 128 ? 128 : 64; }
+
 int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s) {
   XTRL_REQUIRE(a.A && a.B && a.C, "gemm: null operand");
   XTRL_REQUIRE(a.M >= 0 && a.N >= 0 && a.K > 0, "gemm: bad shape M=%d N=%d K=%d", a.M, a.N, a.K);
@@ -1252,6 +1430,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   const bool ln = a.gamma != nullptr, res = a.R != nullptr;
   // (the split-bf16 GELU + dropout kernels have only the row-vector epilogue: other layouts take the
   // scalar-load kernel)
+  if (epi == EPI_RES_LN || epi == EPI_LN_BWD) return ln_gemm_run(a, trans_a, trans_b, epi, vec, s);
   const bool vec_k = vec && (epi != EPI_GELU_DROP || gelu_drop_v4_host(a));
 #define XG(TA_, TB_, E_, L_, R_)                                                                   \
   if (trans_a == TA_ && trans_b == TB_ && epi == E_ && ln == L_ && res == R_) {                    \

@@ -22,6 +22,11 @@ enum GemmEpi : int {
   EPI_MUL_AUX = 5,     // C = v * aux_in                                 (dgrad through a saved derivative)
   EPI_RELU = 8,        // max(v, 0)   (fractal encoder final aggregation, fractal_rl.py:235-239)
   EPI_DGATE = 7,       // s = sigmoid(aux_in2): C = v * s; aux_out = v * aux_in * (1 - s) * s   (value gate)
+  // full-row LayerNorm epilogues (warp-specialised kernel, one column tile holds every column of a row:
+  // N <= 256; x-transformers LayerNorm = layer_norm without affine, eps 1e-5, times gamma)
+  EPI_RES_LN = 9,      // C = v (+ bias) + R;  ln_y1 / ln_y2 = LN(C) * ln_g;  ln_stats[m] = (mean, rstd)
+  EPI_LN_BWD = 10,     // g = v; xhat = (ln_x - mean) rstd; C = rstd (g ln_g - mean_n(g ln_g) - xhat
+                       //   mean_n(g ln_g xhat)) + ln_dres;  ln_part[row tile][n] = sum_tile rows g xhat
 };
 
 struct GemmArgs {
@@ -53,7 +58,17 @@ struct GemmArgs {
   int rowsum_m0 = 0;              //   the bias gradient when A = dY^T; with split-K the per-split
   float* rowsum_ws = nullptr;     //   sums go to rowsum_ws[z][M] and the reduce kernel adds them
   int xcd_remap = 0;              // 1: workgroup ids permuted so each XCD runs consecutive tiles
+  // LayerNorm epilogues (EPI_RES_LN / EPI_LN_BWD)
+  const float* ln_g = nullptr;    // gamma [N]
+  float* ln_y1 = nullptr; int ln_ld1 = 0;   // RES_LN: normalised rows (ln_y2 optional: a second copy)
+  float* ln_y2 = nullptr; int ln_ld2 = 0;
+  float* ln_stats = nullptr;      // [M][2] (mean, rstd): written by RES_LN, read by LN_BWD
+  const float* ln_x = nullptr;    // LN_BWD: the LayerNorm input [M][N] (row stride N)
+  const float* ln_dres = nullptr; // LN_BWD: gradient added to the output (may alias C: same element, same thread)
+  float* ln_part = nullptr;       // LN_BWD: d gamma partials [ceil(M / BM)][N]
 };
+// rows per workgroup of the LayerNorm-epilogue GEMM for an N-column row (the column tile is the row)
+int gemm_ln_rows(int N);
 
 // launch C = op(A, B) for the combination (trans_a, trans_b, epi, LN = gamma != 0, RES = R != 0)
 int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s);

@@ -669,6 +669,44 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
   return XTRL_OK;
 }
 
+// LayerNorm folded into the GEMM that produces / consumes its rows (gemm.hip EPI_RES_LN /
+// EPI_LN_BWD): possible when one column tile holds the whole row and every operand is float4
+bool ln_fusable(const XtrlTrainDesc* D) {
+  static const bool on = [] {   // XTRL_FUSED_LN=0: separate LayerNorm launches (A/B experiments)
+    const char* e = getenv("XTRL_FUSED_LN");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on || D->d % 4 || D->d > 256 || (D->H * D->dh) % 4 || D->ff % 4 || D->in_dim % 4) return false;
+  for (int li = 0; li < D->L; ++li)
+    if (D->layers[li].n_qkv % 4) return false;
+  return true;
+}
+
+// x_out = A W^T (+ bias) + R, then y1 (= y2) = LN(x_out) gamma and the row statistics, one launch
+int linear_res_ln(const Ctx& c, const float* A, int lda, const float* W, const float* bias, const float* R,
+                  float* x_out, int K, const float* gamma, float* y1, int ld1, float* y2, int ld2, float* st) {
+  const int d = c.D->d;
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = x_out; g.ldc = d; g.M = c.T; g.N = d; g.K = K;
+  g.R = R; g.ldr = d; g.ln_g = gamma; g.ln_y1 = y1; g.ln_ld1 = ld1; g.ln_y2 = y2; g.ln_ld2 = ld2; g.ln_stats = st;
+  return gemm_run(g, 0, 0, EPI_RES_LN, c.s);
+}
+
+// dx = LN_backward(dY W; x, stats, gamma) + dres in one launch; d gamma accumulated from the
+// per-row-tile partials
+int dgrad_ln_bwd(const Ctx& c, const float* dY, int ldy, const float* W, int N, const float* x, const float* st,
+                 const float* gamma, const float* dres, float* dx, float* dgamma) {
+  const int d = c.D->d, nb = (c.T + gemm_ln_rows(d) - 1) / gemm_ln_rows(d);
+  XTRL_REQUIRE((int64_t)nb * d <= c.D->part_floats, "train: partial-sum workspace too small");
+  GemmArgs g;
+  g.A = dY; g.lda = ldy; g.B = W; g.ldb = d; g.C = dx; g.ldc = d; g.M = c.T; g.N = d; g.K = N;
+  g.ln_g = gamma; g.ln_x = x; g.ln_stats = const_cast<float*>(st); g.ln_dres = dres; g.ln_part = c.D->part;
+  if (int rc = gemm_run(g, 0, 1, EPI_LN_BWD, c.s)) return rc;
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
+  XTRL_LAUNCHED("train dgrad_ln_bwd");
+  return XTRL_OK;
+}
+
 AttnProblem attn_problem(const Ctx& c, const XtrlTrainLayer& Ly, int li) {
   const XtrlTrainDesc* D = c.D;
   const int I = D->H * D->dh;
@@ -724,10 +762,13 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   if (D->S == 8) hipLaunchKernelGGL(k_embed<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
   else hipLaunchKernelGGL(k_embed<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
   XTRL_LAUNCHED("train embed");
-  // decoder blocks
+  // decoder blocks; fused: every LayerNorm but layer 0's attention pre-norm is formed in the epilogue
+  // of the GEMM that completes its rows (out-projection + residual, FF2 + residual)
+  const bool fuse = ln_fusable(D);
   for (int li = 0; li < D->L; ++li) {
     const XtrlTrainLayer& Ly = D->layers[li];
-    if ((rc = ln_fwd(c, Ly.x_attn, c.P(Ly.ln_attn), Ly.xn_attn, d, nullptr, 0, Ly.st_attn))) return rc;
+    if (li == 0 || !fuse)
+      if ((rc = ln_fwd(c, Ly.x_attn, c.P(Ly.ln_attn), Ly.xn_attn, d, nullptr, 0, Ly.st_attn))) return rc;
     if ((rc = linear_fwd(c, Ly.xn_attn, d, c.P(Ly.w_proj), c.P(Ly.b_proj), Ly.proj, Ly.n_qkv, T, Ly.n_qkv, d,
                          EPI_NONE, nullptr, nullptr, 0, 1 << 30, 3 * I)))
       return rc;
@@ -740,18 +781,36 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = attn_fwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse,
                           D->gate_values ? Ly.proj + 3 * I : nullptr, D->gate_values ? Ly.og : nullptr, s)))
       return rc;
-    if ((rc = linear_fwd(c, D->gate_values ? Ly.og : Ly.o, I, c.P(Ly.w_out), nullptr, Ly.x_ff, d, T, d, I, EPI_NONE,
-                         Ly.x_attn)))
-      return rc;
-    if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
+    if (fuse) {
+      if ((rc = linear_res_ln(c, D->gate_values ? Ly.og : Ly.o, I, c.P(Ly.w_out), nullptr, Ly.x_attn, Ly.x_ff, I,
+                              c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff)))
+        return rc;
+    } else {
+      if ((rc = linear_fwd(c, D->gate_values ? Ly.og : Ly.o, I, c.P(Ly.w_out), nullptr, Ly.x_ff, d, T, d, I, EPI_NONE,
+                           Ly.x_attn)))
+        return rc;
+      if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
+    }
     if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, ff, T, ff, d, EPI_GELU_DROP, nullptr,
                          Ly.u, ff, 1 << 30, 0, D->ff_offset, (uint32_t)li)))
       return rc;
     float* x_out = li + 1 < D->L ? D->layers[li + 1].x_attn : D->x_final;
-    if ((rc = linear_fwd(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
+    if (fuse && li + 1 < D->L) {   // + the next block's attention pre-norm
+      const XtrlTrainLayer& Ln = D->layers[li + 1];
+      if ((rc = linear_res_ln(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(Ln.ln_attn),
+                              Ln.xn_attn, d, nullptr, 0, Ln.st_attn)))
+        return rc;
+    } else if (fuse) {             // + the final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
+      if ((rc = linear_res_ln(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(D->ln_final),
+                              D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final)))
+        return rc;
+    } else {
+      if ((rc = linear_fwd(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
+    }
   }
   // final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
-  if ((rc = ln_fwd(c, D->x_final, c.P(D->ln_final), D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final))) return rc;
+  if (!fuse)
+    if ((rc = ln_fwd(c, D->x_final, c.P(D->ln_final), D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final))) return rc;
   // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
   if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
                        nullptr, D->zp, ldp, d)))
@@ -823,7 +882,14 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   // ---- decoder blocks, last to first.  Side events of the weight gradients whose dY buffer the
   // main stream overwrites later: dx (FF2 / out-projection), dff (FF1, by the next layer's FF2
   // input gradient), dproj (q|k|v projection, by the next layer's gate / attention backward).
-  hipEvent_t e_ff1 = nullptr, e_proj = nullptr;
+  // Fused LayerNorm backward (ln_fusable): the FF1 and q|k|v input-gradient GEMMs finish the
+  // LayerNorm backward and add the residual gradient in their epilogue, alternating between dx and
+  // dx2, so neither overwrites the buffer a pending side-stream weight gradient still reads: the FF
+  // block writes dx2 (read by the out-projection weight gradient), the attention block writes dx
+  // (read by the next FF2 weight gradient).
+  const bool fuse = ln_fusable(D);
+  XTRL_REQUIRE(!fuse || D->dx2, "train: fused LayerNorm backward needs dx2");
+  hipEvent_t e_ff1 = nullptr, e_proj = nullptr, e_out_prev = nullptr;
   for (int li = D->L - 1; li >= 0; --li) {
     const XtrlTrainLayer& Ly = D->layers[li];
     // FF2 (+ residual): dx is the gradient w.r.t. the block output
@@ -835,21 +901,30 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = F.fork())) return rc;
     if ((rc = wgrad(cw, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
     e_ff1 = F.mark();
-    if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
-    if ((rc = F.wait(e_ff2))) return rc;
-    if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
-      return rc;
+    float* xg = D->dx;   // gradient w.r.t. the attention block's output
+    if (fuse) {
+      if ((rc = F.wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
+      if ((rc = dgrad_ln_bwd(c, D->dff, ff, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx2,
+                             c.G(Ly.ln_ff))))
+        return rc;
+      xg = D->dx2;
+    } else {
+      if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+      if ((rc = F.wait(e_ff2))) return rc;
+      if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
+        return rc;
+    }
     // attention out-projection (+ residual) and the value gate
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dx, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
+    if ((rc = wgrad(cw, xg, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
     hipEvent_t e_out = F.mark();
     if ((rc = F.wait(e_proj))) return rc;
     if (D->gate_values) {
-      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30,
+      if ((rc = linear_dgrad(c, xg, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30,
                              Ly.proj + 3 * I, Ly.n_qkv, D->dproj + 3 * I, Ly.n_qkv)))
         return rc;
     } else {
-      if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_NONE))) return rc;
+      if ((rc = linear_dgrad(c, xg, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_NONE))) return rc;
     }
     const AttnProblem ap = attn_problem(c, Ly, li);
     if ((rc = attn_bwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse, D->dog, D->dproj, D->dproj + I,
@@ -874,11 +949,19 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = wgrad(cw, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
       return rc;
     e_proj = F.mark();
-    if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
-    if ((rc = F.wait(e_out))) return rc;
-    if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
-                     c.G(Ly.ln_attn))))
-      return rc;
+    if (fuse) {
+      if ((rc = F.wait(e_ff2))) return rc;   // this block's FF2 weight gradient read dx
+      if ((rc = dgrad_ln_bwd(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), Ly.n_qkv, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn),
+                             D->dx2, D->dx, c.G(Ly.ln_attn))))
+        return rc;
+      e_out_prev = e_out;
+    } else {
+      if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
+      if ((rc = F.wait(e_out))) return rc;
+      if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
+                       c.G(Ly.ln_attn))))
+        return rc;
+    }
   }
   // ---- embeddings: dx is d x0
   if ((rc = F.fork())) return rc;

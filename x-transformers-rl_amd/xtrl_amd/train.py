@@ -75,7 +75,7 @@ class FusedTrainStep:
                         hp=E(T, ldp), z1=E(T, 4 * d), h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d),
                         raw=E(T, n_out), values=E(T, B), pred=E(T, 2 * (S + 1)), done=E(T),
                         d_raw=E(T, n_out), d_values=E(T, B), d_pred=E(T, 2 * (S + 1)), d_done=E(T),
-                        dx=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
+                        dx=E(T, d), dx2=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
         # the library states its own partial-sum needs (LayerNorm-backward row blocks, column sums)
