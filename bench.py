@@ -124,13 +124,16 @@ class DecodeAttnTimer:
     def collect(self, lens):
         """After an update: add kernel time and algorithmic bytes of its T*L launches."""
         torch.cuda.synchronize()
-        for i in range(self.T * self.L):
+        lens = lens.cpu().numpy()
+        # the steps with a live episode (the rollout stops launching sub-graphs once none is live,
+        # so the event pairs of later steps may not belong to this update)
+        T_eff = int(lens.max())
+        for i in range(T_eff * self.L):
             self.ms += self.events[2 * i].elapsed_time(self.events[2 * i + 1])
-        self.launches += self.T * self.L
+        self.launches += T_eff * self.L
         c = self.eng.c
         H, dh = c.heads, c.dim_head
-        lens = lens.cpu().numpy()
-        t = np.arange(self.T)
+        t = np.arange(T_eff)
         alive = (lens[None, :] > t[:, None]).sum(1)                  # live episodes at step t
         # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + q|k|v|gate|mix row (4 dh + 1)
         # + value-residual row (dh) ; write K,V at t (2 dh) + output (dh)

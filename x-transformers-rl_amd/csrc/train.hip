@@ -9,6 +9,8 @@
 #include <cstdlib>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "kernels.h"
 #include "philox.h"
 
@@ -545,6 +547,17 @@ SideStream& side_stream() {
     if (e && atoi(e) == 0) return x;
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+    // XTRL_WGRAD_CUS=n (experiments): the side stream confined to n CUs, every (CUs / n)-th one
+    const char* cus = getenv("XTRL_WGRAD_CUS");
+    int dev = 0, ncu = 0;
+    if (cus && atoi(cus) > 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+      const int want = std::min(atoi(cus), ncu), step = std::max(1, ncu / want);
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0, n = 0; i < ncu && n < want; i += step, ++n) mask[i / 32] |= 1u << (i % 32);
+      x.ok = hipExtStreamCreateWithCUMask(&x.s, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+      return x;
+    }
     x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least) == hipSuccess;
     return x;
   }();

@@ -243,22 +243,49 @@ class RolloutEngine:
         """The per-episode decode state carried between deploy calls (Agent.forward hiddens)."""
         return [t for kv in self.kv for t in kv] + [self.v1]
 
+    CHUNK = int(os.environ.get('XTRL_ROLLOUT_CHUNK', '32'))   # steps per captured sub-graph
+
     @torch.no_grad()
     def run(self, seed, update, episode_of_slot, latent=None, slot_offset=0, slots=None):
-        """Roll out Tmax steps of the device Sim for all E slots; returns the trajectory dict."""
+        """Roll out Tmax steps of the device Sim for all E slots; returns the trajectory dict.
+
+        Graph mode: the T steps are captured as sub-graphs of CHUNK steps.  After launching chunk i
+        the host waits for chunk i - 1 (the GPU meanwhile runs chunk i) and reads the live-row count
+        of its last step (copied to pinned memory inside the stream); once a chunk ended with no
+        live episode, no further chunk is launched — the dead tail of a long-T rollout (C2: T = 500,
+        the longest of 768 episodes ~425 steps at hazard 1/64) costs one chunk, not T - max_len steps."""
         assert self.sim_mode != SIM_HOST
         self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
         if not self.use_graph:
             self._steps()
-        else:
-            if self.graph is None:
-                self._steps()   # warm-up launch outside capture (code objects loaded)
-                self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
+            return self.traj
+        if self.graph is None:
+            self._steps()   # warm-up launch outside capture (code objects loaded)
+            self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
+            CH = max(1, self.CHUNK)
+            self._chunks = [(t0, min(t0 + CH, self.T)) for t0 in range(0, self.T, CH)]
+            self._live_host = torch.zeros(len(self._chunks), dtype=torch.int32, pin_memory=True)
+            self._live_dev = torch.zeros(len(self._chunks), dtype=torch.int32, device=self.dev)
+            graphs = []
+            for i, (t0, t1) in enumerate(self._chunks):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    self._steps()
-                self.graph = g
-            self.graph.replay()
+                    for t in range(t0, t1):
+                        self.step(t)
+                    # live rows at the chunk's last step (the embed kernel of step t1 - 1 counted them)
+                    self._live_dev[i:i + 1].copy_(self.live_count[(t1 - 1) & 1:((t1 - 1) & 1) + 1])
+                graphs.append(g)
+            self.graph = graphs
+            self._chunk_ev = [torch.cuda.Event() for _ in self._chunks]
+        stream = torch.cuda.current_stream()
+        for i, g in enumerate(self.graph):
+            g.replay()
+            self._live_host[i:i + 1].copy_(self._live_dev[i:i + 1], non_blocking=True)
+            self._chunk_ev[i].record(stream)
+            if i >= 1:
+                self._chunk_ev[i - 1].synchronize()
+                if int(self._live_host[i - 1]) == 0:
+                    break
         return self.traj
 
     @torch.no_grad()
