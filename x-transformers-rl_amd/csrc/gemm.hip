@@ -1228,6 +1228,59 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
   }
 }
 
+// every queued split-K job in one launch (SplitKQueue, kernels.h): thread unit u < total float4
+// units sums the S partial float4s of its job's element group in z order (eight loads in flight),
+// the remaining units the row sums (bias gradients).  Jobs are passed by value (kernel arguments).
+struct SplitKJobs {
+  SplitKJob job[kMaxSplitKJobs];
+  int n;
+  int64_t total_q, total_r;
+};
+__global__ __launch_bounds__(256) void k_splitk_reduce_multi(const SplitKJobs J) {
+  const int64_t gsz = (int64_t)gridDim.x * 256;
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < J.total_q + J.total_r; u += gsz) {
+    if (u < J.total_q) {
+      int j = 0;
+      while (j + 1 < J.n && J.job[j + 1].q0 <= u) ++j;
+      const SplitKJob& b = J.job[j];
+      const int64_t q = u - b.q0, MN4 = (int64_t)b.M * b.N / 4;
+      const float4* w4 = reinterpret_cast<const float4*>(b.ws);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      int z = 0;
+      for (; z + 8 <= b.S; z += 8) {
+        float4 p[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[k] = w4[(int64_t)(z + k) * MN4 + q];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          a.x += p[k].x; a.y += p[k].y; a.z += p[k].z; a.w += p[k].w;
+        }
+      }
+      for (; z < b.S; ++z) {
+        const float4 p = w4[(int64_t)z * MN4 + q];
+        a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+      }
+      const int64_t i = q << 2;
+      const int m = (int)(i / b.N), n = (int)(i - (int64_t)m * b.N);
+      float4* dst = reinterpret_cast<float4*>(b.C + (int64_t)m * b.ldc + n);
+      if (b.beta != 0.f) {
+        const float4 o = *dst;
+        a.x += b.beta * o.x; a.y += b.beta * o.y; a.z += b.beta * o.z; a.w += b.beta * o.w;
+      }
+      *dst = a;
+    } else {
+      const int64_t r = u - J.total_q;
+      int j = 0;
+      while (j + 1 < J.n && J.job[j + 1].r0 <= r) ++j;
+      const SplitKJob& b = J.job[j];
+      const int m = b.m0 + (int)(r - b.r0);
+      float acc = 0.f;
+      for (int z = 0; z < b.S; ++z) acc += b.rws[(int64_t)z * b.M + m];
+      b.rowsum[m - b.m0] += acc;
+    }
+  }
+}
+
 bool xcd_env() {   // XTRL_GEMM_XCD=0: hardware workgroup order (A/B experiments)
   static const bool on = [] {
     const char* e = getenv("XTRL_GEMM_XCD");
@@ -1474,8 +1527,30 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
 
 // weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
 // split the token range over workgroups (partial 64x64 tiles in ws), then a fixed-order sum
+int splitk_flush(SplitKQueue& q, hipStream_t s) {
+  if (q.n == 0) return XTRL_OK;
+  SplitKJobs J;
+  J.n = q.n;
+  J.total_q = J.total_r = 0;
+  for (int j = 0; j < q.n; ++j) {
+    J.job[j] = q.job[j];
+    J.job[j].q0 = J.total_q;
+    J.job[j].r0 = J.total_r;
+    J.total_q += (int64_t)q.job[j].M * q.job[j].N / 4;
+    J.total_r += q.job[j].rowsum ? q.job[j].M - q.job[j].m0 : 0;
+  }
+  const int64_t units = J.total_q + J.total_r;
+  hipLaunchKernelGGL(k_splitk_reduce_multi, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 8192))),
+                     dim3(256), 0, s, J);
+  q.n = 0;
+  q.used = 0;
+  XTRL_LAUNCHED("splitk_flush");
+  return XTRL_OK;
+}
+
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
-               float* ws, int64_t ws_floats, hipStream_t s, float* db, int db_n0, const GemmProfile* prof) {
+               float* ws, int64_t ws_floats, hipStream_t s, float* db, int db_n0, const GemmProfile* prof,
+               SplitKQueue* defer) {
   XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
   XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
   XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
@@ -1498,6 +1573,23 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   int kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
   splits = (M + kspan - 1) / kspan;
   auto need = [&](int sp) { return (int64_t)sp * N * K + (db ? (int64_t)sp * N : 0); };
+  // deferred reduction: float4 element groups, and a dW no queued job also writes (jobs of one
+  // launch run concurrently); the partials go behind the queued jobs' in ws
+  bool deferred = defer && splits > 1 && K % 4 == 0 && ldw % 4 == 0 && aligned16(dW);
+  if (deferred)
+    for (int j = 0; j < defer->n; ++j) {
+      const SplitKJob& o = defer->job[j];
+      const float *a0 = dW, *a1 = dW + (int64_t)(N - 1) * ldw + K, *b0 = o.C, *b1 = o.C + (int64_t)(o.M - 1) * o.ldc + o.N;
+      if (a0 < b1 && b0 < a1) deferred = false;
+      if (db && o.rowsum && db < o.rowsum + (o.M - o.m0) && o.rowsum < db + (N - db_n0)) deferred = false;
+    }
+  if (deferred && (defer->n == kMaxSplitKJobs || defer->used + need(splits) > ws_floats)) {
+    if (int rc = splitk_flush(*defer, s)) return rc;   // the queued partials are summed first
+  }
+  if (deferred) {
+    ws += defer->used;
+    ws_floats -= defer->used;
+  }
   while (splits > 1 && need(splits) > ws_floats) {   // fit the partial slabs in ws
     splits = std::max(1, splits / 2);
     kspan = ((M + splits - 1) / splits + 31) / 32 * 32;
@@ -1535,7 +1627,12 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
       ++*prof->n;
     }
   } else launch<2, 2, 1, 1, 1, true, true, EPI_NONE, false, false, true>(a, s);
-  if (splits > 1) {
+  if (splits > 1 && deferred) {
+    SplitKJob& j = defer->job[defer->n++];
+    j.ws = ws; j.C = dW; j.rws = a.rowsum_ws; j.rowsum = db; j.S = splits; j.M = N; j.N = K; j.ldc = ldw;
+    j.m0 = db_n0; j.beta = beta; j.q0 = j.r0 = 0;
+    defer->used += need(splits);
+  } else if (splits > 1) {
     const int64_t MN = (int64_t)N * K;
     const int64_t units = MN;   // scalar path: a thread per element; float4 path: four lanes per float4
     hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 4096))),

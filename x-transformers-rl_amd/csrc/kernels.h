@@ -81,9 +81,29 @@ struct GemmProfile {
   int cap;
   int* n;
 };
+// Deferred split-K reductions: the weight gradients of one backward write their partial tiles to
+// disjoint workspace ranges and queue their reduction; splitk_flush sums every queued job in ONE
+// launch (fixed order per element: deterministic) instead of a reduce launch per weight.
+struct SplitKJob {
+  const float* ws;       // partials [S][M][N]
+  float* C;              // C[m][n] (ldc) = beta C + sum_z partial
+  const float* rws;      // optional row-sum partials [S][M] -> rowsum[m - m0] += sum_z
+  float* rowsum;
+  int S, M, N, ldc, m0;
+  float beta;
+  int64_t q0, r0;        // first float4 unit / first row-sum unit of this job in the launch
+};
+constexpr int kMaxSplitKJobs = 24;
+struct SplitKQueue {
+  SplitKJob job[kMaxSplitKJobs];
+  int n = 0;
+  int64_t used = 0;      // workspace floats taken by the queued jobs
+};
+int splitk_flush(SplitKQueue& q, hipStream_t s);
+
 int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int ldw, int M, int N, int K, float beta,
                float* ws, int64_t ws_floats, hipStream_t s, float* db = nullptr, int db_n0 = 0,
-               const GemmProfile* prof = nullptr);
+               const GemmProfile* prof = nullptr, SplitKQueue* defer = nullptr);
 int gemm_f32(const float* X, int ldx, const float* W, int ldw, const float* bias, const float* ln_gamma,
              const float* R, int ldr, float* Y, int ldy, const int32_t* t_dev, int64_t y_t_stride, int M, int N,
              int K, int act, hipStream_t s);

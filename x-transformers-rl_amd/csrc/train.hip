@@ -514,6 +514,7 @@ struct Ctx {
   const XtrlTrainDesc* D;
   hipStream_t s;
   int T;
+  SplitKQueue* q = nullptr;   // weight gradients: split-K reductions deferred to one launch
   const float* P(int64_t off) const { return off >= 0 ? D->flat + off : nullptr; }
   float* G(int64_t off) const { return off >= 0 ? D->grad + off : nullptr; }
 };
@@ -643,7 +644,7 @@ int wgrad(const Ctx& c, const float* dY, int ldy, const float* X, int ldx, float
           float* db = nullptr, int db_n0 = 0) {
   const GemmProfile prof{c.D->prof_events, c.D->prof_flops, c.D->prof_cap, c.D->prof_n};
   return gemm_wgrad(dY, ldy, X, ldx, dW, K, M, N, K, 1.f, c.D->ws, c.D->ws_floats, c.s, db, db_n0,
-                    c.D->prof_events && c.D->prof_n ? &prof : nullptr);
+                    c.D->prof_events && c.D->prof_n ? &prof : nullptr, c.q);
 }
 
 // dst[0:cols] += sum over rows of src (optionally weighted by rw[r * ld_rw] * rw_scale)
@@ -855,7 +856,14 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   SideStream& side = side_stream();
   const bool two = side.ok && side.ensure(side_events_needed(D->L));
   Fork F{s, side.s, two ? &side : nullptr};
-  const Ctx cw{D, two ? side.s : s, T};   // weight gradients
+  // weight gradients (side stream); their split-K partials are summed by one launch at the end
+  // (XTRL_SPLITK_DEFER=0: a reduce launch after every weight-gradient GEMM)
+  static const bool defer = [] {
+    const char* e = getenv("XTRL_SPLITK_DEFER");
+    return !(e && atoi(e) == 0);
+  }();
+  SplitKQueue skq;
+  const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
   // ---- actor / critic heads
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
@@ -1007,6 +1015,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     XTRL_LAUNCHED("train embed grad");
   }
   // every weight gradient is in before the caller's optimiser step
+  if ((rc = splitk_flush(skq, cw.s))) return rc;
   if ((rc = F.wait(F.mark()))) return rc;
   XTRL_REQUIRE(!F.failed, "train: side-stream event record failed");
   XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L), "train: side events %d != %d", F.next,

@@ -140,7 +140,9 @@ class Agent(nn.Module):
             p.grad = None
         self.ema_flat = self.flat.flat.clone()
         self.flat.rebind(self.ema_model, self.ema_flat)
-        self.gemm_ws = torch.empty(32 << 20, device=dev)    # split-K weight-gradient partial tiles (128 MiB)
+        # split-K weight-gradient partial tiles: one backward's deferred partials (C3 ~190 MB per
+        # minibatch) stay resident until its single reduce launch (384 MiB)
+        self.gemm_ws = torch.empty(96 << 20, device=dev)
         self.model.bind_flat(self.flat, self.gemm_ws)
         ek = dict(EMA_DEFAULTS)
         unknown = set(ema_kwargs or {}) - set(ek)
