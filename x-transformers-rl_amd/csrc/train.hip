@@ -559,7 +559,10 @@ SideStream& side_stream() {
       x.ok = hipExtStreamCreateWithCUMask(&x.s, (uint32_t)mask.size(), mask.data()) == hipSuccess;
       return x;
     }
-    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, least) == hipSuccess;
+    // XTRL_WGRAD_PRIO=1 (experiments): the side stream at the highest priority instead of the lowest
+    const char* pr = getenv("XTRL_WGRAD_PRIO");
+    x.ok = hipStreamCreateWithPriority(&x.s, hipStreamNonBlocking, (pr && atoi(pr) == 1) ? greatest : least) ==
+           hipSuccess;
     return x;
   }();
   return S;
