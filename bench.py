@@ -388,6 +388,8 @@ def main():
         gtimer.attach()
     if world > 1:
         dist.barrier()
+    from xtrl_amd import distributed as dist_
+    coll0 = dict(dist_.COUNTS)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     total = torch.zeros((), device='cuda', dtype=torch.int64)
@@ -409,6 +411,9 @@ def main():
         dist.all_reduce(total)
     elapsed = float(el)
     env_steps = int(total)
+    # collectives of the timed updates (per rank): the bucketed gradient all-reduces, RSNorm rides in
+    # the last bucket, fitness sums
+    coll = {k: (dist_.COUNTS[k] - coll0[k]) / args.steps for k in coll0} if world > 1 else None
     value = env_steps / elapsed
 
     # committed profiles (profiles/rNN_*) are of the default C3 bench: quoted for that workload only
@@ -478,6 +483,11 @@ def main():
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
                     roofline=roofline, attention_roofline=attn_roofline, cpu_baseline=cpu, ppo_loss=loss_delta,
                     phase_ms=phase_ms)
+        if coll is not None:
+            mb = learner.agent.epochs * (len(learner.episode_genes_for_process) // learner.agent.batch_size)
+            line['dp'] = dict(backend=dist.get_backend(), collectives_per_update=coll,
+                              optimiser_steps_per_update=mb,
+                              grad_allreduces_per_step=round(coll['all_reduce'] / mb, 3))
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

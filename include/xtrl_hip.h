@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 10
+#define XTRL_ABI_VERSION 11
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -399,6 +399,13 @@ typedef struct XtrlTrainDesc {
   double* prof_flops;
   int prof_cap;
   int* prof_n;
+  /* optional data-parallel gradient buckets (NULL = off): the backward records, for bucket i =
+   * 0 .. L + 1 in completion order (0: heads + final norm, 1 + j: decoder block L - 1 - j, L + 1:
+   * embeddings / everything), grad_events[2i] on the caller's stream and grad_events[2i + 1] on the
+   * weight-gradient stream once every gradient of the bucket is final, so the caller can all-reduce
+   * bucket i (a contiguous range of the flat gradient, xtrl_amd.model flat_order) while the backward
+   * continues (DDP's bucketed all-reduce, xtrl.py:885/981) */
+  void** grad_events;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

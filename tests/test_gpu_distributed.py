@@ -35,15 +35,19 @@ def _free_port():
     return port
 
 
-def _make(world, shard_by_gene=False, genes=3, episodes=4):
+def _make(world, shard_by_gene=False, genes=3, episodes=4, fractal=None):
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(3)
-    wm = dict(attn_dim_head=16, heads=4, depth=2, attn_gate_values=True, add_value_residual=True,
-              learned_value_residual_mix=True)
+    wm = dict(attn_dim_head=16, heads=4, depth=2)
+    extra = {}
+    if fractal:   # the C5 policy body (causal fractal encoder), as bench.py C5 runs it
+        extra = dict(policy_body='fractal', fractal_levels=fractal)
+    else:
+        wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     learner = Learner(8, 4, (-2., 2.), world_model=wm, max_timesteps=20, batch_size=2,
                       num_episodes_per_update=episodes, evolutionary=True, evolve_every=1, evolve_after_step=0,
                       latent_gene_pool=dict(dim=8, num_genes_per_island=genes, num_selected=2, tournament_size=2),
-                      agent_kwargs=dict(dropout=0.1, seed=7, hidden_dim=48, save_path='/tmp/xtrl_dp_test.pt'),
+                      agent_kwargs=dict(dropout=0.1, seed=7, hidden_dim=48, save_path='/tmp/xtrl_dp_test.pt', **extra),
                       use_graph=False, shard_by_gene=shard_by_gene)
     return learner, SynthVecSim(8, 4, 'lander', hazard_log2=3)
 
@@ -62,8 +66,11 @@ def _worker(rank, world, port, out_dir, mode):
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        gene_mode = mode == 'genes'
-        learner, env = _make(world, shard_by_gene=gene_mode, genes=4 if gene_mode else 3)
+        gene_mode = mode in ('genes', 'c5')
+        if mode == 'c5':     # population 8 over 4 ranks (2 genes each), fractal body
+            learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
+        else:
+            learner, env = _make(world, shard_by_gene=gene_mode, genes=4 if gene_mode else 3)
         a = learner.agent
         traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
         first = dict(actions=traj['actions'].cpu().clone(), lens=lens.cpu().clone(), fit=learner.fitness(cum, genes))
@@ -151,6 +158,31 @@ def test_gene_sharded_epo_partition(tmp_path):
     traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
     fit = learner.fitness(cum, genes)
     for rank in range(2):
+        slots = torch.tensor(r[rank]['slots'])
+        assert torch.equal(r[rank]['first']['lens'], lens.cpu()[slots])
+        assert torch.equal(r[rank]['first']['actions'], traj['actions'].cpu()[slots])
+        torch.testing.assert_close(r[rank]['first']['fit'], fit, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_c5_gene_sharded_population8_four_ranks(tmp_path):
+    """The C5 partition at world 4: EPO population 8, gene g on rank g (mod 4) — two genes per rank —
+    with the fractal policy body, two full learning updates (evolve_ every minibatch).  Ranks stay
+    bitwise in lockstep (weights, EMA, RSNorm, genes); each rank's rollout reproduces the single-
+    process rollout at its global pair slots and the fitness summed over ranks equals the single-
+    process fitness."""
+    r = _run(tmp_path, 'c5', world=4)
+    for rank in range(4):
+        assert {g for _, g in r[rank]['pairs']} == {rank, rank + 4}
+        assert len(r[rank]['pairs']) == 2 * 2
+    for k in ('flat', 'ema', 'rs_mean', 'rs_var', 'genes'):
+        for rank in range(1, 4):
+            assert torch.equal(r[0][k], r[rank][k]), (k, rank)
+    assert torch.isfinite(r[0]['flat']).all()
+    learner, env = _make(1, genes=8, episodes=2, fractal=2)
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    fit = learner.fitness(cum, genes)
+    for rank in range(4):
         slots = torch.tensor(r[rank]['slots'])
         assert torch.equal(r[rank]['first']['lens'], lens.cpu()[slots])
         assert torch.equal(r[rank]['first']['actions'], traj['actions'].cpu()[slots])

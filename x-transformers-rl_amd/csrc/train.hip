@@ -867,6 +867,19 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   }();
   SplitKQueue skq;
   const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
+  // data-parallel gradient buckets: flush the bucket's deferred reductions, then record its events
+  int bucket = 0;
+  auto bucket_done = [&]() -> int {
+    if (!D->grad_events) return XTRL_OK;
+    if (int rc = splitk_flush(skq, cw.s)) return rc;
+    if (hipEventRecord((hipEvent_t)D->grad_events[2 * bucket], s) != hipSuccess ||
+        hipEventRecord((hipEvent_t)D->grad_events[2 * bucket + 1], cw.s) != hipSuccess) {
+      set_error("train: gradient bucket event record failed");
+      return XTRL_E_HIP;
+    }
+    ++bucket;
+    return XTRL_OK;
+  };
   // ---- actor / critic heads
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
@@ -903,6 +916,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
                    c.P(D->ln_final), nullptr, D->dx, c.G(D->ln_final))))
     return rc;
+  if ((rc = bucket_done())) return rc;   // bucket 0: heads, state / gene embeddings, final norm
   // ---- decoder blocks, last to first.  Side events of the weight gradients whose dY buffer the
   // main stream overwrites later: dx (FF2 / out-projection), dff (FF1, by the next layer's FF2
   // input gradient), dproj (q|k|v projection, by the next layer's gate / attention backward).
@@ -986,6 +1000,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
                        c.G(Ly.ln_attn))))
         return rc;
     }
+    if ((rc = bucket_done())) return rc;   // bucket L - li: decoder block li
   }
   // ---- embeddings: dx is d x0
   if ((rc = F.fork())) return rc;
@@ -1019,6 +1034,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   }
   // every weight gradient is in before the caller's optimiser step
   if ((rc = splitk_flush(skq, cw.s))) return rc;
+  if ((rc = bucket_done())) return rc;   // bucket L + 1: embeddings (and the flat buffer's tail)
   if ((rc = F.wait(F.mark()))) return rc;
   XTRL_REQUIRE(!F.failed, "train: side-stream event record failed");
   XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L), "train: side events %d != %d", F.next,

@@ -14,6 +14,9 @@ import torch
 import torch.distributed as dist
 
 
+COUNTS = dict(all_reduce=0, broadcast=0)   # collectives issued by this module (bench rehearsal lines)
+
+
 def is_distributed():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
@@ -73,6 +76,7 @@ def mean_(t):
     if is_distributed():
         x, staged = _on_backend_device(t)
         dist.all_reduce(x)
+        COUNTS['all_reduce'] += 1
         x.div_(dist.get_world_size())
         if staged:
             t.copy_(x)
@@ -83,6 +87,7 @@ def sum_(t):
     if is_distributed():
         x, staged = _on_backend_device(t)
         dist.all_reduce(x)
+        COUNTS['all_reduce'] += 1
         if staged:
             t.copy_(x)
     return t
@@ -92,6 +97,62 @@ def broadcast_(t, src=0):
     if is_distributed():
         x, staged = _on_backend_device(t)
         dist.broadcast(x, src)
+        COUNTS['broadcast'] += 1
         if staged:
             t.copy_(x)
     return t
+
+
+class BucketAllReduce:
+    """DDP's bucketed gradient all-reduce (xtrl.py:885/981) overlapped with the fused backward: the
+    backward records, per bucket of the flat gradient (contiguous ranges in completion order,
+    model.flat_bucket_ranges), an event on each of its two streams once the bucket is final
+    (XtrlTrainDesc.grad_events); ``run`` — called right after the backward is enqueued — makes a
+    communication stream wait for each bucket's events and starts its all-reduce there, so bucket i
+    travels over RCCL / xGMI while the backward still computes buckets i + 1 ...; the caller's
+    stream then waits for all of them and divides by the world size (mean)."""
+
+    MIN_BUCKET = int(os.environ.get('XTRL_DP_BUCKET_FLOATS', str(1 << 20)))   # >= 4 MB per collective
+
+    def __init__(self, buf, ranges):
+        import ctypes as C
+        self.buf, self.ranges = buf, list(ranges)
+        self.groups = self.coalesce(self.ranges, self.MIN_BUCKET)
+        self.events = [torch.cuda.Event() for _ in range(2 * len(self.ranges))]
+        for e in self.events:     # torch creates the HIP event on first record
+            e.record()
+        self.handles = (C.c_void_p * len(self.events))(*[e.cuda_event for e in self.events])
+        self.comm = torch.cuda.Stream(device=buf.device)
+
+    @staticmethod
+    def coalesce(ranges, min_floats):
+        """Consecutive backward buckets merge until a collective carries >= min_floats (a ring
+        all-reduce over xGMI pays a fixed latency per call; C3 -> 3 collectives per optimiser
+        step); a small remainder joins the last group.  -> [(start, end, index of the last member)]:
+        a merged bucket waits for its last member's events."""
+        groups, cur = [], None
+        for i, (a, b) in enumerate(ranges):
+            cur = [a, b, i] if cur is None else [cur[0], b, i]
+            if b - cur[0] >= min_floats:
+                groups.append(tuple(cur))
+                cur = None
+        if cur is not None:
+            if groups and cur[1] - cur[0] < min_floats // 4:
+                cur = [groups.pop()[0], cur[1], cur[2]]
+            groups.append(tuple(cur))
+        return groups
+
+    def run(self):
+        world = dist.get_world_size()
+        works = []
+        with torch.cuda.stream(self.comm):
+            for a, b, i in self.groups:
+                self.comm.wait_event(self.events[2 * i])
+                self.comm.wait_event(self.events[2 * i + 1])
+                if b > a:
+                    works.append(dist.all_reduce(self.buf[a:b], async_op=True))
+                    COUNTS['all_reduce'] += 1
+        for w in works:
+            w.wait()              # the caller's stream waits for the collective
+        self.buf.div_(world)
+        return self.buf

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 from pathlib import Path
 
 import numpy as np
@@ -383,14 +384,19 @@ class Agent(nn.Module):
                 self.flat.zero_grad()
                 if self.fused_learn:
                     stats = step.loss(K, stats_rows[len(self.logs) - logs0])
-                    step.backward()
+                    bar = self.bucket_allreduce()
+                    step.backward(bar.handles if bar is not None else None)
                     loss = stats[L.LS['loss']]
+                    # DDP gradient mean (xtrl.py:981), bucketed and overlapped with the backward; the
+                    # RSNorm batch mean (xtrl.py:601) rides in the last bucket's tail
+                    if bar is not None:
+                        bar.run()
+                    else:
+                        dist_.mean_(self.flat.grad_ext)
                 else:
                     loss, stats = ops.fused_loss(raw, values, pred_raw, done_logit, K)
                     loss.backward()
-                # DDP gradient mean (xtrl.py:981); the fused path's RSNorm batch mean (xtrl.py:601) is in
-                # the same buffer, so one collective per optimiser step
-                dist_.mean_(self.flat.grad_ext if fused else self.flat.grad)
+                    dist_.mean_(self.flat.grad)   # DDP gradient mean (xtrl.py:981)
                 if probe is not None:
                     probe(epoch, mbi, idx, loss, stats)
                 self.optimizer_step()
@@ -416,6 +422,17 @@ class Agent(nn.Module):
                 self.logs.append(stats)
         self.rs_mean, self.rs_var, self.rs_step = rs_mean, rs_var, rs_step
         self.step += 1
+
+    def bucket_allreduce(self):
+        """The overlapped bucketed all-reduce of the fused learn step (None: one process, or
+        XTRL_DP_BUCKETS=0 for one all-reduce after the backward)."""
+        if not dist_.is_distributed() or os.environ.get('XTRL_DP_BUCKETS', '1') == '0' \
+                or not hasattr(self.model, 'flat_bucket_ranges') or self.flat.flat.device.type != 'cuda':
+            return None
+        bar = getattr(self, '_bar', None)
+        if bar is None:
+            self._bar = bar = dist_.BucketAllReduce(self.flat.grad_ext, self.model.flat_bucket_ranges(self.flat))
+        return bar
 
     def batch_gather(self, Tmax):
         bg = getattr(self, '_batch_gather', None)

@@ -181,31 +181,66 @@ class WorldModelActorCritic(nn.Module):
         return (logits.softmax(dim=-1) * self.hl_centers).sum(-1)
 
     # ---- flat-buffer layout / binding ---------------------------------------------------------------
-    def flat_order(self):
-        """Parameter order of the flat buffer: the q|k|v|gate|mix weights of each attention block, the
-        first actor / critic head layers and to_pred.0 | to_pred_done are adjacent so their
-        concatenations are views (one GEMM operand each).  Groups whose size is a multiple of 4
-        floats come first, so every GEMM weight starts 16-byte aligned (float4 operand loads)."""
+    def flat_buckets_names(self):
+        """Parameter groups of the flat buffer, bucketed in the order the fused backward completes
+        them (train.hip records an event per bucket, include/xtrl_hip.h grad_events): [heads + state /
+        gene embeddings + final norm], [decoder block L-1], ..., [block 0], [input embeddings].  A
+        group's names must be adjacent: the q|k|v|gate|mix weights of each attention block, the first
+        actor / critic head layers and to_pred.0 | to_pred_done are one GEMM operand each (views).
+        Groups whose size is not a multiple of 4 floats move to the last bucket, so every GEMM weight
+        starts 16-byte aligned (float4 operand loads).  -> list of buckets, each a list of groups."""
         c = self.cfg
         params = dict(self.named_parameters())
-        groups = []
-        for li, (_, _) in enumerate(self.blocks()):
-            pre = f'transformer.attn_layers.layers.{2 * li}.1.'
+        taken = set()
+
+        def grp(names):
+            taken.update(names)
+            return list(names)
+
+        heads = [grp(['action_head.0.weight', 'critic_head.0.weight']), grp(['action_head.0.bias', 'critic_head.0.bias']),
+                 grp(['to_pred.0.weight', 'to_pred_done.0.weight']), grp(['to_pred.0.bias', 'to_pred_done.0.bias'])]
+        head_pre = ('action_head.', 'critic_head.', 'to_pred.', 'to_pred_done.', 'to_state_embed.', 'latent_to_embed.',
+                    'transformer.attn_layers.final_norm.')
+        heads += [grp([n]) for n in params if n not in taken and n.startswith(head_pre)]
+        blocks = []
+        for li in reversed(range(len(self.blocks()))):
+            pa, pf = f'transformer.attn_layers.layers.{2 * li}.', f'transformer.attn_layers.layers.{2 * li + 1}.'
+            pre = pa + '1.'
             mix = c.value_residual and c.learned_mix and li > 0
-            groups.append([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
-                          + ([pre + 'to_v_gate.weight'] if c.gate_values else [])
-                          + ([pre + 'to_value_residual_mix.0.weight'] if mix else []))
+            g = [grp([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight']
+                     + ([pre + 'to_v_gate.weight'] if c.gate_values else [])
+                     + ([pre + 'to_value_residual_mix.0.weight'] if mix else []))]
             bias = ([pre + 'to_v_gate.bias'] if c.gate_values else []) + \
                    ([pre + 'to_value_residual_mix.0.bias'] if mix else [])
             if bias:
-                groups.append(bias)
-        groups += [['action_head.0.weight', 'critic_head.0.weight'], ['action_head.0.bias', 'critic_head.0.bias'],
-                   ['to_pred.0.weight', 'to_pred_done.0.weight'], ['to_pred.0.bias', 'to_pred_done.0.bias']]
-        taken = {n for g in groups for n in g}
-        groups += [[n] for n in params if n not in taken]
+                g.append(grp(bias))
+            g += [grp([n]) for n in params if n not in taken and (n.startswith(pa) or n.startswith(pf))]
+            blocks.append(g)
+        embeds = [grp([n]) for n in params if n not in taken]
+        buckets = [heads] + blocks + [embeds]
         size = lambda g: sum(params[n].numel() for n in g)
-        groups.sort(key=lambda g: size(g) % 4 != 0)   # stable: aligned groups first
-        return [n for g in groups for n in g]
+        tail = [g for b in buckets for g in b if size(g) % 4]
+        buckets = [[g for g in b if size(g) % 4 == 0] for b in buckets]
+        buckets[-1] += tail
+        return buckets
+
+    def flat_order(self):
+        return [n for b in self.flat_buckets_names() for g in b for n in g]
+
+    def flat_bucket_ranges(self, flat):
+        """[(start, end)] of each bucket in ``flat.grad_ext`` (the last one runs to its end: the
+        RSNorm-mean tail rides with it)."""
+        out = []
+        for b in self.flat_buckets_names():
+            names = [n for g in b for n in g]
+            out.append([flat.index[names[0]][0], flat.index[names[-1]][1]] if names else None)
+        for i in range(len(out)):
+            if out[i] is None:
+                out[i] = [out[i - 1][1], out[i - 1][1]] if i else [0, 0]
+        for a, b in zip(out, out[1:]):
+            assert a[1] == b[0], 'flat buckets are not contiguous'
+        out[-1][1] = flat.grad_ext.numel()
+        return [tuple(r) for r in out]
 
     def bind_flat(self, flat, ws):
         """Record the concatenated weight / gradient views used by forward_train."""

@@ -184,7 +184,10 @@ class FusedTrainStep:
         del T
         return stats.clone() if own else stats
 
-    def backward(self):
+    def backward(self, grad_events=None):
+        """``grad_events``: ctypes array of 2 (L + 2) HIP event handles recorded per gradient bucket
+        (distributed.BucketAllReduce), or None."""
+        self.D.grad_events = C.cast(grad_events, C.POINTER(C.c_void_p)) if grad_events is not None else None
         L.check(L.lib().xtrl_train_backward(C.byref(self.D), L.stream()), 'train_backward')
 
 
