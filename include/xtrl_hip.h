@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 11
+#define XTRL_ABI_VERSION 12
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -410,6 +410,62 @@ typedef struct XtrlTrainDesc {
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
 int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Hand-scheduled learn step of the causal fractal policy body (xtrl_amd.fractal
+ * FractalPolicyActorCritic: fractal_rl.py:116-132, 274-346 made causal per timestep, DESIGN.md
+ * decision log).  Replaces the reference-mode autograd step (model.forward_train + loss.backward,
+ * xtrl.py:928-983): the base XtrlTrainDesc carries the minibatch, the heads (identical to the
+ * decoder's: to_pred / to_pred_done / actor / critic / state and gene embeddings), the loss
+ * gradients and the workspaces (its layers / L / H-projection fields are unused; w_pin / ln_final
+ * unused); the fractal descriptor the encoder.  Per level: x_in = x + level_embed; q|k|v; causal
+ * flash attention (dropout); s1 = x_in + o W_out^T, x1 = LN1(s1); s2 = x1 + (g W_gv^T) W_go^T,
+ * x2 = LN2(s2); h = drop(gelu(x2 W1^T + b1)); s3 = x2 + h W2^T + b2, x3 = LN3(s3); mean = causal
+ * running mean of x3; cat[:, l d:] = mean W_p^T + b_p; g <- g + mean W_gu^T + b_gu.  Then
+ * features = ReLU(cat W_fa0^T + b) W_fa2^T + b (cat's last d columns: the final g).
+ * nn.LayerNorm (weight and bias) is formed in the epilogue of the GEMM completing its rows.
+ * --------------------------------------------------------------------------------------------- */
+typedef struct XtrlFractalTrainLevel {
+  int64_t w_qkv;                   /* self_attn.to_q | to_k | to_v [3I][d], adjacent in the flat buffer */
+  int64_t w_out, w_gv, w_go;       /* self_attn.to_out [d][I], global_attn.to_v [I][d], .to_out [d][I] */
+  int64_t ln1_w, ln1_b, ln2_w, ln2_b, ln3_w, ln3_b;
+  int64_t w_ff1, b_ff1, w_ff2, b_ff2, w_proj, b_proj, level_embed;
+  /* activations [T][.] kept for the backward */
+  float* xin;                      /* [T][d] level input (x + level embedding) */
+  float* qkv;                      /* [T][3I] */
+  float* o;                        /* [T][I] attention output */
+  float* lse;                      /* [b][H][n] */
+  float* s1; float* x1; float* st1;   /* pre-norm sum, normalised, (mean, rstd) [T][2] */
+  float* g;                        /* [T][d] global state entering the level */
+  float* gv;                       /* [T][I] g W_gv^T */
+  float* s2; float* x2; float* st2;
+  float* h; float* u;              /* [T][ff] drop(gelu) and its saved derivative */
+  float* s3; float* x3; float* st3;
+  float* mean;                     /* [T][d] causal running mean of x3 */
+} XtrlFractalTrainLevel;
+
+typedef struct XtrlFractalTrainDesc {
+  int levels;
+  int64_t b_in;                    /* input_embed.bias (its weight: the base's w_pin) */
+  int64_t g_init, w_gu, b_gu, w_fa0, b_fa0, w_fa2, b_fa2;
+  const float* scale_embeds;       /* [levels][d] (level_embedding.scale_embeds buffer) */
+  float* le;                       /* [levels][d] scratch: level_embeds + scale_embeds */
+  float* bias0;                    /* [d] scratch: input_embed.bias + le[0] */
+  float* cat;                      /* [T][(levels + 1) d] level projections | final global state */
+  float* hfa;                      /* [T][2d] ReLU(final_aggregation[0]) */
+  /* backward scratch [T][.] */
+  float* dxa; float* dxb; float* ds; float* dmean; float* dga; float* dgb;
+  float* dgv;                      /* [T][I] */
+  float* dz;                       /* [T][ff] */
+  float* dqkv;                     /* [T][3I] */
+  float* dob;                      /* [T][I] */
+  float* dcat;                     /* [T][(levels + 1) d] */
+  float* dhfa;                     /* [T][2d] */
+  const XtrlFractalTrainLevel* level;   /* host array [levels] */
+} XtrlFractalTrainDesc;
+
+int xtrl_fractal_train_forward(const XtrlTrainDesc* base, const XtrlFractalTrainDesc* f, void* stream);
+int xtrl_fractal_train_backward(const XtrlTrainDesc* base, const XtrlFractalTrainDesc* f, void* stream);
 /* Y = drop(gelu(X W^T + b)) and deriv = drop(gelu'(X W^T + b)) (x-transformers FeedForward's first
  * Linear + GELU + Dropout, xtrl.py Decoder ff; fractal_rl.py FeedForward), dropout keep bits the
  * stream of xtrl_ff_dropout_mask(seed, offset, layer) and of the fused learn step */

@@ -857,9 +857,9 @@ def test_fused_train_step_large_tiles_matches_autograd():
     _fused_vs_autograd(False, False, True, 0.25, 130, depth=2, episodes=96, batch=96, hazard=9, dim=128)
 
 
-def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, dim):
+def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, dim, fractal=None):
     learner, env, _ = make_learner(depth=depth, gates=gates, evo=evo, cont=cont, T=T, episodes=episodes,
-                                   batch=batch, seed=9, hazard=hazard, dim=dim)
+                                   batch=batch, seed=9, hazard=hazard, dim=dim, fractal_levels=fractal)
     agent = learner.agent
     agent.cfg.dropout = p
     agent.model.cfg.dropout = p
@@ -874,6 +874,18 @@ def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, d
     for name, (s, e) in agent.flat.index.items():
         err = float((a['grad'][s:e] - b['grad'][s:e]).abs().max())
         assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cont,evo,p,T,levels,dim', [(False, True, 0.25, 70, 2, 64), (True, False, 0.1, 40, 3, 64),
+                                                     (False, False, 0.0, 130, 1, 48), (False, True, 0.25, 100, 2, 256)])
+def test_fractal_fused_train_step_matches_autograd(cont, evo, p, T, levels, dim):
+    """The hand-scheduled fractal learn step (xtrl_fractal_train_forward/backward: LayerNorm with
+    bias in the GEMM epilogues, causal running means as scans, dropout from the shared Philox
+    streams) against the reference-mode autograd step (FractalPolicyActorCritic.forward_train +
+    fused loss + loss.backward) on identical weights, minibatch and masks: loss within 1e-5
+    relative, every gradient within 1e-4 of the gradient scale."""
+    _fused_vs_autograd(cont, evo, False, p, T, depth=levels, episodes=8, batch=4, hazard=5, dim=dim, fractal=levels)
 
 
 # ----------------------------------------------------------------------------------------------
@@ -1044,6 +1056,12 @@ def test_c3_full_minibatch_fused_matches_reference_mode():
     gradients over 192 workgroups on the side stream — against the reference-mode autograd step on
     identical weights, minibatch and dropout masks."""
     _fused_vs_autograd(False, False, True, 0.25, 128, depth=4, episodes=128, batch=128, hazard=6, dim=256)
+
+
+def test_c5_full_minibatch_fractal_fused_matches_reference_mode():
+    """The C5 learn step at its bench minibatch (128 episodes x 128 steps, 4 levels, d 256, 4 x 16
+    heads, EPO genes, dropout 0.25): the fused fractal step against the reference-mode autograd step."""
+    _fused_vs_autograd(False, True, False, 0.25, 128, depth=4, episodes=128, batch=128, hazard=6, dim=256, fractal=4)
 
 
 def test_ema_schedule_and_model_copy_back_match_oracle():

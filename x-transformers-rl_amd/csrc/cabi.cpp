@@ -46,7 +46,8 @@ extern "C" int64_t xtrl_struct_size(const char* name) {
                {"XtrlDecodeDesc", sizeof(XtrlDecodeDesc)},   {"XtrlTrainLayer", sizeof(XtrlTrainLayer)},
                {"XtrlTrainDesc", sizeof(XtrlTrainDesc)},     {"XtrlBatchDesc", sizeof(XtrlBatchDesc)},
                {"XtrlLossDesc", sizeof(XtrlLossDesc)},       {"XtrlFractalLevel", sizeof(XtrlFractalLevel)},
-               {"XtrlFractalDesc", sizeof(XtrlFractalDesc)}};
+               {"XtrlFractalDesc", sizeof(XtrlFractalDesc)},     {"XtrlFractalTrainLevel", sizeof(XtrlFractalTrainLevel)},
+               {"XtrlFractalTrainDesc", sizeof(XtrlFractalTrainDesc)}};
   for (const auto& s : sizes)
     if (name && strcmp(name, s.name) == 0) return s.size;
   return -1;

@@ -49,7 +49,7 @@ __device__ __forceinline__ float f4c(const float4& v, int k) {
 // the row-vector epilogue applies when every row segment it reads or writes is a 16-byte aligned float4
 template <int EPI, bool RES>
 __device__ __forceinline__ bool epi_v4_ok(const GemmArgs& a, const float* C) {
-  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE), AUX2 = (EPI == EPI_DGATE);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE || EPI == EPI_MASK_POS), AUX2 = (EPI == EPI_DGATE);
   constexpr bool AOUT = (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE || EPI == EPI_DGATE);
   bool ok = (a.N & 3) == 0 && (a.ldc & 3) == 0 && al16(C);
   if constexpr (RES) ok = ok && (a.ldr & 3) == 0 && al16(a.R);
@@ -87,7 +87,7 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
   const bool acc_c = a.beta != 0.f;
   constexpr bool DROP = (EPI == EPI_GELU_DROP);
   constexpr bool SAVE = (EPI == EPI_GELU_DROP || EPI == EPI_SILU_SAVE);
-  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE), AUX2 = (EPI == EPI_DGATE);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE || EPI == EPI_MASK_POS), AUX2 = (EPI == EPI_DGATE);
   const int c4 = lane & 3;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -166,6 +166,7 @@ __device__ __forceinline__ void gemm_epilogue_v4(const GemmArgs& a, f32x16 (&acc
           float x = v[g][k];
           float aux_o = SAVE ? ax[g][k] : 0.f;
           if constexpr (EPI == EPI_MUL_AUX) x = x * f4c(x1[g], k);
+          if constexpr (EPI == EPI_MASK_POS) x = f4c(x1[g], k) > 0.f ? x : 0.f;
           if constexpr (EPI == EPI_DGATE) {
             const float sg = sigmoidf_(f4c(x2[g], k));
             aux_o = (x * f4c(x1[g], k)) * (1.0f - sg) * sg;
@@ -204,7 +205,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
   }
   const bool acc_c = a.beta != 0.f;
   constexpr bool DROP = (EPI == EPI_GELU_DROP);
-  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE);
+  constexpr bool AUX1 = (EPI == EPI_MUL_AUX || EPI == EPI_DGATE || EPI == EPI_MASK_POS);
   constexpr bool AUX2 = (EPI == EPI_DGATE);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -270,6 +271,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& a, f32x16 (&acc)[T
             }
           }
           if constexpr (EPI == EPI_MUL_AUX) v = v * x1[r];
+          if constexpr (EPI == EPI_MASK_POS) v = x1[r] > 0.f ? v : 0.f;
           if constexpr (EPI == EPI_DGATE) {
             const float sg = sigmoidf_(x2[r]);
             aux_o = (v * x1[r]) * (1.0f - sg) * sg;
@@ -771,9 +773,11 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
   if (!cok) gam = z4;
   const float inv_n = 1.0f / (float)N;
   if constexpr (EPI == EPI_RES_LN) {
-    float4 bia = z4;
+    float4 bia = z4, beta = z4, add2 = z4;
     if (a.bias) bia = ld4(a.bias);
-    if (!cok) bia = z4;
+    if (a.ln_b) beta = ld4(a.ln_b);
+    if (a.ln_b2) add2 = ld4(a.ln_b2);
+    if (!cok) bia = beta = add2 = z4;
     float4 v[RPW], r[RPW];
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr) {
@@ -792,13 +796,16 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       float4 dl = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
       if (!cok) dl = z4;
       const float rstd = 1.0f / sqrtf(wave_sum((dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w)) * inv_n + 1e-5f);
-      const float4 y = make_float4((dl.x * rstd) * gam.x, (dl.y * rstd) * gam.y, (dl.z * rstd) * gam.z,
-                                   (dl.w * rstd) * gam.w);
+      float4 y = make_float4((dl.x * rstd) * gam.x, (dl.y * rstd) * gam.y, (dl.z * rstd) * gam.z,
+                             (dl.w * rstd) * gam.w);
+      if (a.ln_b) y = make_float4(y.x + beta.x, y.y + beta.y, y.z + beta.z, y.w + beta.w);
       if (m < M) {
         if (cok) {
           *reinterpret_cast<float4*>(a.C + (int64_t)m * a.ldc + c) = x;
           *reinterpret_cast<float4*>(a.ln_y1 + (int64_t)m * a.ln_ld1 + c) = y;
-          if (a.ln_y2) *reinterpret_cast<float4*>(a.ln_y2 + (int64_t)m * a.ln_ld2 + c) = y;
+          if (a.ln_y2)
+            *reinterpret_cast<float4*>(a.ln_y2 + (int64_t)m * a.ln_ld2 + c) =
+                make_float4(y.x + add2.x, y.y + add2.y, y.z + add2.z, y.w + add2.w);
         }
         if (lane == 0) *reinterpret_cast<float2*>(a.ln_stats + 2 * (int64_t)m) = make_float2(mean, rstd);
       }
@@ -1359,7 +1366,8 @@ int ln_gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, bool vec, 
   const bool kt = a.K % 32 != 0, narrow = a.N <= 128;
   if (epi == EPI_RES_LN) {
     XTRL_REQUIRE(!trans_b && res && a.ln_y1 && a.ldr % 4 == 0 && a.ln_ld1 % 4 == 0 && (!a.ln_y2 || a.ln_ld2 % 4 == 0) &&
-                     (!a.bias || ((uintptr_t)a.bias & 15u) == 0),
+                     (!a.bias || ((uintptr_t)a.bias & 15u) == 0) && (!a.ln_b || ((uintptr_t)a.ln_b & 15u) == 0) &&
+                     (!a.ln_b2 || (a.ln_y2 && ((uintptr_t)a.ln_b2 & 15u) == 0)),
                  "gemm: residual + LayerNorm epilogue arguments");
     if (narrow) {
       if (kt) launch_ws<false, false, EPI_RES_LN, true, 128, 128, true>(a, s);
@@ -1471,7 +1479,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   XTRL_REQUIRE(!(a.gamma && trans_a), "gemm: LayerNorm prologue needs a row-major A");
   XTRL_REQUIRE(!((epi == EPI_GELU_DROP || epi == EPI_SILU_SAVE || epi == EPI_DGATE) && !a.aux_out),
                "gemm: epilogue %d needs aux_out", epi);
-  XTRL_REQUIRE(!((epi == EPI_MUL_AUX || epi == EPI_DGATE) && !a.aux_in),
+  XTRL_REQUIRE(!((epi == EPI_MUL_AUX || epi == EPI_DGATE || epi == EPI_MASK_POS) && !a.aux_in),
                "gemm: epilogue %d needs aux_in", epi);
   XTRL_REQUIRE(!(epi == EPI_DGATE && !a.aux_in2), "gemm: gate epilogue needs aux_in2");
   if (a.M == 0 || a.N == 0) return XTRL_OK;
@@ -1503,6 +1511,8 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   XG(0, 0, EPI_SILU_SAVE, false, false)
   // dgrad (B = weight used as [k][n]) with fused activation / dropout / gate backward
   XG(0, 1, EPI_NONE, false, false)
+  XG(0, 1, EPI_NONE, false, true)       // input gradient + a residual-path gradient (fractal post-norm blocks)
+  XG(0, 1, EPI_MASK_POS, false, false)  // input gradient through a ReLU (fractal final aggregation)
   XG(0, 1, EPI_MUL_AUX, false, false)
   XG(0, 1, EPI_DGATE, false, false)
   // wgrad (A = dY^T)
@@ -1586,6 +1596,10 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   if (deferred && (defer->n == kMaxSplitKJobs || defer->used + need(splits) > ws_floats)) {
     if (int rc = splitk_flush(*defer, s)) return rc;   // the queued partials are summed first
   }
+  // a split that is not queued reduces at once from the front of ws, where queued partials lie
+  // (and may accumulate into a dW a queued job also writes): sum the queue first
+  if (defer && !deferred && splits > 1 && defer->n > 0)
+    if (int rc = splitk_flush(*defer, s)) return rc;
   if (deferred) {
     ws += defer->used;
     ws_floats -= defer->used;

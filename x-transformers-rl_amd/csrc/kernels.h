@@ -27,6 +27,7 @@ enum GemmEpi : int {
   EPI_RES_LN = 9,      // C = v (+ bias) + R;  ln_y1 / ln_y2 = LN(C) * ln_g;  ln_stats[m] = (mean, rstd)
   EPI_LN_BWD = 10,     // g = v; xhat = (ln_x - mean) rstd; C = rstd (g ln_g - mean_n(g ln_g) - xhat
                        //   mean_n(g ln_g xhat)) + ln_dres;  ln_part[row tile][n] = sum_tile rows g xhat
+  EPI_MASK_POS = 11,   // C = aux_in > 0 ? v : 0        (dgrad through a ReLU whose output is aux_in)
 };
 
 struct GemmArgs {
@@ -60,6 +61,8 @@ struct GemmArgs {
   int xcd_remap = 0;              // 1: workgroup ids permuted so each XCD runs consecutive tiles
   // LayerNorm epilogues (EPI_RES_LN / EPI_LN_BWD)
   const float* ln_g = nullptr;    // gamma [N]
+  const float* ln_b = nullptr;    // RES_LN: beta [N] (nn.LayerNorm bias; x-transformers LayerNorm has none)
+  const float* ln_b2 = nullptr;   // RES_LN: ln_y2 = LN(C) * ln_g (+ ln_b) + ln_b2 (the next level's input)
   float* ln_y1 = nullptr; int ln_ld1 = 0;   // RES_LN: normalised rows (ln_y2 optional: a second copy)
   float* ln_y2 = nullptr; int ln_ld2 = 0;
   float* ln_stats = nullptr;      // [M][2] (mean, rstd): written by RES_LN, read by LN_BWD

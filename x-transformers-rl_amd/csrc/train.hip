@@ -154,21 +154,23 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
 // four issued together; small blocks so they co-reside with the weight-gradient GEMM workgroups of
 // the backward side stream: learn 125.3 -> 124.0 ms against 16-wave blocks): upstream gradient g = s1 * g1 + g2 (g2 optional),
 // dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)) (+ dres; dx may alias dres);
-// per-block partial d gamma = sum_rows g * xhat -> part[block][d]
+// per-block partial d gamma = sum_rows g * xhat -> part[block][d] (and, for nn.LayerNorm's bias,
+// d beta = sum_rows g -> part_b[block][d] when part_b is given)
 constexpr int LN_ROWS = 16, LN_WAVES = 4, LN_R = 4;   // 256-thread blocks fit beside a side-stream GEMM workgroup on its CU
 template <int DPL>
 __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2,
                                                           int ldg2, const float* x, const float* stats,
                                                           const float* gamma, const float* dres, float* dx,
-                                                          float* part, int T, int d) {
+                                                          float* part, float* part_b, int T, int d) {
   __shared__ float red[LN_WAVES][64 * DPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float gam[DPL], dg[DPL];
+  float gam[DPL], dg[DPL], db[DPL];
 #pragma unroll
   for (int k = 0; k < DPL; ++k) {
     const int c = lane + 64 * k;
     gam[k] = c < d ? gamma[c] : 0.f;
     dg[k] = 0.f;
+    db[k] = 0.f;
   }
   const int r0 = blockIdx.x * LN_ROWS;
   for (int rb = w * LN_R; rb < LN_ROWS; rb += LN_WAVES * LN_R) {
@@ -203,6 +205,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
         xh[k] = c < d ? (xv[q][k] - mu[q]) * rs[q] : 0.f;
         gm[k] = g[q][k] * gam[k];
         dg[k] += g[q][k] * xh[k];
+        db[k] += g[q][k];
         sa += gm[k];
         sb += gm[k] * xh[k];
       }
@@ -228,6 +231,17 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
 #pragma unroll
     for (int j = 0; j < LN_WAVES; ++j) v += red[j][c];
     part[(int64_t)blockIdx.x * d + c] = v;
+  }
+  if (!part_b) return;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < DPL; ++k) red[w][lane + 64 * k] = db[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 64 * LN_WAVES) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < LN_WAVES; ++j) v += red[j][c];
+    part_b[(int64_t)blockIdx.x * d + c] = v;
   }
 }
 
@@ -408,8 +422,8 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld
   for (int a = 0; a < MAXA; ++a) acc[a] = 0.f;
 #pragma unroll 4
   for (int r = r0; r < r1; ++r) {
-    const int p = prev[r], q = next[r];
-    const float x = g1[(int64_t)r * ld1 + c], y = g2[(int64_t)r * ld2 + c];
+    const int p = prev ? prev[r] : -1, q = next[r];   // (no prev: the next-action input only)
+    const float x = prev ? g1[(int64_t)r * ld1 + c] : 0.f, y = g2[(int64_t)r * ld2 + c];
 #pragma unroll
     for (int a = 0; a < MAXA; ++a) {
       if (a < A) {
@@ -505,6 +519,87 @@ __global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint32_t
   const int q = m & 3;
   const uint32_t w = q == 0 ? r.x : (q == 1 ? r.y : (q == 2 ? r.z : r.w));
   mask[i] = (uint8_t)(thresh == 0 || w >= thresh);
+}
+
+// ---- fractal learn step (fractal_rl.py:116-136, 274-346 made causal; xtrl_amd/fractal.py) -------
+// causal running mean over each episode's steps (the reference's sequence mean made causal)
+//   REV = 0: dst[e, t] = (sum_{s <= t} src[e, s]) / (t + 1)                       (x3.cumsum(1) / cnt)
+//   REV = 1: dst[e, s] = add[e, s] + sum_{t >= s} src[e, t] / (t + 1)            (its backward)
+// Block (episode e, 64 columns), CM_G groups of 64 threads each owning a contiguous range of steps:
+// pass 1 sums the range, the group totals are combined through LDS, pass 2 rescans the range from
+// the carried-in total (coalesced: a group reads 64 consecutive floats of a row per step)
+constexpr int CM_G = 16;
+template <int REV>
+__global__ __launch_bounds__(64 * CM_G) void k_causal_mean(const float* src, int lds, const float* add, int ldadd,
+                                                          float* dst, int ldd, int n, int d) {
+  __shared__ float tot[CM_G][64];
+  const int e = blockIdx.x, cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int per = (n + CM_G - 1) / CM_G, t0 = min(n, grp * per), t1 = min(n, t0 + per);
+  const bool ok = c < d;
+  const int64_t base = (int64_t)e * n;
+  float s = 0.f;
+  if (ok)
+    for (int t = t0; t < t1; ++t) {
+      const float v = src[(base + t) * lds + c];
+      s += REV ? v / (float)(t + 1) : v;
+    }
+  tot[grp][cl] = s;
+  __syncthreads();
+  float carry = 0.f;
+  if (REV) {
+    for (int j = CM_G - 1; j > grp; --j) carry += tot[j][cl];
+  } else {
+    for (int j = 0; j < grp; ++j) carry += tot[j][cl];
+  }
+  if (!ok) return;
+  if (REV) {
+    for (int t = t1 - 1; t >= t0; --t) {
+      carry += src[(base + t) * lds + c] / (float)(t + 1);
+      dst[(base + t) * ldd + c] = (add ? add[(base + t) * ldadd + c] : 0.f) + carry;
+    }
+  } else {
+    for (int t = t0; t < t1; ++t) {
+      carry += src[(base + t) * lds + c];
+      dst[(base + t) * ldd + c] = carry / (float)(t + 1);
+    }
+  }
+}
+
+// out[i] = a[i] + b[i]
+__global__ void k_vec_add(const float* a, const float* b, float* out, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+// dst[r][c] = alpha * a[r][c] + (b ? b[r][c] : 0)   (a row vector broadcast when lda == 0)
+__global__ void k_rows_axpb(const float* a, int lda, float alpha, const float* b, int ldb, float* dst, int ldd,
+                            int rows, int cols) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)rows * cols) return;
+  const int64_t r = i / cols;
+  const int c = (int)(i - r * cols);
+  float v = alpha * a[r * lda + c];
+  if (b) v += b[r * ldb + c];
+  dst[r * ldd + c] = v;
+}
+
+// SafeEmbedding of the next action (xtrl.py:181-195): out[r] = W[a_r] for 0 <= a_r < A, else 0
+__global__ void k_action_rows(const int32_t* act, const float* W, int A, float* out, int ldo, int rows, int d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)rows * d) return;
+  const int64_t r = i / d;
+  const int c = (int)(i - r * d), a = act[r];
+  out[r * ldo + c] = (a >= 0 && a < A) ? W[(int64_t)a * d + c] : 0.f;
+}
+
+// dst[r][c] = src[r / n][c]: one row per episode broadcast over its n steps (the gene embedding)
+__global__ void k_rows_bcast_ep(const float* src, float* dst, int ldd, int rows, int n, int d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)rows * d) return;
+  const int64_t r = i / d;
+  const int c = (int)(i - r * d);
+  dst[r * ldd + c] = src[(r / n) * d + c];
 }
 
 // ---- host helpers -----------------------------------------------------------------------------
@@ -673,15 +768,17 @@ int ln_fwd(const Ctx& c, const float* x, const float* gamma, float* y1, int ld1,
 }
 
 int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, int ldg2, const float* x,
-           const float* st, const float* gamma, const float* dres, float* dx, float* dgamma) {
+           const float* st, const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta = nullptr) {
   const int d = c.D->d, nb = (int)blocks(c.T, LN_ROWS);
-  XTRL_REQUIRE((int64_t)nb * d <= c.D->part_floats, "train: partial-sum workspace too small");
+  XTRL_REQUIRE((int64_t)nb * d * (dbeta ? 2 : 1) <= c.D->part_floats, "train: partial-sum workspace too small");
+  float* pb = dbeta ? c.D->part + (int64_t)nb * d : nullptr;
   const dim3 g(nb), bl(64 * LN_WAVES);
-  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
-  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
-  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
-  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, c.T, d);
+  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
+  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
+  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
+  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
   hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
+  if (dbeta) hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, pb, nb, d, dbeta);
   XTRL_LAUNCHED("train ln_bwd");
   return XTRL_OK;
 }
@@ -761,11 +858,80 @@ int validate(const XtrlTrainDesc* D) {
 
 }  // namespace
 
+// ---- the heads every policy body shares (xtrl.py:533-557, fractal_rl.py:586-619) -------------
+// input: ac_in = [embed | state embed (| latent embed)], ewa = [embed | next-action embed]
+int heads_forward(const Ctx& c) {
+  const XtrlTrainDesc* D = c.D;
+  const int T = c.T, d = D->d, ldp = d + 4;
+  const hipStream_t s = c.s;
+  int rc;
+  // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
+  if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
+                       nullptr, D->zp, ldp, d)))
+    return rc;
+  const int S1x2 = 2 * (D->S + 1);
+  if ((rc = linear_fwd(c, D->hp, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred, S1x2, T, S1x2, d, EPI_NONE)))
+    return rc;
+  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->hp + d, ldp, D->done, 1, T);
+  // actor | critic first layers in one GEMM, then the two output layers
+  if ((rc = linear_fwd(c, D->ac_in, D->in_dim, c.P(D->w_h1), c.P(D->b_h1), D->h1, 4 * d, T, 4 * d, D->in_dim,
+                       EPI_SILU_SAVE, nullptr, D->z1, 4 * d)))
+    return rc;
+  if ((rc = linear_fwd(c, D->h1, 4 * d, c.P(D->w_a2), c.P(D->b_a2), D->raw, D->n_out, T, D->n_out, 2 * d, EPI_NONE)))
+    return rc;
+  if ((rc = linear_fwd(c, D->h1 + 2 * d, 4 * d, c.P(D->w_c2), c.P(D->b_c2), D->values, D->B, T, D->B, 2 * d,
+                       EPI_NONE)))
+    return rc;
+  XTRL_LAUNCHED("train heads");
+  return XTRL_OK;
+}
+
+// heads backward -> dac (gradient of ac_in), dewa (of ewa); the weight gradients of the heads, the
+// state embedding and the gene conditioning (c: main stream, cw: weight-gradient stream)
+int heads_backward(const Ctx& c, const Ctx& cw, Fork& F) {
+  const XtrlTrainDesc* D = c.D;
+  const int T = c.T, d = D->d, ldp = d + 4, S1x2 = 2 * (D->S + 1);
+  const hipStream_t s = c.s;
+  int rc;
+  // ---- actor / critic heads
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
+  if ((rc = wgrad(cw, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d, c.G(D->b_c2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_MUL_AUX, D->z1,
+                         4 * d)))
+    return rc;
+  if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_MUL_AUX,
+                         D->z1 + 2 * d, 4 * d)))
+    return rc;
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
+  if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
+  // state embedding and gene conditioning
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
+  if (D->evolutionary) {
+    XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
+    hipLaunchKernelGGL(k_latent_grad, dim3(D->b, (d + 63) / 64), dim3(64 * LG_G), 0, s, D->dac, D->in_dim, 2 * d,
+                       D->b, D->n, d, D->part);
+    hipLaunchKernelGGL(k_latent_wgrad, dim3(blocks(d * (D->G + 1), 256)), dim3(256), 0, s, D->part, D->latent, D->b,
+                       d, D->G, c.G(D->w_lat), c.G(D->b_lat));
+    XTRL_LAUNCHED("train latent grad");
+  }
+  // ---- world-model heads
+  if ((rc = wgrad(cw, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
+  if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_MUL_AUX, D->zp, ldp))) return rc;
+  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);
+  if ((rc = F.fork())) return rc;
+  if ((rc = wgrad(cw, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
+  if ((rc = linear_dgrad(c, D->dzp, ldp, c.P(D->w_pd), D->dewa, 2 * d, T, d + 1, 2 * d, EPI_NONE))) return rc;
+  return XTRL_OK;
+}
+
 // ============================================================================================
 int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   if (int rc = validate(D)) return rc;
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4;
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff;
   int rc;
   // embeddings
   if (D->evolutionary) {
@@ -828,23 +994,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   // final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
   if (!fuse)
     if ((rc = ln_fwd(c, D->x_final, c.P(D->ln_final), D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final))) return rc;
-  // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
-  if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
-                       nullptr, D->zp, ldp, d)))
-    return rc;
-  const int S1x2 = 2 * (D->S + 1);
-  if ((rc = linear_fwd(c, D->hp, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred, S1x2, T, S1x2, d, EPI_NONE)))
-    return rc;
-  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->hp + d, ldp, D->done, 1, T);
-  // actor | critic first layers in one GEMM, then the two output layers
-  if ((rc = linear_fwd(c, D->ac_in, D->in_dim, c.P(D->w_h1), c.P(D->b_h1), D->h1, 4 * d, T, 4 * d, D->in_dim,
-                       EPI_SILU_SAVE, nullptr, D->z1, 4 * d)))
-    return rc;
-  if ((rc = linear_fwd(c, D->h1, 4 * d, c.P(D->w_a2), c.P(D->b_a2), D->raw, D->n_out, T, D->n_out, 2 * d, EPI_NONE)))
-    return rc;
-  if ((rc = linear_fwd(c, D->h1 + 2 * d, 4 * d, c.P(D->w_c2), c.P(D->b_c2), D->values, D->B, T, D->B, 2 * d,
-                       EPI_NONE)))
-    return rc;
+  if ((rc = heads_forward(c))) return rc;
   XTRL_LAUNCHED("train forward");
   return XTRL_OK;
 }
@@ -854,7 +1004,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   if (int rc = validate(D)) return rc;
   XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "train: missing loss gradients");
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, ldp = d + 4, S1x2 = 2 * (D->S + 1);
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff;
   int rc;
   SideStream& side = side_stream();
   const bool two = side.ok && side.ensure(side_events_needed(D->L));
@@ -880,37 +1030,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     ++bucket;
     return XTRL_OK;
   };
-  // ---- actor / critic heads
-  if ((rc = F.fork())) return rc;
-  if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
-  if ((rc = wgrad(cw, D->d_values, D->B, D->h1 + 2 * d, 4 * d, c.G(D->w_c2), T, D->B, 2 * d, c.G(D->b_c2)))) return rc;
-  if ((rc = linear_dgrad(c, D->d_raw, D->n_out, c.P(D->w_a2), D->dz1, 4 * d, T, D->n_out, 2 * d, EPI_MUL_AUX, D->z1,
-                         4 * d)))
-    return rc;
-  if ((rc = linear_dgrad(c, D->d_values, D->B, c.P(D->w_c2), D->dz1 + 2 * d, 4 * d, T, D->B, 2 * d, EPI_MUL_AUX,
-                         D->z1 + 2 * d, 4 * d)))
-    return rc;
-  if ((rc = F.fork())) return rc;
-  if ((rc = wgrad(cw, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
-  if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
-  // state embedding and gene conditioning
-  if ((rc = F.fork())) return rc;
-  if ((rc = wgrad(cw, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
-  if (D->evolutionary) {
-    XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
-    hipLaunchKernelGGL(k_latent_grad, dim3(D->b, (d + 63) / 64), dim3(64 * LG_G), 0, s, D->dac, D->in_dim, 2 * d,
-                       D->b, D->n, d, D->part);
-    hipLaunchKernelGGL(k_latent_wgrad, dim3(blocks(d * (D->G + 1), 256)), dim3(256), 0, s, D->part, D->latent, D->b,
-                       d, D->G, c.G(D->w_lat), c.G(D->b_lat));
-    XTRL_LAUNCHED("train latent grad");
-  }
-  // ---- world-model heads
-  if ((rc = wgrad(cw, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
-  if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_MUL_AUX, D->zp, ldp))) return rc;
-  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);
-  if ((rc = F.fork())) return rc;
-  if ((rc = wgrad(cw, D->dzp, ldp, D->ewa, 2 * d, c.G(D->w_pd), T, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
-  if ((rc = linear_dgrad(c, D->dzp, ldp, c.P(D->w_pd), D->dewa, 2 * d, T, d + 1, 2 * d, EPI_NONE))) return rc;
+  if ((rc = heads_backward(c, cw, F))) return rc;
   // action-embedding gradient of the next-action input (and, below, of the previous action)
   // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
   if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
@@ -1042,6 +1162,327 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   return XTRL_OK;
 }
 
+// ============================================================================================
+// Fractal policy body learn step (include/xtrl_hip.h XtrlFractalTrainDesc; the reference-mode
+// autograd forward it replaces: xtrl_amd/fractal.py FractalPolicyActorCritic.forward_train)
+namespace {
+int validate_fractal(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F) {
+  XTRL_REQUIRE(D && F && F->level && D->flat && D->grad, "fractal train: null descriptor / levels / parameters");
+  XTRL_REQUIRE(F->levels > 0 && D->b > 0 && D->n > 0 && D->d > 0 && D->H > 0 && D->dh > 0 && D->ff > 0,
+               "fractal train: bad sizes");
+  XTRL_REQUIRE(D->d % 4 == 0 && D->d <= 256 && (D->H * D->dh) % 4 == 0 && D->ff % 4 == 0,
+               "fractal train: needs d %% 4 == 0, d <= 256, H dh %% 4 == 0, ff %% 4 == 0 (d = %d)", D->d);
+  XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "fractal train: in_dim mismatch");
+  XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "fractal train: evolutionary needs latent buffers");
+  XTRL_REQUIRE(D->continuous ? D->next_action_f != nullptr : D->next_action != nullptr,
+               "fractal train: missing next actions");
+  XTRL_REQUIRE(D->continuous || D->A <= EMB_MAXA, "fractal train: %d discrete actions > %d unsupported", D->A, EMB_MAXA);
+  XTRL_REQUIRE(D->w_pin >= 0 && F->b_in >= 0 && F->g_init >= 0 && F->w_gu >= 0 && F->w_fa0 >= 0 && F->w_fa2 >= 0,
+               "fractal train: missing encoder parameters");
+  XTRL_REQUIRE(F->scale_embeds && F->le && F->bias0 && F->cat && F->hfa, "fractal train: missing buffers");
+  for (int l = 0; l < F->levels; ++l) {
+    const XtrlFractalTrainLevel& V = F->level[l];
+    XTRL_REQUIRE(V.w_qkv >= 0 && V.w_out >= 0 && V.w_gv >= 0 && V.w_go >= 0 && V.w_ff1 >= 0 && V.w_ff2 >= 0 &&
+                     V.w_proj >= 0 && V.ln1_w >= 0 && V.ln2_w >= 0 && V.ln3_w >= 0 && V.level_embed >= 0,
+                 "fractal train: level %d misses parameters", l);
+    XTRL_REQUIRE(V.xin && V.qkv && V.o && V.lse && V.s1 && V.x1 && V.st1 && V.g && V.gv && V.s2 && V.x2 && V.st2 &&
+                     V.h && V.u && V.s3 && V.x3 && V.st3 && V.mean,
+                 "fractal train: level %d misses activation buffers", l);
+  }
+  return XTRL_OK;
+}
+
+// x_out = A W^T (+ bias) + R; y1 = nn.LayerNorm(x_out) (weight, bias); y2 = y1 + b2 (optional): one launch
+int linear_res_ln_affine(const Ctx& c, const float* A, int lda, const float* W, int K, const float* bias,
+                         const float* R, float* x_out, const float* gamma, const float* beta, float* y1, float* st,
+                         float* y2 = nullptr, const float* b2 = nullptr) {
+  const int d = c.D->d;
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = x_out; g.ldc = d; g.M = c.T; g.N = d; g.K = K;
+  g.R = R; g.ldr = d; g.ln_g = gamma; g.ln_b = beta; g.ln_b2 = b2; g.ln_y1 = y1; g.ln_ld1 = d; g.ln_y2 = y2;
+  g.ln_ld2 = d; g.ln_stats = st;
+  return gemm_run(g, 0, 0, EPI_RES_LN, c.s);
+}
+
+// C = A W^T + bias + R with R's own leading dimension
+int linear_fwd_res(const Ctx& c, const float* A, int lda, const float* W, const float* bias, const float* R, int ldr,
+                   float* C, int ldc, int N, int K) {
+  GemmArgs g;
+  g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = C; g.ldc = ldc; g.M = c.T; g.N = N; g.K = K;
+  g.R = R; g.ldr = ldr;
+  return gemm_run(g, 0, 0, EPI_NONE, c.s);
+}
+
+// dX = dY W + R (R: a residual-path gradient, may alias dX)
+int dgrad_res(const Ctx& c, const float* dY, int ldy, const float* W, int N, int K, const float* R, int ldr, float* dX,
+              int ldx) {
+  GemmArgs g;
+  g.A = dY; g.lda = ldy; g.B = W; g.ldb = K; g.C = dX; g.ldc = ldx; g.M = c.T; g.N = K; g.K = N;
+  g.R = R; g.ldr = ldr;
+  return gemm_run(g, 0, 1, EPI_NONE, c.s);
+}
+
+AttnProblem fractal_attn(const Ctx& c, int level) {
+  const XtrlTrainDesc* D = c.D;
+  const int I = D->H * D->dh;
+  AttnProblem p{};
+  p.b = D->b; p.H = D->H; p.n = D->n; p.dh = D->dh; p.lens = D->lens; p.scale = D->attn_scale;
+  p.dropout = D->dropout; p.seed = D->seed; p.offset = D->attn_offset; p.sub = (uint32_t)level;
+  p.in = attn_layout_tokens(D->n, 3 * I, D->dh);
+  p.out = attn_layout_tokens(D->n, I, D->dh);
+  p.grad = attn_layout_tokens(D->n, 3 * I, D->dh);
+  p.gate = p.grad;
+  return p;
+}
+
+int causal_mean(const Ctx& c, const float* src, int lds, const float* add, int ldadd, float* dst, int ldd, bool rev) {
+  const XtrlTrainDesc* D = c.D;
+  const dim3 g(D->b, (D->d + 63) / 64), bl(64 * CM_G);
+  if (rev) hipLaunchKernelGGL(k_causal_mean<1>, g, bl, 0, c.s, src, lds, add, ldadd, dst, ldd, D->n, D->d);
+  else hipLaunchKernelGGL(k_causal_mean<0>, g, bl, 0, c.s, src, lds, add, ldadd, dst, ldd, D->n, D->d);
+  XTRL_LAUNCHED("fractal causal_mean");
+  return XTRL_OK;
+}
+
+int rows_axpb(const Ctx& c, const float* a, int lda, float alpha, const float* b, int ldb, float* dst, int ldd, int rows,
+              int cols) {
+  hipLaunchKernelGGL(k_rows_axpb, dim3(blocks((int64_t)rows * cols, 256)), dim3(256), 0, c.s, a, lda, alpha, b, ldb, dst,
+                     ldd, rows, cols);
+  XTRL_LAUNCHED("fractal rows_axpb");
+  return XTRL_OK;
+}
+}  // namespace
+
+int fractal_train_forward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F, hipStream_t s) {
+  if (int rc = validate_fractal(D, F)) return rc;
+  const Ctx c{D, s, D->b * D->n};
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels, S = D->S, ldcat = (Lv + 1) * d;
+  int rc;
+  // level embeddings le[l] = level_embeds[l] + scale_embeds[l] (level_embeds: one [levels][d]
+  // parameter, level 0's offset its base) and the level-0 input bias b_in + le[0]
+  hipLaunchKernelGGL(k_vec_add, dim3(blocks(Lv * d, 256)), dim3(256), 0, s, c.P(F->level[0].level_embed),
+                     F->scale_embeds, F->le, Lv * d);
+  hipLaunchKernelGGL(k_vec_add, dim3(blocks(d, 256)), dim3(256), 0, s, c.P(F->b_in), F->le, F->bias0, d);
+  XTRL_LAUNCHED("fractal embeds");
+  // x_in,0 = input_embed(state) + le[0];  g_0 = global_state_init on every row
+  if ((rc = linear_fwd(c, D->swr, S + 1, c.P(D->w_pin), F->bias0, F->level[0].xin, d, T, d, S, EPI_NONE))) return rc;
+  if ((rc = rows_axpb(c, c.P(F->g_init), 0, 1.f, nullptr, 0, F->level[0].g, d, T, d))) return rc;
+  // heads' inputs besides the features: to_state_embed(state) -> ac_in[:, d:2d], the gene embedding
+  // broadcast -> ac_in[:, 2d:], the next action's embedding -> ewa[:, d:]
+  if ((rc = linear_fwd(c, D->swr, S + 1, c.P(D->w_se), c.P(D->b_se), D->ac_in + d, D->in_dim, T, d, S, EPI_NONE)))
+    return rc;
+  if (D->evolutionary) {
+    hipLaunchKernelGGL(k_latent_embed, dim3(blocks(D->b * d, 256)), dim3(256), 0, s, D->latent, c.P(D->w_lat),
+                       c.P(D->b_lat), D->lat_e, D->b, D->G, d);
+    hipLaunchKernelGGL(k_rows_bcast_ep, dim3(blocks((int64_t)T * d, 256)), dim3(256), 0, s, D->lat_e, D->ac_in + 2 * d,
+                       D->in_dim, T, D->n, d);
+  }
+  if (D->continuous) {
+    if ((rc = linear_fwd(c, D->next_action_f, D->A, c.P(D->act_emb), c.P(D->act_emb_b), D->ewa + d, 2 * d, T, d, D->A,
+                         EPI_NONE)))
+      return rc;
+  } else {
+    hipLaunchKernelGGL(k_action_rows, dim3(blocks((int64_t)T * d, 256)), dim3(256), 0, s, D->next_action,
+                       c.P(D->act_emb), D->A, D->ewa + d, 2 * d, T, d);
+  }
+  XTRL_LAUNCHED("fractal inputs");
+  for (int l = 0; l < Lv; ++l) {
+    const XtrlFractalTrainLevel& V = F->level[l];
+    // self-attention: q | k | v (adjacent weights, one GEMM), causal flash attention with dropout
+    if ((rc = linear_fwd(c, V.xin, d, c.P(V.w_qkv), nullptr, V.qkv, 3 * I, T, 3 * I, d, EPI_NONE))) return rc;
+    const AttnProblem ap = fractal_attn(c, l);
+    if ((rc = attn_fwd_ex(ap, V.qkv, V.qkv + I, V.qkv + 2 * I, V.o, V.lse, nullptr, nullptr, s))) return rc;
+    // s1 = x_in + o W_out^T, x1 = norm1(s1)
+    if ((rc = linear_res_ln_affine(c, V.o, I, c.P(V.w_out), I, nullptr, V.xin, V.s1, c.P(V.ln1_w), c.P(V.ln1_b), V.x1,
+                                   V.st1)))
+      return rc;
+    // cross-attention to the one-token global state (softmax over one key == 1): s2 = x1 + (g W_gv^T) W_go^T
+    if ((rc = linear_fwd(c, V.g, d, c.P(V.w_gv), nullptr, V.gv, I, T, I, d, EPI_NONE))) return rc;
+    if ((rc = linear_res_ln_affine(c, V.gv, I, c.P(V.w_go), I, nullptr, V.x1, V.s2, c.P(V.ln2_w), c.P(V.ln2_b), V.x2,
+                                   V.st2)))
+      return rc;
+    // feed-forward: h = drop(gelu(x2 W1^T + b1)); s3 = x2 + h W2^T + b2, x3 = norm3(s3) (and the next
+    // level's input x3 + le[l + 1] from the same epilogue)
+    if ((rc = linear_fwd(c, V.x2, d, c.P(V.w_ff1), c.P(V.b_ff1), V.h, ff, T, ff, d, EPI_GELU_DROP, nullptr, V.u, ff,
+                         1 << 30, 0, D->ff_offset, (uint32_t)l)))
+      return rc;
+    const bool last = l + 1 == Lv;
+    if ((rc = linear_res_ln_affine(c, V.h, ff, c.P(V.w_ff2), ff, c.P(V.b_ff2), V.x2, V.s3, c.P(V.ln3_w), c.P(V.ln3_b),
+                                   V.x3, V.st3, last ? nullptr : F->level[l + 1].xin, last ? nullptr : F->le + (l + 1) * d)))
+      return rc;
+    // causal running mean; level projection into cat[:, l d:]; g <- g + mean W_gu^T + b_gu
+    if ((rc = causal_mean(c, V.x3, d, nullptr, 0, V.mean, d, false))) return rc;
+    if ((rc = linear_fwd(c, V.mean, d, c.P(V.w_proj), c.P(V.b_proj), F->cat + l * d, ldcat, T, d, d, EPI_NONE))) return rc;
+    if ((rc = linear_fwd_res(c, V.mean, d, c.P(F->w_gu), c.P(F->b_gu), V.g, d, last ? F->cat + Lv * d : F->level[l + 1].g,
+                             last ? ldcat : d, d, d)))
+      return rc;
+  }
+  // features = final_aggregation(cat) -> ac_in[:, :d] and ewa[:, :d]
+  if ((rc = linear_fwd(c, F->cat, ldcat, c.P(F->w_fa0), c.P(F->b_fa0), F->hfa, 2 * d, T, 2 * d, ldcat, EPI_RELU))) return rc;
+  if ((rc = linear_fwd(c, F->hfa, 2 * d, c.P(F->w_fa2), c.P(F->b_fa2), D->ac_in, D->in_dim, T, d, 2 * d, EPI_NONE)))
+    return rc;
+  if ((rc = rows_axpb(c, D->ac_in, D->in_dim, 1.f, nullptr, 0, D->ewa, 2 * d, T, d))) return rc;
+  if ((rc = heads_forward(c))) return rc;
+  XTRL_LAUNCHED("fractal train forward");
+  return XTRL_OK;
+}
+
+// events one fractal backward takes (forks + marks): heads 4, action embedding 1, aggregation 1 + 2,
+// per level 7 forks + 7 marks, input embedding 1 + 1, final join 1
+constexpr size_t fractal_events_needed(int Lv) { return 14 * (size_t)Lv + 11; }
+
+int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F, hipStream_t s) {
+  if (int rc = validate_fractal(D, F)) return rc;
+  XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "fractal train: missing loss gradients");
+  XTRL_REQUIRE(F->dxa && F->dxb && F->ds && F->dmean && F->dga && F->dgb && F->dgv && F->dz && F->dqkv && F->dob &&
+                   F->dcat && F->dhfa,
+               "fractal train: missing backward scratch");
+  const Ctx c{D, s, D->b * D->n};
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels, S = D->S, ldcat = (Lv + 1) * d;
+  const int64_t Td = (int64_t)T * d;
+  int rc;
+  SideStream& side = side_stream();
+  const bool two = side.ok && side.ensure(fractal_events_needed(Lv));
+  Fork Fk{s, side.s, two ? &side : nullptr};
+  static const bool defer = [] {
+    const char* e = getenv("XTRL_SPLITK_DEFER");
+    return !(e && atoi(e) == 0);
+  }();
+  SplitKQueue skq;
+  const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
+  if ((rc = heads_backward(c, cw, Fk))) return rc;
+  // d features = frac * dac[:, :d] + dewa[:, :d]  (frac_gradient: the actor / critic share scaled)
+  float* dfeat = F->ds + 3 * Td;   // ds holds 4 [T][d] planes: LN1 / LN2 / LN3 input gradients, d features
+  if ((rc = rows_axpb(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, dfeat, d, T, d))) return rc;
+  // next-action embedding
+  if (D->continuous) {
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, D->dewa + d, 2 * d, D->next_action_f, D->A, c.G(D->act_emb), T, d, D->A, c.G(D->act_emb_b))))
+      return rc;
+  } else {
+    int chunks = (int)std::min<int64_t>(std::min(1024, std::max(1, T / 16)),
+                                        std::max<int64_t>(1, D->part_floats / ((int64_t)D->A * d)));
+    const int chunk_rows = (T + chunks - 1) / chunks;
+    chunks = (T + chunk_rows - 1) / chunk_rows;
+    XTRL_REQUIRE((int64_t)chunks * D->A * d <= D->part_floats, "fractal train: partial-sum workspace too small");
+    const dim3 eg(blocks(d, 256), chunks);
+    if (D->A <= 4)
+      hipLaunchKernelGGL(k_embed_grad_part<4>, eg, dim3(256), 0, s, nullptr, 0, nullptr, D->dewa + d, 2 * d,
+                         D->next_action, T, d, D->A, chunk_rows, D->part);
+    else if (D->A <= 8)
+      hipLaunchKernelGGL(k_embed_grad_part<8>, eg, dim3(256), 0, s, nullptr, 0, nullptr, D->dewa + d, 2 * d,
+                         D->next_action, T, d, D->A, chunk_rows, D->part);
+    else
+      hipLaunchKernelGGL(k_embed_grad_part<EMB_MAXA>, eg, dim3(256), 0, s, nullptr, 0, nullptr, D->dewa + d, 2 * d,
+                         D->next_action, T, d, D->A, chunk_rows, D->part);
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(D->A * d, CS_COLS)), dim3(64 * CS_WAVES), 0, s, D->part, chunks,
+                       D->A * d, c.G(D->act_emb));
+    XTRL_LAUNCHED("fractal action embed grad");
+    if ((rc = Fk.fork())) return rc;   // (keeps the event count independent of the action kind)
+  }
+  // final aggregation: feat = hfa W_fa2^T + b; hfa = ReLU(cat W_fa0^T + b)
+  if ((rc = wgrad(cw, dfeat, d, F->hfa, 2 * d, c.G(F->w_fa2), T, d, 2 * d, c.G(F->b_fa2)))) return rc;
+  Fk.mark();
+  if ((rc = linear_dgrad(c, dfeat, d, c.P(F->w_fa2), F->dhfa, 2 * d, T, d, 2 * d, EPI_MASK_POS, F->hfa, 2 * d))) return rc;
+  if ((rc = Fk.fork())) return rc;
+  if ((rc = wgrad(cw, F->dhfa, 2 * d, F->cat, ldcat, c.G(F->w_fa0), T, 2 * d, ldcat, c.G(F->b_fa0)))) return rc;
+  Fk.mark();
+  if ((rc = linear_dgrad(c, F->dhfa, 2 * d, c.P(F->w_fa0), F->dcat, ldcat, T, 2 * d, ldcat, EPI_NONE))) return rc;
+  // levels, last to first.  dgn: gradient of g_{l+1} (the final g: cat's last d columns); dxn:
+  // gradient of x3_l from level l + 1's input (none for the last level).  Scratch a side-stream
+  // weight gradient still reads is not overwritten before its event: the LN planes of ds, dz, dgv and
+  // dqkv by the next (shallower) level, the dg buffers (alternating) two levels on.
+  const float* dgn = F->dcat + Lv * d;
+  int lddgn = ldcat;
+  const float* dxn = nullptr;
+  float* ds1 = F->ds;
+  float* ds2 = F->ds + Td;
+  float* ds3 = F->ds + 2 * Td;
+  hipEvent_t e_gu_prev = nullptr, e_ff2 = nullptr, e_ff1 = nullptr, e_go = nullptr,
+             e_gv = nullptr, e_out = nullptr, e_qkv = nullptr;
+  for (int l = Lv - 1; l >= 0; --l) {
+    const XtrlFractalTrainLevel& V = F->level[l];
+    // g_{l+1} = g_l + mean W_gu^T + b_gu;  cat[:, l d:] = mean W_p^T + b_p
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, dgn, lddgn, V.mean, d, c.G(F->w_gu), T, d, d, c.G(F->b_gu)))) return rc;
+    if ((rc = wgrad(cw, F->dcat + l * d, ldcat, V.mean, d, c.G(V.w_proj), T, d, d, c.G(V.b_proj)))) return rc;
+    const hipEvent_t e_gu = Fk.mark();
+    if ((rc = linear_dgrad(c, dgn, lddgn, c.P(F->w_gu), F->dmean, d, T, d, d, EPI_NONE))) return rc;
+    if ((rc = dgrad_res(c, F->dcat + l * d, ldcat, c.P(V.w_proj), d, d, F->dmean, d, F->dmean, d))) return rc;
+    // mean = causal running mean of x3: dx3 = dxn + reverse scan of dmean / (t + 1)
+    if ((rc = causal_mean(c, F->dmean, d, dxn, d, F->dxa, d, true))) return rc;
+    // norm3 backward -> ds3 (d gamma, d beta)
+    if ((rc = Fk.wait(e_ff2))) return rc;
+    if ((rc = ln_bwd(c, F->dxa, d, 1.f, nullptr, 0, V.s3, V.st3, c.P(V.ln3_w), nullptr, ds3, c.G(V.ln3_w),
+                     c.G(V.ln3_b))))
+      return rc;
+    // feed-forward: s3 = x2 + h W2^T + b2
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, ds3, d, V.h, ff, c.G(V.w_ff2), T, d, ff, c.G(V.b_ff2)))) return rc;
+    e_ff2 = Fk.mark();
+    if ((rc = Fk.wait(e_ff1))) return rc;
+    if ((rc = linear_dgrad(c, ds3, d, c.P(V.w_ff2), F->dz, ff, T, d, ff, EPI_MUL_AUX, V.u, ff))) return rc;
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, F->dz, ff, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
+    e_ff1 = Fk.mark();
+    // dx2 = ds3 + dz W1
+    if ((rc = dgrad_res(c, F->dz, ff, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
+    // norm2 backward -> ds2; cross-attention: s2 = x1 + gv W_go^T, gv = g W_gv^T
+    if ((rc = Fk.wait(e_go))) return rc;
+    if ((rc = ln_bwd(c, F->dxb, d, 1.f, nullptr, 0, V.s2, V.st2, c.P(V.ln2_w), nullptr, ds2, c.G(V.ln2_w),
+                     c.G(V.ln2_b))))
+      return rc;
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, ds2, d, V.gv, I, c.G(V.w_go), T, d, I))) return rc;
+    e_go = Fk.mark();
+    if ((rc = Fk.wait(e_gv))) return rc;
+    if ((rc = linear_dgrad(c, ds2, d, c.P(V.w_go), F->dgv, I, T, d, I, EPI_NONE))) return rc;
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, F->dgv, I, V.g, d, c.G(V.w_gv), T, I, d))) return rc;
+    e_gv = Fk.mark();
+    // dg_l = dg_{l+1} + dgv W_gv into the dg buffer that held dg_{l+2}, which level l + 1's
+    // global-update weight gradient (event e_gu_prev) was the last to read
+    float* dgc = ((Lv - 1 - l) & 1) ? F->dgb : F->dga;
+    if ((rc = Fk.wait(e_gu_prev))) return rc;
+    if ((rc = dgrad_res(c, F->dgv, I, c.P(V.w_gv), I, d, dgn, lddgn, dgc, d))) return rc;
+    // norm1 backward (its input gradient: ds2, the residual path of s2) -> ds1
+    if ((rc = Fk.wait(e_out))) return rc;
+    if ((rc = ln_bwd(c, ds2, d, 1.f, nullptr, 0, V.s1, V.st1, c.P(V.ln1_w), nullptr, ds1, c.G(V.ln1_w), c.G(V.ln1_b))))
+      return rc;
+    // self-attention: s1 = x_in + o W_out^T
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, ds1, d, V.o, I, c.G(V.w_out), T, d, I))) return rc;
+    e_out = Fk.mark();
+    if ((rc = linear_dgrad(c, ds1, d, c.P(V.w_out), F->dob, I, T, d, I, EPI_NONE))) return rc;
+    if ((rc = Fk.wait(e_qkv))) return rc;
+    const AttnProblem ap = fractal_attn(c, l);
+    if ((rc = attn_bwd_ex(ap, V.qkv, V.qkv + I, V.qkv + 2 * I, V.o, V.lse, F->dob, F->dqkv, F->dqkv + I, F->dqkv + 2 * I,
+                          D->delta, s)))
+      return rc;
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, F->dqkv, 3 * I, V.xin, d, c.G(V.w_qkv), T, 3 * I, d))) return rc;
+    e_qkv = Fk.mark();
+    // d x_in = ds1 + dqkv W_qkv; the level embedding's gradient is its column sum
+    if ((rc = dgrad_res(c, F->dqkv, 3 * I, c.P(V.w_qkv), 3 * I, d, ds1, d, F->dxa, d))) return rc;
+    if ((rc = colsum(c, F->dxa, d, T, d, c.G(V.level_embed)))) return rc;
+    dxn = F->dxa;
+    dgn = dgc;
+    lddgn = d;
+    e_gu_prev = e_gu;
+  }
+  // input embedding (x_in,0 = state W_in^T + b_in + le[0]) and global_state_init (g_0 on every row)
+  if ((rc = Fk.fork())) return rc;
+  if ((rc = wgrad(cw, F->dxa, d, D->swr, S + 1, c.G(D->w_pin), T, d, S, c.G(F->b_in)))) return rc;
+  Fk.mark();
+  if ((rc = colsum(c, dgn, lddgn, T, d, c.G(F->g_init)))) return rc;
+  if ((rc = splitk_flush(skq, cw.s))) return rc;
+  if ((rc = Fk.wait(Fk.mark()))) return rc;
+  XTRL_REQUIRE(!Fk.failed, "fractal train: side-stream event record failed");
+  XTRL_REQUIRE(!Fk.on() || (size_t)Fk.next == fractal_events_needed(Lv), "fractal train: side events %d != %d", Fk.next,
+               (int)fractal_events_needed(Lv));
+  return XTRL_OK;
+}
+
 }  // namespace xtrl
 
 extern "C" int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream) {
@@ -1050,6 +1491,14 @@ extern "C" int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream) {
 
 extern "C" int xtrl_train_backward(const XtrlTrainDesc* desc, void* stream) {
   return xtrl::train_backward(desc, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_fractal_train_forward(const XtrlTrainDesc* base, const XtrlFractalTrainDesc* f, void* stream) {
+  return xtrl::fractal_train_forward(base, f, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_fractal_train_backward(const XtrlTrainDesc* base, const XtrlFractalTrainDesc* f, void* stream) {
+  return xtrl::fractal_train_backward(base, f, xtrl::as_stream(stream));
 }
 
 extern "C" int64_t xtrl_train_part_floats(int T, int b, int d, int A) {

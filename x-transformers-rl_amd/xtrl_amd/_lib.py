@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -98,6 +98,21 @@ class TrainDesc(C.Structure):
                    ('grad_events', C.POINTER(C.c_void_p))])
 
 
+class FractalTrainLevel(C.Structure):
+    _fields_ = ([(n, I64) for n in ('w_qkv', 'w_out', 'w_gv', 'w_go', 'ln1_w', 'ln1_b', 'ln2_w', 'ln2_b', 'ln3_w',
+                                    'ln3_b', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2', 'w_proj', 'b_proj', 'level_embed')]
+                + [(n, P) for n in ('xin', 'qkv', 'o', 'lse', 's1', 'x1', 'st1', 'g', 'gv', 's2', 'x2', 'st2', 'h', 'u',
+                                    's3', 'x3', 'st3', 'mean')])
+
+
+class FractalTrainDesc(C.Structure):
+    _fields_ = ([('levels', I32)]
+                + [(n, I64) for n in ('b_in', 'g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2')]
+                + [(n, P) for n in ('scale_embeds', 'le', 'bias0', 'cat', 'hfa', 'dxa', 'dxb', 'ds', 'dmean',
+                                    'dga', 'dgb', 'dgv', 'dz', 'dqkv', 'dob', 'dcat', 'dhfa')]
+                + [('level', C.POINTER(FractalTrainLevel))])
+
+
 class BatchDesc(C.Structure):
     _fields_ = ([(n, I32) for n in ('N', 'Tmax', 'n', 'b', 'S', 'A', 'B', 'continuous')]
                 + [(n, P) for n in ('states', 'actions', 'actions_f', 'rewards', 'logp', 'bounds', 'values', 'returns',
@@ -150,11 +165,14 @@ SIGNATURES = {
     'xtrl_rng_uniform': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_rng_normal': (F32, [U64, U32, U32, U32, U32, U32]),
     'xtrl_source_hash': (C.c_char_p, []),
+    'xtrl_fractal_train_forward': (I32, [C.POINTER(TrainDesc), C.POINTER(FractalTrainDesc), P]),
+    'xtrl_fractal_train_backward': (I32, [C.POINTER(TrainDesc), C.POINTER(FractalTrainDesc), P]),
 }
 
 STRUCTS = {'XtrlDecodeLayer': DecodeLayer, 'XtrlRngState': RngState, 'XtrlDecodeDesc': DecodeDesc,
            'XtrlTrainLayer': TrainLayer, 'XtrlTrainDesc': TrainDesc, 'XtrlBatchDesc': BatchDesc,
-           'XtrlLossDesc': LossDesc, 'XtrlFractalLevel': FractalLevel, 'XtrlFractalDesc': FractalDesc}
+           'XtrlLossDesc': LossDesc, 'XtrlFractalLevel': FractalLevel, 'XtrlFractalDesc': FractalDesc,
+           'XtrlFractalTrainLevel': FractalTrainLevel, 'XtrlFractalTrainDesc': FractalTrainDesc}
 
 _lib = None
 

@@ -325,13 +325,41 @@ class FractalPolicyActorCritic(FractalWorldModelActorCritic):
     def hl_value(self, logits):
         return (logits.softmax(dim=-1) * self.hl_centers).sum(-1)
 
+    def block_prefix(self, li):
+        """Parameter-name prefix of the block level ``li`` runs (FractalEncoder.get_fractal_block)."""
+        enc = self.fractal_encoder
+        if enc.share_weights:
+            return 'fractal_encoder.fractal_block.'
+        if enc.use_hypernetwork:
+            return 'fractal_encoder.base_block.'
+        return f'fractal_encoder.fractal_blocks.{li}.'
+
     def flat_order(self):
-        """Every parameter once; groups whose size is a multiple of 4 floats first (16-byte aligned
-        GEMM weights)."""
+        """Every parameter once.  Weights used as one GEMM operand by the fused learn step
+        (train.FractalTrainStep) are adjacent: each block's to_q | to_k | to_v, the actor | critic first
+        layers, to_pred.0 | to_pred_done.0 (weights and biases); groups whose size is not a multiple
+        of 4 floats go last, so every GEMM weight starts 16-byte aligned."""
         params = dict(self.named_parameters())
-        names = list(params)
-        names.sort(key=lambda n: params[n].numel() % 4 != 0)
-        return names
+        taken, groups = set(), []
+
+        def grp(names):
+            taken.update(names)
+            groups.append(list(names))
+
+        grp(['action_head.0.weight', 'critic_head.0.weight'])
+        grp(['action_head.0.bias', 'critic_head.0.bias'])
+        grp(['to_pred.0.weight', 'to_pred_done.0.weight'])
+        grp(['to_pred.0.bias', 'to_pred_done.0.bias'])
+        for li in range(self.levels):
+            pre = self.block_prefix(li) + 'self_attn.'
+            if pre + 'to_q.weight' not in taken:
+                grp([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight'])
+        for n in params:
+            if n not in taken:
+                grp([n])
+        size = lambda g: sum(params[n].numel() for n in g)
+        groups = [g for g in groups if size(g) % 4 == 0] + [g for g in groups if size(g) % 4]
+        return [n for g in groups for n in g]
 
     def bind_flat(self, flat, ws):
         self._flat, self._ws = flat, ws

@@ -123,7 +123,6 @@ class Agent(nn.Module):
                                           'set attn_gate_values / add_value_residual to False')
             levels = int(fractal_levels or c.depth)
             self.model = FractalPolicyActorCritic(c, levels).to(dev)
-            fused_learn = False   # the fused learn step (train.FusedTrainStep) is the decoder's
         elif policy_body == 'decoder':
             self.model = WorldModelActorCritic(c).to(dev)
         else:
@@ -445,9 +444,10 @@ class Agent(nn.Module):
         """The fused learn step, with activation buffers for up to (batch_size, n) minibatches."""
         ts = self._train_step
         if ts is None or b > ts.b_max or n > ts.n_max:
-            from .train import FusedTrainStep
-            self._train_step = ts = FusedTrainStep(self.model, self.flat, self.gemm_ws, max(b, self.batch_size),
-                                                   max(n, ts.n_max if ts is not None else 0))
+            from .train import FractalTrainStep, FusedTrainStep
+            cls = FractalTrainStep if self.policy_body == 'fractal' else FusedTrainStep
+            self._train_step = ts = cls(self.model, self.flat, self.gemm_ws, max(b, self.batch_size),
+                                        max(n, ts.n_max if ts is not None else 0))
         return ts
 
     def pop_logs(self):

@@ -16,6 +16,33 @@ from . import _lib as L
 from .params import FlatParams
 
 
+def _off(flat, name):
+    return flat.index[name][0] if name in flat.index else -1
+
+
+def _span_off(flat, names):
+    flat.span(names)   # asserts adjacency
+    return flat.index[names[0]][0]
+
+
+def _heads_desc(D, c, flat):
+    """Offsets of the heads every policy body shares (xtrl.py:533-557, fractal_rl.py:586-619)."""
+    off = lambda n: _off(flat, n)
+    if c.continuous:
+        D.act_emb, D.act_emb_b = off('action_embeds.weight'), off('action_embeds.bias')
+    else:
+        D.act_emb, D.act_emb_b = off('action_embeds.embed.weight'), -1
+    D.reward_embed, D.w_se, D.b_se = off('reward_embed'), off('to_state_embed.weight'), off('to_state_embed.bias')
+    D.w_pd = _span_off(flat, ['to_pred.0.weight', 'to_pred_done.0.weight'])
+    D.b_pd = _span_off(flat, ['to_pred.0.bias', 'to_pred_done.0.bias'])
+    D.w_pred2, D.b_pred2 = off('to_pred.2.weight'), off('to_pred.2.bias')
+    D.w_lat, D.b_lat = off('latent_to_embed.weight'), off('latent_to_embed.bias')
+    D.w_h1 = _span_off(flat, ['action_head.0.weight', 'critic_head.0.weight'])
+    D.b_h1 = _span_off(flat, ['action_head.0.bias', 'critic_head.0.bias'])
+    D.w_a2, D.b_a2 = off('action_head.2.weight'), off('action_head.2.bias')
+    D.w_c2, D.b_c2 = off('critic_head.2.weight'), off('critic_head.2.bias')
+
+
 class FusedTrainStep:
     def __init__(self, model, flat: FlatParams, ws: torch.Tensor, b_max: int, n_max: int):
         c = model.cfg
@@ -93,20 +120,8 @@ class FusedTrainStep:
         D.frac_head_grad, D.attn_scale = float(c.frac_head_grad), float(dh ** -0.5)
         D.flat, D.grad = flat.flat.data_ptr(), flat.grad.data_ptr()
         D.w_pin = off('transformer.project_in.weight')
-        if c.continuous:
-            D.act_emb, D.act_emb_b = off('action_embeds.weight'), off('action_embeds.bias')
-        else:
-            D.act_emb, D.act_emb_b = off('action_embeds.embed.weight'), -1
-        D.reward_embed, D.w_se, D.b_se = off('reward_embed'), off('to_state_embed.weight'), off('to_state_embed.bias')
+        _heads_desc(D, c, flat)
         D.ln_final = off('transformer.attn_layers.final_norm.gamma')
-        D.w_pd = span_off(['to_pred.0.weight', 'to_pred_done.0.weight'])
-        D.b_pd = span_off(['to_pred.0.bias', 'to_pred_done.0.bias'])
-        D.w_pred2, D.b_pred2 = off('to_pred.2.weight'), off('to_pred.2.bias')
-        D.w_lat, D.b_lat = off('latent_to_embed.weight'), off('latent_to_embed.bias')
-        D.w_h1 = span_off(['action_head.0.weight', 'critic_head.0.weight'])
-        D.b_h1 = span_off(['action_head.0.bias', 'critic_head.0.bias'])
-        D.w_a2, D.b_a2 = off('action_head.2.weight'), off('action_head.2.bias')
-        D.w_c2, D.b_c2 = off('critic_head.2.weight'), off('critic_head.2.bias')
         D.inv_freq = self.inv_freq.data_ptr()
         for k, t in self.buf.items():
             setattr(D, k, t.data_ptr())
@@ -121,6 +136,13 @@ class FusedTrainStep:
         """swr [b][n][S+1] normalised states | previous reward; actions [b][n] int32 (discrete) or
         [b][n][A] float (continuous); latent [b][G] or None; lens [b] int32.
         Returns views raw [b][n][n_out], values [b][n][B], pred [b][n][2(S+1)], done [b][n]."""
+        self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
+                          dropout)
+        L.check(L.lib().xtrl_train_forward(C.byref(self.D), L.stream()), 'train_forward')
+        return self._outputs()
+
+    def _bind_inputs(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
+                     dropout):
         c, D = self.cfg, self.D
         b, n = swr.shape[0], swr.shape[1]
         assert b <= self.b_max and n <= self.n_max, (b, n, self.b_max, self.n_max)
@@ -143,7 +165,9 @@ class FusedTrainStep:
         if latent is not None:
             self._keep.append(latent.contiguous())
             D.latent = self._keep[-1].data_ptr()
-        L.check(L.lib().xtrl_train_forward(C.byref(D), L.stream()), 'train_forward')
+
+    def _outputs(self):
+        b, n = self.D.b, self.D.n
         T = b * n
         bf = self.buf
         return (bf['raw'][:T].view(b, n, -1), bf['values'][:T].view(b, n, -1), bf['pred'][:T].view(b, n, -1),
@@ -189,6 +213,112 @@ class FusedTrainStep:
         (distributed.BucketAllReduce), or None."""
         self.D.grad_events = C.cast(grad_events, C.POINTER(C.c_void_p)) if grad_events is not None else None
         L.check(L.lib().xtrl_train_backward(C.byref(self.D), L.stream()), 'train_backward')
+
+
+class FractalTrainStep(FusedTrainStep):
+    """The hand-scheduled learn step of the causal fractal policy body (fractal.FractalPolicyActorCritic,
+    xtrl_fractal_train_forward / _backward): the same minibatch interface, loss and heads as the
+    decoder's FusedTrainStep; the encoder per level: q|k|v GEMM, causal flash attention, three
+    post-norm residual blocks with nn.LayerNorm formed in the GEMM epilogues, the causal running
+    mean, level projection and global-state update, then the final aggregation."""
+
+    def __init__(self, model, flat: FlatParams, ws: torch.Tensor, b_max: int, n_max: int):
+        c = model.cfg
+        self.model, self.flat, self.cfg, self.ws = model, flat, c, ws
+        dev = flat.flat.device
+        self.dev = dev
+        d, H, dh, Lv = c.dim, c.heads, c.dim_head, model.levels
+        I, ff, B = H * dh, c.dim * c.ff_mult, c.num_bins
+        S, A = c.state_dim, c.num_actions
+        n_out = A * (2 if c.continuous else 1)
+        T = b_max * n_max
+        self.b_max, self.n_max, self.T_max = b_max, n_max, T
+        f32 = dict(device=dev, dtype=torch.float32)
+        E = lambda *shape: torch.empty(*shape, **f32)
+        off = lambda name: _off(flat, name)
+        enc = 'fractal_encoder.'
+        le0 = off(enc + 'level_embedding.level_embeds')
+        levels = (L.FractalTrainLevel * Lv)()
+        self.levels_py = []
+        for li in range(Lv):
+            pre = model.block_prefix(li)
+            V = levels[li]
+            V.w_qkv = _span_off(flat, [pre + 'self_attn.to_q.weight', pre + 'self_attn.to_k.weight',
+                                       pre + 'self_attn.to_v.weight'])
+            V.w_out, V.w_gv, V.w_go = off(pre + 'self_attn.to_out.weight'), off(pre + 'global_attn.to_v.weight'), \
+                off(pre + 'global_attn.to_out.weight')
+            for k in (1, 2, 3):
+                setattr(V, f'ln{k}_w', off(pre + f'norm{k}.weight'))
+                setattr(V, f'ln{k}_b', off(pre + f'norm{k}.bias'))
+            V.w_ff1, V.b_ff1 = off(pre + 'ff.ff.0.0.weight'), off(pre + 'ff.ff.0.0.bias')
+            V.w_ff2, V.b_ff2 = off(pre + 'ff.ff.2.weight'), off(pre + 'ff.ff.2.bias')
+            V.w_proj, V.b_proj = off(enc + f'level_projections.{li}.weight'), off(enc + f'level_projections.{li}.bias')
+            V.level_embed = le0 + li * d
+            bufs = dict(xin=E(T, d), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), s1=E(T, d), x1=E(T, d),
+                        st1=E(T, 2), g=E(T, d), gv=E(T, I), s2=E(T, d), x2=E(T, d), st2=E(T, 2), h=E(T, ff),
+                        u=E(T, ff), s3=E(T, d), x3=E(T, d), st3=E(T, 2), mean=E(T, d))
+            for k, t in bufs.items():
+                setattr(V, k, t.data_ptr())
+            self.levels_py.append(bufs)
+        self.levels = levels
+        ldp = d + 4
+        self.buf = dict(ac_in=E(T, c.in_dim), ewa=E(T, 2 * d), zp=E(T, ldp), hp=E(T, ldp), z1=E(T, 4 * d),
+                        h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d), raw=E(T, n_out), values=E(T, B),
+                        pred=E(T, 2 * (S + 1)), done=E(T), d_raw=E(T, n_out), d_values=E(T, B),
+                        d_pred=E(T, 2 * (S + 1)), d_done=E(T), dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp),
+                        dewa=E(T, 2 * d), delta=E(b_max * H * n_max))
+        # LayerNorm backward: d gamma and d beta partial rows side by side
+        part = max(256 * max(ff, 4 * d, B, 3 * I), 1024 * max(A, 1) * d,
+                   2 * int(L.lib().xtrl_train_part_floats(T, b_max, d, A)))
+        self.buf['part'] = E(part)
+        self.tok = torch.empty(b_max, n_max, L.LOSS_TOK, **f32)
+        self.stats = torch.zeros(L.LOSS_STATS, **f32)
+        self.scale_embeds = model.fractal_encoder.level_embedding.scale_embeds[:Lv].to(dev).float().contiguous()
+        self.fbuf = dict(scale_embeds=self.scale_embeds, le=E(Lv, d), bias0=E(d), cat=E(T, (Lv + 1) * d),
+                         hfa=E(T, 2 * d), dxa=E(T, d), dxb=E(T, d), ds=E(4, T, d), dmean=E(T, d), dga=E(T, d),
+                         dgb=E(T, d), dgv=E(T, I), dz=E(T, ff), dqkv=E(T, 3 * I), dob=E(T, I),
+                         dcat=E(T, (Lv + 1) * d), dhfa=E(T, 2 * d))
+
+        D = L.TrainDesc()
+        D.S, D.A, D.d, D.L, D.H, D.dh, D.ff, D.B = S, A, d, Lv, H, dh, ff, B
+        D.in_dim, D.n_out, D.G = c.in_dim, n_out, c.dim_gene if c.evolutionary else 0
+        D.continuous, D.evolutionary, D.gate_values, D.rot_dim = int(c.continuous), int(c.evolutionary), 0, 0
+        D.frac_head_grad, D.attn_scale = float(c.frac_head_grad), float(dh ** -0.5)
+        D.flat, D.grad = flat.flat.data_ptr(), flat.grad.data_ptr()
+        D.w_pin = off(enc + 'input_embed.weight')
+        _heads_desc(D, c, flat)
+        D.ln_final = -1
+        for k, t in self.buf.items():
+            setattr(D, k, t.data_ptr())
+        D.part_floats = self.buf['part'].numel()
+        D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
+        D.layers = None
+        self.D = D
+        Fd = L.FractalTrainDesc()
+        Fd.levels = Lv
+        Fd.b_in = off(enc + 'input_embed.bias')
+        Fd.g_init = off(enc + 'global_state_init')
+        Fd.w_gu, Fd.b_gu = off(enc + 'global_state_update.weight'), off(enc + 'global_state_update.bias')
+        Fd.w_fa0, Fd.b_fa0 = off(enc + 'final_aggregation.0.weight'), off(enc + 'final_aggregation.0.bias')
+        Fd.w_fa2, Fd.b_fa2 = off(enc + 'final_aggregation.2.weight'), off(enc + 'final_aggregation.2.bias')
+        for k, t in self.fbuf.items():
+            setattr(Fd, k, t.data_ptr())
+        Fd.level = C.cast(levels, C.POINTER(L.FractalTrainLevel))
+        self.Fd = Fd
+
+    def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
+                dropout):
+        self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
+                          dropout)
+        L.check(L.lib().xtrl_fractal_train_forward(C.byref(self.D), C.byref(self.Fd), L.stream()),
+                'fractal_train_forward')
+        return self._outputs()
+
+    def backward(self, grad_events=None):
+        """(no per-bucket events: the caller all-reduces the whole gradient after the backward)"""
+        assert grad_events is None, 'the fractal learn step has no gradient buckets'
+        L.check(L.lib().xtrl_fractal_train_backward(C.byref(self.D), C.byref(self.Fd), L.stream()),
+                'fractal_train_backward')
 
 
 def ff_dropout_mask(M, N, p, seed, offset, device, layer=0):
