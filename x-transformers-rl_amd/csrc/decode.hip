@@ -946,6 +946,15 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
           __hip_atomic_store(part + (16 * mt + 4 * q + i) * d + w * 16 * NT2 + 16 * nt + lr,
                              acc[mt][nt][0][i] + acc[mt][nt][1][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // Ordering (not the HIP memory model's release/acquire: a relaxed counter is formally a race
+  // there): the gfx950 visibility rules of /opt/skills/guides/MI355X_MICROARCH.md § visibility,
+  // "Valid forms", consumer bullet (1)-(4) — (2) every partial byte is stored sc1 (relaxed
+  // agent-scope atomic store = global_store ... sc1, write-through to the memory side), (3) every
+  // storing wave waits vmcnt(0) for its stores and the one counter add comes after a workgroup
+  // barrier behind all those waits, (1) the last arriver reads every partial with sc1 loads
+  // (relaxed agent-scope atomic load = global_load ... sc1, bypassing its CU's L1), so no
+  // agent-scope release (buffer_wbl2) or acquire (buffer_inv) is needed.  Checked in the ISA of
+  // this kernel: the partial stores / loads are global_store/load_dword ... sc1, never flat_.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its partial stores have completed
   __syncthreads();
   if (tid == 0)
