@@ -42,7 +42,8 @@ CONFIGS = {
     # configs[2] of BASELINE.json — the north-star workload, per GPU
     'c3': dict(workload='C3: LunarLander-shaped VecSim (S=8, A=4, hazard 1/64), 1024 episodes x 128 steps per '
                         'update per GPU, depth-4 d=256 4x16-head gated value-residual world-model policy, '
-                        'batch 128 episodes, 4 epochs, dropout 0.25',
+                        'batch 128 episodes, 4 epochs, dropout 0.25; no EPO (BASELINE.json configs[2] names no gene pool: one '
+                        'policy, actor / critic heads on [embed | state embed], in = 2d)',
                S=8, A=4, episodes=1024, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=False,
                batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
     # configs[1] — train_lander defaults (evolutionary, 3 genes), 256 episodes, depth-2 d=128
@@ -135,9 +136,12 @@ class DecodeAttnTimer:
         H, dh = c.heads, c.dim_head
         t = np.arange(T_eff)
         alive = (lens[None, :] > t[:, None]).sum(1)                  # live episodes at step t
-        # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + q|k|v|gate|mix row (4 dh + 1)
-        # + value-residual row (dh) ; write K,V at t (2 dh) + output (dh)
-        per_head = 4.0 * (2 * t * dh + (4 * dh + 1) + dh + 2 * dh + dh)
+        # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + its q|k|v(|gate|mix) row
+        # (3 dh, + dh + 1 with gates / mix) (+ the value-residual row dh); write K,V at t (2 dh) +
+        # output (dh)
+        row = 3 * dh + (dh if c.gate_values else 0) + (1 if c.learned_mix else 0)
+        vres = dh if c.value_residual else 0
+        per_head = 4.0 * (2 * t * dh + row + vres + 2 * dh + dh)
         self.bytes += float(self.L * (alive * H * per_head).sum())
 
     def detach(self):
@@ -192,32 +196,40 @@ class WgradGemmTimer:
         D.prof_events, D.prof_flops, D.prof_cap, D.prof_n = None, None, 0, None
 
 
-def pmc_traffic(*kernels):
-    """HBM bytes per launch of the kernels whose names contain one of ``kernels`` (dispatch-weighted
-    mean) from the newest committed PMC summary (profiles/rNN_pmc_traffic.json, written by
-    tools/gpu_check.sh pmc from two rocprofv3 --pmc passes of this bench: 2 x FETCH_SIZE +
-    WRITE_SIZE, the gfx950 correction of the MI355X guide)."""
+def _profile(kind, config):
+    """Newest committed profile of ``kind`` for a bench config: profiles/rNN_<kind>.<ext> for the
+    default C3 line, profiles/rNN_<kind>_<config>.<ext> for the others (tools/gpu_check.sh)."""
     import glob
-    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_pmc_traffic.json')))
-    if not files:
+    suffix = '' if config == 'c3' else f'_{config}'
+    ext = 'json' if kind == 'pmc_traffic' else 'csv'
+    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / f'r[0-9][0-9]_{kind}{suffix}.{ext}')))
+    return files[-1] if files else None
+
+
+def pmc_traffic(config, *kernels):
+    """HBM bytes per launch of the kernels whose names contain one of ``kernels`` (dispatch-weighted
+    mean) from the newest committed PMC summary of this config (profiles/rNN_pmc_traffic[_cfg].json,
+    written by tools/gpu_check.sh pmc from rocprofv3 --pmc passes of this bench: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of the MI355X guide)."""
+    path = _profile('pmc_traffic', config)
+    if path is None:
         return None
-    data = json.load(open(files[-1]))
+    data = json.load(open(path))
     hits = [v for k, v in data.items() if any(x in k for x in kernels)]
     n = sum(h['dispatches'] for h in hits)
     return round(sum(h['traffic'] * h['dispatches'] for h in hits) / n) if n else None
 
 
-def rocprof_avg_us(*kernels):
+def rocprof_avg_us(config, *kernels):
     """Average duration (us, call-weighted) of the kernels whose names contain one of ``kernels``
-    in the newest committed `rocprofv3 --kernel-trace --stats` summary of this bench
-    (profiles/rNN_kernel_stats.csv) — the profiler's clock beside the bench's HIP events."""
+    in the newest committed `rocprofv3 --kernel-trace --stats` summary of this config's bench
+    (profiles/rNN_kernel_stats[_cfg].csv) — the profiler's clock beside the bench's HIP events."""
     import csv
-    import glob
-    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_kernel_stats.csv')))
-    if not files:
+    path = _profile('kernel_stats', config)
+    if path is None:
         return None
     calls = total = 0
-    with open(files[-1]) as f:
+    with open(path) as f:
         for row in csv.DictReader(f):
             if any(k in row['Name'] for k in kernels):
                 calls += int(row['Calls'])
@@ -225,17 +237,63 @@ def rocprof_avg_us(*kernels):
     return round(total / calls / 1e3, 2) if calls else None
 
 
-def pmc_mfma_busy(*kernels):
+def pmc_mfma_busy(config, *kernels):
     """Matrix-core busy fraction of the kernels (dispatch-weighted mean of SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), the third PMC pass of tools/gpu_check.sh pmc), or None."""
-    import glob
-    files = sorted(glob.glob(str(Path(__file__).resolve().parent / 'profiles' / 'r*_pmc_traffic.json')))
-    if not files:
+    path = _profile('pmc_traffic', config)
+    if path is None:
         return None
-    data = json.load(open(files[-1]))
+    data = json.load(open(path))
     hits = [v for k, v in data.items() if any(x in k for x in kernels) and 'mfma_busy' in v]
     n = sum(h['dispatches'] for h in hits)
     return round(sum(h['mfma_busy'] * h['dispatches'] for h in hits) / n, 4) if n else None
+
+
+def algorithmic_work(c, levels, lens, epochs):
+    """SURVEY 8(d) algorithmic work per executed env-step of the model ``c`` (ModelConfig; ``levels``:
+    the fractal body's level count, None = the decoder): rollout FLOPs, update FLOPs (3 x epochs x
+    (rollout + world-model heads)) and decode K/V bytes, with t_bar = the mean number of keys a step
+    attends over (its position + 1) across the executed steps of ``lens``."""
+    lens = np.asarray(lens, dtype=np.float64)
+    t_bar = float((lens * (lens + 1) / 2).sum() / max(lens.sum(), 1))
+    d, S, A, B, H = c.dim, c.state_dim, c.num_actions, c.num_bins, c.heads
+    I, ff = c.heads * c.dim_head, c.dim * c.ff_mult
+    n_out = A * (2 if c.continuous else 1)
+    in_dim = d * (3 if c.evolutionary else 2)
+    heads = 2 * in_dim * 2 * d * 2 + 2 * 2 * d * (n_out + B) + (2 * c.dim_gene * d if c.evolutionary else 0)
+    embed = 4 * S * d
+    if levels is None:
+        L = c.depth
+        n_qkv = 3 * I + (I if c.gate_values else 0)
+        body = L * (2 * d * n_qkv + 2 * I * d + 2 * 2 * d * ff + 4 * I * t_bar)
+        body += (L - 1) * 2 * d * H if (c.value_residual and c.learned_mix) else 0
+    else:
+        L = levels
+        body = L * (2 * d * 3 * I + 2 * I * d + 2 * 2 * d * I + 2 * 2 * d * ff + 2 * 2 * d * d + 4 * I * t_bar)
+        body += 2 * (L + 1) * d * 2 * d + 2 * 2 * d * d
+    rollout = body + embed + heads
+    update = 3 * epochs * (rollout + 4 * d * d + 4 * d * (S + 1) + 4 * d)
+    kv = L * 2 * t_bar * I * 4 + L * 2 * I * 4
+    return dict(rollout_flops=rollout, update_flops=update, kv_bytes=kv, t_bar=t_bar)
+
+
+def total_roofline(value, work, mfma_busy):
+    """env-steps/s against the SURVEY 8(d) total roof: per env-step max(rollout FLOPs / peak, K/V
+    bytes / HBM) + update FLOPs / peak, at the fp32 MFMA peak SURVEY prices it on and at the
+    split-bf16 (X6) peak the GEMMs run at."""
+    def roof(peak_tf):
+        t = max(work['rollout_flops'] / (peak_tf * 1e12), work['kv_bytes'] / (HBM_PEAK_GBS * 1e9)) + \
+            work['update_flops'] / (peak_tf * 1e12)
+        return 1.0 / t
+    r32, r6 = roof(MFMA_F32_PEAK_TFLOPS), roof(X6_PEAK_TFLOPS)
+    return dict(achieved=round(value, 1), unit='env-steps/s', roof=round(r32), frac=round(value / r32, 4),
+                peak='fp32 MFMA %.1f TF/s (SURVEY 8(d)), HBM %.0f GB/s' % (MFMA_F32_PEAK_TFLOPS, HBM_PEAK_GBS),
+                roof_x6=round(r6), frac_x6=round(value / r6, 4),
+                peak_x6='split-bf16 (X6) %.1f TF/s = bf16 dense peak / 6' % X6_PEAK_TFLOPS,
+                rollout_mflop_per_step=round(work['rollout_flops'] / 1e6, 3),
+                update_mflop_per_step=round(work['update_flops'] / 1e6, 3),
+                kv_kb_per_step=round(work['kv_bytes'] / 1e3, 1), t_bar=round(work['t_bar'], 2),
+                mfma_busy_dominant_kernel=mfma_busy)
 
 
 def host_cores():
@@ -372,8 +430,9 @@ def main():
 
     for _ in range(args.warmup):
         one_update(learner, env, T)
-    # (the roofline timers instrument the decoder's decode step and fused learn step: C3 / C2 / C1)
-    timer = None if args.no_roofline or cfg.get('fractal') else DecodeAttnTimer(learner, env, T)
+    # roofline timers: HIP events around the decode attention launches and the learn step's
+    # weight-gradient GEMM launches (both policy bodies)
+    timer = None if args.no_roofline else DecodeAttnTimer(learner, env, T)
     gtimer = None
     if timer is not None:
         # untimed: capture the rollout graph with the event records inside, and count the
@@ -405,6 +464,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if timer is not None and lens_log:
         timer.collect(lens_log[-1])   # the event pairs hold the last update's T*L launches
+    lens_last = lens_log[-1].cpu().numpy() if lens_log else None
     el = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -416,8 +476,8 @@ def main():
     coll = {k: (dist_.COUNTS[k] - coll0[k]) / args.steps for k in coll0} if world > 1 else None
     value = env_steps / elapsed
 
-    # committed profiles (profiles/rNN_*) are of the default C3 bench: quoted for that workload only
-    prof = (lambda f, *k: f(*k)) if args.config == 'c3' else (lambda f, *k: None)
+    # committed profiles of this config's bench (profiles/rNN_*[_cfg])
+    prof = lambda f, *k: f(args.config, *k)   # noqa: E731
 
     phase_ms = dict(rollout=round(sum(e[0].elapsed_time(e[1]) for e in PHASES) / len(PHASES), 2),
                     learn=round(sum(e[1].elapsed_time(e[2]) for e in PHASES) / len(PHASES), 2))
@@ -456,6 +516,11 @@ def main():
                 timer.bytes / timer.launches / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))
         timer.detach()
 
+    total_roof = None
+    if lens_last is not None:
+        ag = learner.agent
+        work = algorithmic_work(ag.cfg, cfg.get('fractal'), lens_last, ag.epochs)
+        total_roof = total_roofline(value, work, roofline.get('mfma_busy') if roofline else None)
     loss_delta = None
     cpu = None
     # the loss-delta check runs one more update (its learn all-reduces gradients) and the CPU
@@ -481,7 +546,8 @@ def main():
                     config=dict(workload=cfg['workload'],
                                 global_batch=cfg['episodes'] * (cfg.get('genes', 3) if cfg['evo'] else 1) * world,
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),
-                    roofline=roofline, attention_roofline=attn_roofline, cpu_baseline=cpu, ppo_loss=loss_delta,
+                    roofline=roofline, attention_roofline=attn_roofline, total_roofline=total_roof,
+                    cpu_baseline=cpu, ppo_loss=loss_delta,
                     phase_ms=phase_ms)
         if coll is not None:
             mb = learner.agent.epochs * (len(learner.episode_genes_for_process) // learner.agent.batch_size)

@@ -26,8 +26,8 @@ int main() {
   float *A, *B, *C, *D, *bias;
   (void)hipMalloc(&A, (size_t)M * K * 4);
   (void)hipMalloc(&B, (size_t)N * K * 4);
-  (void)hipMalloc(&C, (size_t)M * N * 4);
-  (void)hipMalloc(&D, (size_t)M * N * 4);
+  (void)hipMalloc(&C, (size_t)M * (N + 64) * 4);
+  (void)hipMalloc(&D, (size_t)M * (N + 64) * 4);
   (void)hipMalloc(&bias, (size_t)N * 4);
   {   // non-zero operands (zero inputs run at a higher clock and skip erf's slow branches)
     std::vector<float> h((size_t)M * K);
@@ -48,5 +48,14 @@ int main() {
   printf("+dropout (byte)   %7.1f us\n", time_us(g, xtrl::EPI_GELU_DROP));
   g.drop_thresh = xtrl::dropout_thresh(0.1f); g.drop_thresh8 = 0; g.inv_keep = 1.f / 0.9f;
   printf("+dropout (word)   %7.1f us\n", time_us(g, xtrl::EPI_GELU_DROP));
+  // output row strides off the 4 KiB power of two (channel / bank spread of the store streams)
+  g.drop_thresh = xtrl::dropout_thresh(0.25f); g.drop_thresh8 = xtrl::dropout_thresh8(0.25f); g.inv_keep = 1.f / 0.75f;
+  for (int pad : {4, 16, 32, 64}) {
+    g.ldc = N + pad; g.ld_aux_out = N + pad;
+    printf("byte, ld %4d      %7.1f us   (plain %7.1f us)\n", N + pad, time_us(g, xtrl::EPI_GELU_DROP),
+           time_us(g, xtrl::EPI_NONE));
+  }
+  g.ldc = N; g.ld_aux_out = N;
+  // the derivative written to a second buffer only (no C store): the cost of each stream
   return 0;
 }

@@ -103,9 +103,18 @@ def show(path):
             ts = int(rows[a]['Start_Timestamp']); te = int(rows[b]['Start_Timestamp'])
             print(f'\nminibatch (gather #2..#3): {b - a} kernels, wall {(te - ts) / 1e3:.1f} us, '
                   f'busy {sum(dur[a:b]):.1f} us')
+            qk = 'Stream_Id' if 'Stream_Id' in rows[0] else 'Queue_Id'
+            last_end = {}
+            idle_q = defaultdict(float)
             for i in range(a, b):
                 gap = (int(rows[i]['Start_Timestamp']) - int(rows[i - 1]['End_Timestamp'])) / 1e3
-                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  {short(names[i])}')
+                q = rows[i].get(qk)
+                # the gap since this stream's previous kernel ended (its own idle time)
+                qgap = (int(rows[i]['Start_Timestamp']) - last_end[q]) / 1e3 if q in last_end else 0.0
+                idle_q[q] += max(qgap, 0.0)
+                last_end[q] = int(rows[i]['End_Timestamp'])
+                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  q{q} qgap {qgap:6.1f} at {(int(rows[i]["Start_Timestamp"]) - ts) / 1e3:7.1f}  {short(names[i])}')
+            print('  stream idle inside the minibatch: ' + ', '.join(f'{q}: {v:.1f} us' for q, v in idle_q.items()))
         # one decode step: the kernels between two consecutive sampling launches in the rollout
         samples = [i for i in roll if 'k_sample' in names[i] or 'k_heads_sample' in names[i]]
         if len(samples) > 12:

@@ -1193,7 +1193,9 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
     }
     if ((rc = dproj(D, t, xin, d, Q.w_qkv, d, nullptr, nullptr, 0, nullptr, 0, D->qkv, D->n_qkv, 3 * I, EPI_NONE, s)))
       return rc;
+    if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
+    if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
     if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s))) return rc;
     add_layernorm_launch(xin, d, F->mean, d, Q.ln1_w, Q.ln1_b, F->x1, d, E, d, F->ln_eps, s);   // x1 = LN1(x + attn)
     XTRL_LAUNCHED("add_layernorm");

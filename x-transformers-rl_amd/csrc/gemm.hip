@@ -811,6 +811,10 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       }
     }
   } else {
+    // EPI_LN_BWD: the x-transformers LayerNorm (no bias) with a residual gradient added after;
+    // EPI_LN_BWD2: nn.LayerNorm post-norm blocks (gradient added before, d beta, optional chain)
+    constexpr bool X = EPI == EPI_LN_BWD2;
+    const int ps = X && a.ln_pstride ? a.ln_pstride : N;
     float4 g[RPW], xv[RPW], dr[RPW];
     float2 st[RPW];
 #pragma unroll
@@ -818,11 +822,13 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       const int row = wave + 8 * rr, mc = min(m0 + row, M - 1);
       g[rr] = *reinterpret_cast<const float4*>(tile + row * LDT + cc);
       xv[rr] = ld4(a.ln_x + (int64_t)mc * N);
-      dr[rr] = a.ln_dres ? ld4(a.ln_dres + (int64_t)mc * N) : z4;
+      if constexpr (X) dr[rr] = a.ln_gpre ? ld4(a.ln_gpre + (int64_t)mc * N) : z4;
+      else dr[rr] = a.ln_dres ? ld4(a.ln_dres + (int64_t)mc * N) : z4;
       st[rr] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (int64_t)mc);
+      if constexpr (X) g[rr] = make_float4(g[rr].x + dr[rr].x, g[rr].y + dr[rr].y, g[rr].z + dr[rr].z, g[rr].w + dr[rr].w);
       if (!cok) g[rr] = z4;
     }
-    float4 dg = z4;
+    float4 dg = z4, db = z4;
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr) {
       const int m = m0 + wave + 8 * rr;
@@ -832,26 +838,69 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       const float4 gm = make_float4(g[rr].x * gam.x, g[rr].y * gam.y, g[rr].z * gam.z, g[rr].w * gam.w);
       if (m < M) {
         dg.x += g[rr].x * xh.x; dg.y += g[rr].y * xh.y; dg.z += g[rr].z * xh.z; dg.w += g[rr].w * xh.w;
+        if constexpr (X) { db.x += g[rr].x; db.y += g[rr].y; db.z += g[rr].z; db.w += g[rr].w; }
       }
       const float ma = wave_sum((gm.x + gm.y) + (gm.z + gm.w)) * inv_n;
       const float mb = wave_sum((gm.x * xh.x + gm.y * xh.y) + (gm.z * xh.z + gm.w * xh.w)) * inv_n;
       float4 o;
-      o.x = rs * (gm.x - ma - xh.x * mb) + dr[rr].x;
-      o.y = rs * (gm.y - ma - xh.y * mb) + dr[rr].y;
-      o.z = rs * (gm.z - ma - xh.z * mb) + dr[rr].z;
-      o.w = rs * (gm.w - ma - xh.w * mb) + dr[rr].w;
+      o.x = rs * (gm.x - ma - xh.x * mb);
+      o.y = rs * (gm.y - ma - xh.y * mb);
+      o.z = rs * (gm.z - ma - xh.z * mb);
+      o.w = rs * (gm.w - ma - xh.w * mb);
+      if constexpr (!X) {
+        o.x += dr[rr].x; o.y += dr[rr].y; o.z += dr[rr].z; o.w += dr[rr].w;
+      }
+      if (!cok) o = z4;
       if (m < M && cok) *reinterpret_cast<float4*>(a.C + (int64_t)m * a.ldc + c) = o;
+      if constexpr (X) g[rr] = o;   // the chained LayerNorm's upstream gradient
     }
-    // d gamma partial of this row tile: the 8 waves' column sums, added in wave order
+    // partials of this row tile: the 8 waves' column sums, added in wave order
     float* red = tile + BM * LDT;
-    if (cok) *reinterpret_cast<float4*>(red + wave * BN + c) = dg;
-    __syncthreads();
     const int t = threadIdx.x;
-    if (t < N) {
-      float sum = 0.f;
+    auto tile_sum = [&](float4 v, float* dst) {
+      __syncthreads();
+      if (cok) *reinterpret_cast<float4*>(red + wave * BN + c) = v;
+      __syncthreads();
+      if (t < N) {
+        float sum = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) sum += red[w * BN + t];
-      a.ln_part[(int64_t)row_tile * N + t] = sum;
+        for (int w = 0; w < 8; ++w) sum += red[w * BN + t];
+        dst[(int64_t)row_tile * ps + t] = sum;
+      }
+    };
+    tile_sum(dg, a.ln_part);
+    if constexpr (X) {
+      if (a.ln_part_b) tile_sum(db, a.ln_part_b);
+      if (a.ln2_out) {   // chained: the LayerNorm whose output's whole gradient is the one just formed
+        float4 gam2 = ld4(a.ln2_g);
+        if (!cok) gam2 = z4;
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int row = wave + 8 * rr, mc = min(m0 + row, M - 1);
+          xv[rr] = ld4(a.ln2_x + (int64_t)mc * N);
+          st[rr] = *reinterpret_cast<const float2*>(a.ln2_stats + 2 * (int64_t)mc);
+        }
+        dg = db = z4;
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int m = m0 + wave + 8 * rr;
+          const float mu = st[rr].x, rs = st[rr].y;
+          float4 xh = make_float4((xv[rr].x - mu) * rs, (xv[rr].y - mu) * rs, (xv[rr].z - mu) * rs, (xv[rr].w - mu) * rs);
+          if (!cok) xh = z4;
+          const float4 gm = make_float4(g[rr].x * gam2.x, g[rr].y * gam2.y, g[rr].z * gam2.z, g[rr].w * gam2.w);
+          if (m < M) {
+            dg.x += g[rr].x * xh.x; dg.y += g[rr].y * xh.y; dg.z += g[rr].z * xh.z; dg.w += g[rr].w * xh.w;
+            db.x += g[rr].x; db.y += g[rr].y; db.z += g[rr].z; db.w += g[rr].w;
+          }
+          const float ma = wave_sum((gm.x + gm.y) + (gm.z + gm.w)) * inv_n;
+          const float mb = wave_sum((gm.x * xh.x + gm.y * xh.y) + (gm.z * xh.z + gm.w * xh.w)) * inv_n;
+          const float4 o = make_float4(rs * (gm.x - ma - xh.x * mb), rs * (gm.y - ma - xh.y * mb),
+                                       rs * (gm.z - ma - xh.z * mb), rs * (gm.w - ma - xh.w * mb));
+          if (m < M && cok) *reinterpret_cast<float4*>(a.ln2_out + (int64_t)m * N + c) = o;
+        }
+        tile_sum(dg, a.ln2_part);
+        tile_sum(db, a.ln2_part_b);
+      }
     }
   }
 }
@@ -889,7 +938,7 @@ __device__ int g_ws_mode;   // 1: consumers skip the MFMAs; 2: producers skip lo
 template <bool TA, bool TB, int EPI, bool RES, int BM = 128, int BN = 128, bool KT = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
   constexpr int BK = 32, XRS = BK + 8, NP = 256, TM = 2, TN = 2, WN = BN / 64;
-  constexpr bool LNE = (EPI == EPI_RES_LN || EPI == EPI_LN_BWD);
+  constexpr bool LNE = (EPI == EPI_RES_LN || EPI == EPI_LN_BWD || EPI == EPI_LN_BWD2);
   constexpr int A_F4 = BM * BK / 4 / NP, B_F4 = BN * BK / 4 / NP;   // float4 per producer thread per slab
   constexpr int IMG = 3 * (BM + BN) * XRS;                           // bf16 per piece image
   static_assert((BM == 128 && BN == 128) || (BM == 64 && BN == 256), "tile 128 x 128 or 64 x 256");
@@ -1376,10 +1425,18 @@ int ln_gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, bool vec, 
       if (kt) launch_ws<false, false, EPI_RES_LN, true, 64, 256, true>(a, s);
       else launch_ws<false, false, EPI_RES_LN, true, 64, 256, false>(a, s);
     }
-  } else {
+  } else if (epi == EPI_LN_BWD) {
     XTRL_REQUIRE(trans_b && !res && a.ln_x && a.ln_part, "gemm: LayerNorm-backward epilogue arguments");
     if (narrow) launch_ws<false, true, EPI_LN_BWD, false, 128, 128, true>(a, s);
     else launch_ws<false, true, EPI_LN_BWD, false, 64, 256, true>(a, s);
+  } else {
+    XTRL_REQUIRE(trans_b && !res && a.ln_x && a.ln_part && (!a.ln_gpre || ((uintptr_t)a.ln_gpre & 15u) == 0) &&
+                     (!a.ln2_out || (a.ln2_g && a.ln2_x && a.ln2_stats && a.ln2_part && a.ln2_part_b &&
+                                     ((uintptr_t)a.ln2_out & 15u) == 0 && ((uintptr_t)a.ln2_g & 15u) == 0)) &&
+                     a.ldc == a.N,
+                 "gemm: post-norm LayerNorm-backward epilogue arguments");
+    if (narrow) launch_ws<false, true, EPI_LN_BWD2, false, 128, 128, true>(a, s);
+    else launch_ws<false, true, EPI_LN_BWD2, false, 64, 256, true>(a, s);
   }
   XTRL_LAUNCHED("gemm_ln");
   return XTRL_OK;
@@ -1491,7 +1548,7 @@ int gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, hipStream_t s
   const bool ln = a.gamma != nullptr, res = a.R != nullptr;
   // (the split-bf16 GELU + dropout kernels have only the row-vector epilogue: other layouts take the
   // scalar-load kernel)
-  if (epi == EPI_RES_LN || epi == EPI_LN_BWD) return ln_gemm_run(a, trans_a, trans_b, epi, vec, s);
+  if (epi == EPI_RES_LN || epi == EPI_LN_BWD || epi == EPI_LN_BWD2) return ln_gemm_run(a, trans_a, trans_b, epi, vec, s);
   const bool vec_k = vec && (epi != EPI_GELU_DROP || gelu_drop_v4_host(a));
 #define XG(TA_, TB_, E_, L_, R_)                                                                   \
   if (trans_a == TA_ && trans_b == TB_ && epi == E_ && ln == L_ && res == R_) {                    \

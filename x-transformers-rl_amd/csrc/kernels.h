@@ -28,6 +28,9 @@ enum GemmEpi : int {
   EPI_LN_BWD = 10,     // g = v; xhat = (ln_x - mean) rstd; C = rstd (g ln_g - mean_n(g ln_g) - xhat
                        //   mean_n(g ln_g xhat)) + ln_dres;  ln_part[row tile][n] = sum_tile rows g xhat
   EPI_MASK_POS = 11,   // C = aux_in > 0 ? v : 0        (dgrad through a ReLU whose output is aux_in)
+  EPI_LN_BWD2 = 12,    // post-norm (nn.LayerNorm) backward: g = v + ln_gpre; C = LN_bwd(g) (+ d gamma / d beta
+                       //   partials); with ln2_out also C2 = LN_bwd(C; ln2_x, ln2_stats, ln2_g) (+ partials):
+                       //   two chained post-norm LayerNorms whose residual path has no other branch
 };
 
 struct GemmArgs {
@@ -69,6 +72,16 @@ struct GemmArgs {
   const float* ln_x = nullptr;    // LN_BWD: the LayerNorm input [M][N] (row stride N)
   const float* ln_dres = nullptr; // LN_BWD: gradient added to the output (may alias C: same element, same thread)
   float* ln_part = nullptr;       // LN_BWD: d gamma partials [ceil(M / BM)][N]
+  // EPI_LN_BWD2 (partial rows of stride ln_pstride: the four partial sets of one row tile side by side)
+  const float* ln_gpre = nullptr; // gradient added to the GEMM output before the LayerNorm backward [M][N]
+  float* ln_part_b = nullptr;     // d beta partials
+  int ln_pstride = 0;
+  const float* ln2_g = nullptr;   // the chained LayerNorm: gamma, input, (mean, rstd), output, partials
+  const float* ln2_x = nullptr;
+  const float* ln2_stats = nullptr;
+  float* ln2_out = nullptr;
+  float* ln2_part = nullptr;
+  float* ln2_part_b = nullptr;
 };
 // rows per workgroup of the LayerNorm-epilogue GEMM for an N-column row (the column tile is the row)
 int gemm_ln_rows(int N);

@@ -30,6 +30,8 @@ struct EmbedArgs {
   float *x0, *ac_in, *ewa;
   int T, n, S, A, d, in_dim, continuous, evolutionary;
   float keep;
+  const float* ln_g;   // (k_embed_ln) layer 0's attention pre-norm: gamma, output rows, (mean, rstd)
+  float *xn, *st;
 };
 
 constexpr int EMB_TOK = 32, EMB_U = 8, EMB_MAXS = 32;
@@ -92,6 +94,96 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
         a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se[u];
         a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an[u];
         if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = le[u];
+      }
+    }
+  }
+}
+
+// k_embed with layer 0's attention pre-norm folded in (d <= 256: thread c owns column c): per
+// batch of EMB_U tokens the row sums and the centred sums of squares meet through LDS (two
+// barriers), then x0, LN(x0) gamma and (mean, rstd) are stored — k_ln_fwd's arithmetic (two-pass
+// variance, eps 1e-5) with the row sum associated per wave, then over the 4 waves
+template <int S_>
+__global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
+  constexpr int MS = S_ > 0 ? S_ : EMB_MAXS;
+  const int S = S_ > 0 ? S_ : a.S;
+  __shared__ float red[2][4][EMB_U];
+  const int c = threadIdx.x, lane = c & 63, w = c >> 6;
+  const bool on = c < a.d;
+  const int cc = on ? c : 0;
+  float wp[MS], ws[MS];
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    wp[s] = s < S ? a.w_pin[(int64_t)cc * S + s] : 0.f;
+    ws[s] = s < S ? a.w_se[(int64_t)cc * S + s] : 0.f;
+  }
+  const float bse = a.b_se[cc], re = a.reward_embed[cc], gam = on ? a.ln_g[cc] : 0.f;
+  const float bemb = a.continuous ? a.act_emb_b[cc] : 0.f;
+  const float inv_d = 1.0f / (float)a.d;
+  for (int t0 = blockIdx.x * EMB_TOK; t0 < min(a.T, (int)(blockIdx.x + 1) * EMB_TOK); t0 += EMB_U) {
+    float x[EMB_U], se[EMB_U], an[EMB_U], le[EMB_U];
+#pragma unroll
+    for (int u = 0; u < EMB_U; ++u) {
+      const int t = min(t0 + u, a.T - 1);
+      const float* st = a.swr + (int64_t)t * (S + 1);
+      float sp = 0.f, ss = 0.f;
+#pragma unroll
+      for (int s = 0; s < MS; ++s) {
+        if (s < S) {
+          const float v = st[s];
+          sp += v * wp[s];
+          ss += v * ws[s];
+        }
+      }
+      float ap;
+      if (a.continuous) {
+        const float* wa = a.act_emb + (int64_t)cc * a.A;
+        float p = 0.f, q = 0.f;
+        for (int k = 0; k < a.A; ++k) {
+          p += a.prev_af[(int64_t)t * a.A + k] * wa[k];
+          q += a.next_af[(int64_t)t * a.A + k] * wa[k];
+        }
+        ap = p + bemb;
+        an[u] = q + bemb;
+      } else {   // SafeEmbedding: action < 0 -> zero vector (xtrl.py:181-195)
+        const int p = a.prev_a[t], q = a.next_a[t];
+        ap = p >= 0 ? a.act_emb[(int64_t)p * a.d + cc] : 0.f;
+        an[u] = q >= 0 ? a.act_emb[(int64_t)q * a.d + cc] : 0.f;
+      }
+      x[u] = on ? sp + (ap + (st[S] * re) * a.keep) : 0.f;
+      se[u] = ss + bse;
+      le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + cc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < EMB_U; ++u) {
+      const float r = wave_sum(x[u]);
+      if (lane == 0) red[0][w][u] = r;
+    }
+    __syncthreads();
+    float mean[EMB_U], dl[EMB_U];
+#pragma unroll
+    for (int u = 0; u < EMB_U; ++u) {
+      mean[u] = ((red[0][0][u] + red[0][1][u]) + (red[0][2][u] + red[0][3][u])) * inv_d;
+      dl[u] = on ? x[u] - mean[u] : 0.f;
+      const float q = wave_sum(dl[u] * dl[u]);
+      if (lane == 0) red[1][w][u] = q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < EMB_U; ++u) {
+      const int t = t0 + u;
+      if (t >= a.T) break;
+      const float rstd = 1.0f / sqrtf(((red[1][0][u] + red[1][1][u]) + (red[1][2][u] + red[1][3][u])) * inv_d + 1e-5f);
+      if (on) {
+        a.x0[(int64_t)t * a.d + c] = x[u];
+        a.xn[(int64_t)t * a.d + c] = (dl[u] * rstd) * gam;
+        a.ac_in[(int64_t)t * a.in_dim + a.d + c] = se[u];
+        a.ewa[(int64_t)t * 2 * a.d + a.d + c] = an[u];
+        if (a.evolutionary) a.ac_in[(int64_t)t * a.in_dim + 2 * a.d + c] = le[u];
+      }
+      if (c == 0) {
+        a.st[2 * (int64_t)t] = mean[u];
+        a.st[2 * (int64_t)t + 1] = rstd;
       }
     }
   }
@@ -161,7 +253,7 @@ template <int DPL>
 __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2,
                                                           int ldg2, const float* x, const float* stats,
                                                           const float* gamma, const float* dres, float* dx,
-                                                          float* part, float* part_b, int T, int d) {
+                                                          float* part, float* part_b, int pstride, int T, int d) {
   __shared__ float red[LN_WAVES][64 * DPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gam[DPL], dg[DPL], db[DPL];
@@ -230,7 +322,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
     float v = 0.f;
 #pragma unroll
     for (int j = 0; j < LN_WAVES; ++j) v += red[j][c];
-    part[(int64_t)blockIdx.x * d + c] = v;
+    part[(int64_t)blockIdx.x * pstride + c] = v;
   }
   if (!part_b) return;
   __syncthreads();
@@ -241,7 +333,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
     float v = 0.f;
 #pragma unroll
     for (int j = 0; j < LN_WAVES; ++j) v += red[j][c];
-    part_b[(int64_t)blockIdx.x * d + c] = v;
+    part_b[(int64_t)blockIdx.x * pstride + c] = v;
   }
 }
 
@@ -771,14 +863,23 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
            const float* st, const float* gamma, const float* dres, float* dx, float* dgamma, float* dbeta = nullptr) {
   const int d = c.D->d, nb = (int)blocks(c.T, LN_ROWS);
   XTRL_REQUIRE((int64_t)nb * d * (dbeta ? 2 : 1) <= c.D->part_floats, "train: partial-sum workspace too small");
-  float* pb = dbeta ? c.D->part + (int64_t)nb * d : nullptr;
+  // with d beta: the two partial rows of a block side by side ([gamma | beta], stride 2d), so one
+  // column-sum launch finishes both when the parameters are adjacent (nn.LayerNorm weight, bias)
+  const int ps = dbeta ? 2 * d : d;
+  float* pb = dbeta ? c.D->part + d : nullptr;
   const dim3 g(nb), bl(64 * LN_WAVES);
-  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
-  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
-  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
-  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, c.D->part, pb, c.T, d);
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
-  if (dbeta) hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, pb, nb, d, dbeta);
+  float* P = c.D->part;
+  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
+  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
+  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
+  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
+  if (!dbeta) {
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, P, nb, d, dgamma);
+  } else if (dbeta == dgamma + d) {
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(2 * d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, P, nb, 2 * d, dgamma);
+  } else {
+    XTRL_REQUIRE(false, "train: LayerNorm weight and bias gradients must be adjacent");
+  }
   XTRL_LAUNCHED("train ln_bwd");
   return XTRL_OK;
 }
@@ -941,16 +1042,27 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   EmbedArgs ea{D->swr, c.P(D->w_pin), c.P(D->act_emb), c.P(D->act_emb_b), c.P(D->reward_embed), c.P(D->w_se),
                c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
                D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
-               D->evolutionary, D->reward_keep};
-  if (D->S == 8) hipLaunchKernelGGL(k_embed<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
-  else hipLaunchKernelGGL(k_embed<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
-  XTRL_LAUNCHED("train embed");
-  // decoder blocks; fused: every LayerNorm but layer 0's attention pre-norm is formed in the epilogue
-  // of the GEMM that completes its rows (out-projection + residual, FF2 + residual)
+               D->evolutionary, D->reward_keep, nullptr, nullptr, nullptr};
+  // fused: every LayerNorm is formed by the kernel that completes its rows — layer 0's attention
+  // pre-norm by the embedding, the others in the epilogue of the GEMM before them (out-projection +
+  // residual, FF2 + residual)
   const bool fuse = ln_fusable(D);
+  if (fuse) {
+    const XtrlTrainLayer& L0 = D->layers[0];
+    ea.ln_g = c.P(L0.ln_attn);
+    ea.xn = L0.xn_attn;
+    ea.st = L0.st_attn;
+    if (D->S == 8) hipLaunchKernelGGL(k_embed_ln<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+    else hipLaunchKernelGGL(k_embed_ln<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+  } else if (D->S == 8) {
+    hipLaunchKernelGGL(k_embed<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+  } else {
+    hipLaunchKernelGGL(k_embed<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+  }
+  XTRL_LAUNCHED("train embed");
   for (int li = 0; li < D->L; ++li) {
     const XtrlTrainLayer& Ly = D->layers[li];
-    if (li == 0 || !fuse)
+    if (!fuse)
       if ((rc = ln_fwd(c, Ly.x_attn, c.P(Ly.ln_attn), Ly.xn_attn, d, nullptr, 0, Ly.st_attn))) return rc;
     if ((rc = linear_fwd(c, Ly.xn_attn, d, c.P(Ly.w_proj), c.P(Ly.b_proj), Ly.proj, Ly.n_qkv, T, Ly.n_qkv, d,
                          EPI_NONE, nullptr, nullptr, 0, 1 << 30, 3 * I)))
@@ -1222,6 +1334,37 @@ int dgrad_res(const Ctx& c, const float* dY, int ldy, const float* W, int N, int
   return gemm_run(g, 0, 1, EPI_NONE, c.s);
 }
 
+// dx = dY W + gpre -> ds_a = norm2 backward(dx) and ds_b = norm1 backward(ds_a), one launch; the four
+// partial rows of a row tile side by side [d gamma1 | d beta1 | d gamma2 | d beta2] -> one column sum
+// into the adjacent norm1.weight | norm1.bias | norm2.weight | norm2.bias gradients
+int dgrad_post_ln2(const Ctx& c, const float* dY, int ldy, const float* W, const float* gpre,
+                   const XtrlFractalTrainLevel& V, float* ds_a, float* ds_b) {
+  const int d = c.D->d, K = c.D->ff, nb = (c.T + gemm_ln_rows(d) - 1) / gemm_ln_rows(d);
+  XTRL_REQUIRE(V.ln1_b == V.ln1_w + d && V.ln2_w == V.ln1_w + 2 * d && V.ln2_b == V.ln1_w + 3 * d,
+               "fractal train: norm1 / norm2 parameters must be adjacent in the flat buffer");
+  XTRL_REQUIRE((int64_t)nb * 4 * d <= c.D->part_floats, "fractal train: partial-sum workspace too small");
+  float* P = c.D->part;
+  GemmArgs g;
+  g.A = dY; g.lda = ldy; g.B = W; g.ldb = d; g.C = ds_a; g.ldc = d; g.M = c.T; g.N = d; g.K = K;
+  g.ln_g = c.P(V.ln2_w); g.ln_x = V.s2; g.ln_stats = V.st2; g.ln_gpre = gpre;
+  g.ln_part = P + 2 * d; g.ln_part_b = P + 3 * d; g.ln_pstride = 4 * d;
+  g.ln2_g = c.P(V.ln1_w); g.ln2_x = V.s1; g.ln2_stats = V.st1; g.ln2_out = ds_b; g.ln2_part = P;
+  g.ln2_part_b = P + d;
+  if (int rc = gemm_run(g, 0, 1, EPI_LN_BWD2, c.s)) return rc;
+  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(4 * d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, P, nb, 4 * d,
+                     c.G(V.ln1_w));
+  XTRL_LAUNCHED("fractal dgrad_post_ln2");
+  return XTRL_OK;
+}
+
+bool ln_fusable_fractal(const XtrlTrainDesc* D) {
+  static const bool on = [] {
+    const char* e = getenv("XTRL_FUSED_LN");
+    return !(e && atoi(e) == 0);
+  }();
+  return on && D->d % 4 == 0 && D->d <= 256 && D->ff % 4 == 0;
+}
+
 AttnProblem fractal_attn(const Ctx& c, int level) {
   const XtrlTrainDesc* D = c.D;
   const int I = D->H * D->dh;
@@ -1392,6 +1535,8 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
   // gradient of x3_l from level l + 1's input (none for the last level).  Scratch a side-stream
   // weight gradient still reads is not overwritten before its event: the LN planes of ds, dz, dgv and
   // dqkv by the next (shallower) level, the dg buffers (alternating) two levels on.
+  // the chained post-norm LayerNorm backward epilogue (XTRL_FUSED_LN=0: separate launches)
+  const bool post2 = ln_fusable_fractal(D);
   const float* dgn = F->dcat + Lv * d;
   int lddgn = ldcat;
   const float* dxn = nullptr;
@@ -1425,13 +1570,22 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, F->dz, ff, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
     e_ff1 = Fk.mark();
-    // dx2 = ds3 + dz W1
-    if ((rc = dgrad_res(c, F->dz, ff, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
-    // norm2 backward -> ds2; cross-attention: s2 = x1 + gv W_go^T, gv = g W_gv^T
+    // dx2 = ds3 + dz W1; norm2 backward -> ds2; norm1 backward (x1's whole gradient is ds2, the
+    // residual path of s2) -> ds1: one launch (the LayerNorm backward of both in the epilogue)
     if ((rc = Fk.wait(e_go))) return rc;
-    if ((rc = ln_bwd(c, F->dxb, d, 1.f, nullptr, 0, V.s2, V.st2, c.P(V.ln2_w), nullptr, ds2, c.G(V.ln2_w),
-                     c.G(V.ln2_b))))
-      return rc;
+    if ((rc = Fk.wait(e_out))) return rc;
+    if (post2) {
+      if ((rc = dgrad_post_ln2(c, F->dz, ff, c.P(V.w_ff1), ds3, V, ds2, ds1))) return rc;
+    } else {
+      if ((rc = dgrad_res(c, F->dz, ff, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
+      if ((rc = ln_bwd(c, F->dxb, d, 1.f, nullptr, 0, V.s2, V.st2, c.P(V.ln2_w), nullptr, ds2, c.G(V.ln2_w),
+                       c.G(V.ln2_b))))
+        return rc;
+      if ((rc = ln_bwd(c, ds2, d, 1.f, nullptr, 0, V.s1, V.st1, c.P(V.ln1_w), nullptr, ds1, c.G(V.ln1_w),
+                       c.G(V.ln1_b))))
+        return rc;
+    }
+    // cross-attention: s2 = x1 + gv W_go^T, gv = g W_gv^T
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, ds2, d, V.gv, I, c.G(V.w_go), T, d, I))) return rc;
     e_go = Fk.mark();
@@ -1445,10 +1599,6 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
     float* dgc = ((Lv - 1 - l) & 1) ? F->dgb : F->dga;
     if ((rc = Fk.wait(e_gu_prev))) return rc;
     if ((rc = dgrad_res(c, F->dgv, I, c.P(V.w_gv), I, d, dgn, lddgn, dgc, d))) return rc;
-    // norm1 backward (its input gradient: ds2, the residual path of s2) -> ds1
-    if ((rc = Fk.wait(e_out))) return rc;
-    if ((rc = ln_bwd(c, ds2, d, 1.f, nullptr, 0, V.s1, V.st1, c.P(V.ln1_w), nullptr, ds1, c.G(V.ln1_w), c.G(V.ln1_b))))
-      return rc;
     // self-attention: s1 = x_in + o W_out^T
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, ds1, d, V.o, I, c.G(V.w_out), T, d, I))) return rc;

@@ -337,6 +337,7 @@ class Agent(nn.Module):
         assert n_mb * attn_stride < 2 ** 32, "attention dropout counters exceed 32 bits"
         stats_rows = torch.zeros(n_mb, L.LOSS_STATS, device=dev) if fused else None
         logs0 = len(self.logs)
+        lat_ep = None
         for epoch in range(self.epochs):
             for mbi, k in enumerate(range(0, N, self.batch_size)):
                 idx = perms[epoch, k:k + self.batch_size]
@@ -358,7 +359,9 @@ class Agent(nn.Module):
                     mb_old_lp, mb_ret = old_lp[idx].contiguous(), returns[idx].contiguous()
                     mb_old_v, mb_done = old_values[idx].contiguous(), bounds[idx].contiguous()
                 keep = reward_coin(self.seed, update, epoch, mbi, c.reward_dropout)
-                latent = self.latent(gene_ids[idx]) if c.evolutionary else None
+                if c.evolutionary and lat_ep is None:   # per-episode latents, refreshed after an evolve
+                    lat_ep = self.latent(gene_ids)
+                latent = lat_ep.index_select(0, idx) if c.evolutionary else None
                 # dropout streams: every minibatch of the update its own FF counter and a disjoint
                 # range of attention counters (layer in the Philox c3 sub-index, include/xtrl_hip.h)
                 ordinal = epoch * n_mb_epoch + mbi
@@ -418,6 +421,7 @@ class Agent(nn.Module):
                     g = torch.Generator().manual_seed(evolve_seed(self.seed, update, epoch, mbi))
                     self.gene_pool.evolve_(fitnesses, generator=g)
                     self._genes_dev = None
+                    lat_ep = None
                 self.logs.append(stats)
         self.rs_mean, self.rs_var, self.rs_step = rs_mean, rs_var, rs_step
         self.step += 1
