@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 12
+#define XTRL_ABI_VERSION 13
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -406,6 +406,10 @@ typedef struct XtrlTrainDesc {
    * bucket i (a contiguous range of the flat gradient, xtrl_amd.model flat_order) while the backward
    * continues (DDP's bucketed all-reduce, xtrl.py:885/981) */
   void** grad_events;
+  /* row stride (floats) of the [T][ff] feed-forward buffers hd, u, dff (the fractal body's h, u, dz):
+   * >= ff, a multiple of 4; 0 = ff.  A stride off the 4 KiB power of two (e.g. ff + 16) spreads the
+   * FF1 epilogue's two store streams over the memory channels */
+  int ld_ff;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

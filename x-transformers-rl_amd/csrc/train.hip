@@ -706,6 +706,10 @@ struct Ctx {
   float* G(int64_t off) const { return off >= 0 ? D->grad + off : nullptr; }
 };
 
+// row stride of the [T][ff] feed-forward buffers (hd, u, dff; fractal h, u, dz): ld_ff >= ff, 0 = ff
+// (a stride off the 4 KiB power of two spreads the FF1 epilogue's two store streams: 93 -> 82 us)
+inline int ld_ff(const XtrlTrainDesc* D) { return D->ld_ff > 0 ? D->ld_ff : D->ff; }
+
 // ---- weight gradients on a side stream ---------------------------------------------------------
 // The weight-gradient GEMMs (and their split-K reduces) are off the backward's critical path: only
 // the optimiser step reads dW.  They run on a low-priority side stream, each after an event on the
@@ -949,6 +953,7 @@ int validate(const XtrlTrainDesc* D) {
   XTRL_REQUIRE(D->d <= 64 * kMaxDPerLane, "train: d = %d > %d unsupported", D->d, 64 * kMaxDPerLane);
   XTRL_REQUIRE(D->dh % 2 == 0 && D->rot_dim <= D->dh, "train: bad rotary dims");
   XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "train: in_dim mismatch");
+  XTRL_REQUIRE(D->ld_ff == 0 || (D->ld_ff >= D->ff && D->ld_ff % 4 == 0), "train: ld_ff %d (ff %d)", D->ld_ff, D->ff);
   XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "train: evolutionary needs latent buffers");
   XTRL_REQUIRE(D->S <= EMB_MAXS, "train: state_dim %d > %d unsupported", D->S, EMB_MAXS);
   XTRL_REQUIRE(D->continuous || D->A <= EMB_MAXA, "train: %d discrete actions > %d unsupported", D->A, EMB_MAXA);
@@ -1032,7 +1037,7 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F) {
 int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   if (int rc = validate(D)) return rc;
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff;
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D);
   int rc;
   // embeddings
   if (D->evolutionary) {
@@ -1086,21 +1091,21 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
         return rc;
       if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
     }
-    if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, ff, T, ff, d, EPI_GELU_DROP, nullptr,
-                         Ly.u, ff, 1 << 30, 0, D->ff_offset, (uint32_t)li)))
+    if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, lf, T, ff, d, EPI_GELU_DROP, nullptr,
+                         Ly.u, lf, 1 << 30, 0, D->ff_offset, (uint32_t)li)))
       return rc;
     float* x_out = li + 1 < D->L ? D->layers[li + 1].x_attn : D->x_final;
     if (fuse && li + 1 < D->L) {   // + the next block's attention pre-norm
       const XtrlTrainLayer& Ln = D->layers[li + 1];
-      if ((rc = linear_res_ln(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(Ln.ln_attn),
+      if ((rc = linear_res_ln(c, Ly.hd, lf, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(Ln.ln_attn),
                               Ln.xn_attn, d, nullptr, 0, Ln.st_attn)))
         return rc;
     } else if (fuse) {             // + the final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
-      if ((rc = linear_res_ln(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(D->ln_final),
+      if ((rc = linear_res_ln(c, Ly.hd, lf, c.P(Ly.w_ff2), c.P(Ly.b_ff2), Ly.x_ff, x_out, ff, c.P(D->ln_final),
                               D->ac_in, D->in_dim, D->ewa, 2 * d, D->st_final)))
         return rc;
     } else {
-      if ((rc = linear_fwd(c, Ly.hd, ff, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
+      if ((rc = linear_fwd(c, Ly.hd, lf, c.P(Ly.w_ff2), c.P(Ly.b_ff2), x_out, d, T, d, ff, EPI_NONE, Ly.x_ff))) return rc;
     }
   }
   // final norm -> embed, into ac_in[:, :d] and ewa[:, :d]
@@ -1116,7 +1121,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   if (int rc = validate(D)) return rc;
   XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "train: missing loss gradients");
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff;
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D);
   int rc;
   SideStream& side = side_stream();
   const bool two = side.ok && side.ensure(side_events_needed(D->L));
@@ -1164,22 +1169,22 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     const XtrlTrainLayer& Ly = D->layers[li];
     // FF2 (+ residual): dx is the gradient w.r.t. the block output
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dx, d, Ly.hd, ff, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
+    if ((rc = wgrad(cw, D->dx, d, Ly.hd, lf, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
     hipEvent_t e_ff2 = F.mark();
     if ((rc = F.wait(e_ff1))) return rc;
-    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, ff, T, d, ff, EPI_MUL_AUX, Ly.u, ff))) return rc;
+    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, lf, T, d, ff, EPI_MUL_AUX, Ly.u, lf))) return rc;
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dff, ff, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = wgrad(cw, D->dff, lf, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
     e_ff1 = F.mark();
     float* xg = D->dx;   // gradient w.r.t. the attention block's output
     if (fuse) {
       if ((rc = F.wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
-      if ((rc = dgrad_ln_bwd(c, D->dff, ff, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx2,
+      if ((rc = dgrad_ln_bwd(c, D->dff, lf, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx2,
                              c.G(Ly.ln_ff))))
         return rc;
       xg = D->dx2;
     } else {
-      if ((rc = linear_dgrad(c, D->dff, ff, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+      if ((rc = linear_dgrad(c, D->dff, lf, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
       if ((rc = F.wait(e_ff2))) return rc;
       if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
         return rc;
@@ -1285,6 +1290,8 @@ int validate_fractal(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F) {
   XTRL_REQUIRE(D->d % 4 == 0 && D->d <= 256 && (D->H * D->dh) % 4 == 0 && D->ff % 4 == 0,
                "fractal train: needs d %% 4 == 0, d <= 256, H dh %% 4 == 0, ff %% 4 == 0 (d = %d)", D->d);
   XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "fractal train: in_dim mismatch");
+  XTRL_REQUIRE(D->ld_ff == 0 || (D->ld_ff >= D->ff && D->ld_ff % 4 == 0), "fractal train: ld_ff %d (ff %d)", D->ld_ff,
+               D->ff);
   XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "fractal train: evolutionary needs latent buffers");
   XTRL_REQUIRE(D->continuous ? D->next_action_f != nullptr : D->next_action != nullptr,
                "fractal train: missing next actions");
@@ -1399,7 +1406,8 @@ int rows_axpb(const Ctx& c, const float* a, int lda, float alpha, const float* b
 int fractal_train_forward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F, hipStream_t s) {
   if (int rc = validate_fractal(D, F)) return rc;
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels, S = D->S, ldcat = (Lv + 1) * d;
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D), Lv = F->levels, S = D->S,
+            ldcat = (Lv + 1) * d;
   int rc;
   // level embeddings le[l] = level_embeds[l] + scale_embeds[l] (level_embeds: one [levels][d]
   // parameter, level 0's offset its base) and the level-0 input bias b_in + le[0]
@@ -1446,11 +1454,11 @@ int fractal_train_forward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F,
       return rc;
     // feed-forward: h = drop(gelu(x2 W1^T + b1)); s3 = x2 + h W2^T + b2, x3 = norm3(s3) (and the next
     // level's input x3 + le[l + 1] from the same epilogue)
-    if ((rc = linear_fwd(c, V.x2, d, c.P(V.w_ff1), c.P(V.b_ff1), V.h, ff, T, ff, d, EPI_GELU_DROP, nullptr, V.u, ff,
+    if ((rc = linear_fwd(c, V.x2, d, c.P(V.w_ff1), c.P(V.b_ff1), V.h, lf, T, ff, d, EPI_GELU_DROP, nullptr, V.u, lf,
                          1 << 30, 0, D->ff_offset, (uint32_t)l)))
       return rc;
     const bool last = l + 1 == Lv;
-    if ((rc = linear_res_ln_affine(c, V.h, ff, c.P(V.w_ff2), ff, c.P(V.b_ff2), V.x2, V.s3, c.P(V.ln3_w), c.P(V.ln3_b),
+    if ((rc = linear_res_ln_affine(c, V.h, lf, c.P(V.w_ff2), ff, c.P(V.b_ff2), V.x2, V.s3, c.P(V.ln3_w), c.P(V.ln3_b),
                                    V.x3, V.st3, last ? nullptr : F->level[l + 1].xin, last ? nullptr : F->le + (l + 1) * d)))
       return rc;
     // causal running mean; level projection into cat[:, l d:]; g <- g + mean W_gu^T + b_gu
@@ -1481,7 +1489,8 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
                    F->dcat && F->dhfa,
                "fractal train: missing backward scratch");
   const Ctx c{D, s, D->b * D->n};
-  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels, S = D->S, ldcat = (Lv + 1) * d;
+  const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D), Lv = F->levels, S = D->S,
+            ldcat = (Lv + 1) * d;
   const int64_t Td = (int64_t)T * d;
   int rc;
   SideStream& side = side_stream();
@@ -1563,21 +1572,21 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
       return rc;
     // feed-forward: s3 = x2 + h W2^T + b2
     if ((rc = Fk.fork())) return rc;
-    if ((rc = wgrad(cw, ds3, d, V.h, ff, c.G(V.w_ff2), T, d, ff, c.G(V.b_ff2)))) return rc;
+    if ((rc = wgrad(cw, ds3, d, V.h, lf, c.G(V.w_ff2), T, d, ff, c.G(V.b_ff2)))) return rc;
     e_ff2 = Fk.mark();
     if ((rc = Fk.wait(e_ff1))) return rc;
-    if ((rc = linear_dgrad(c, ds3, d, c.P(V.w_ff2), F->dz, ff, T, d, ff, EPI_MUL_AUX, V.u, ff))) return rc;
+    if ((rc = linear_dgrad(c, ds3, d, c.P(V.w_ff2), F->dz, lf, T, d, ff, EPI_MUL_AUX, V.u, lf))) return rc;
     if ((rc = Fk.fork())) return rc;
-    if ((rc = wgrad(cw, F->dz, ff, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
+    if ((rc = wgrad(cw, F->dz, lf, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
     e_ff1 = Fk.mark();
     // dx2 = ds3 + dz W1; norm2 backward -> ds2; norm1 backward (x1's whole gradient is ds2, the
     // residual path of s2) -> ds1: one launch (the LayerNorm backward of both in the epilogue)
     if ((rc = Fk.wait(e_go))) return rc;
     if ((rc = Fk.wait(e_out))) return rc;
     if (post2) {
-      if ((rc = dgrad_post_ln2(c, F->dz, ff, c.P(V.w_ff1), ds3, V, ds2, ds1))) return rc;
+      if ((rc = dgrad_post_ln2(c, F->dz, lf, c.P(V.w_ff1), ds3, V, ds2, ds1))) return rc;
     } else {
-      if ((rc = dgrad_res(c, F->dz, ff, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
+      if ((rc = dgrad_res(c, F->dz, lf, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
       if ((rc = ln_bwd(c, F->dxb, d, 1.f, nullptr, 0, V.s2, V.st2, c.P(V.ln2_w), nullptr, ds2, c.G(V.ln2_w),
                        c.G(V.ln2_b))))
         return rc;

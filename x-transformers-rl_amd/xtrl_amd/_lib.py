@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -95,7 +95,7 @@ class TrainDesc(C.Structure):
                                     'dzp', 'dewa', 'delta', 'part')]
                 + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer)),
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P),
-                   ('grad_events', C.POINTER(C.c_void_p))])
+                   ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32)])
 
 
 class FractalTrainLevel(C.Structure):

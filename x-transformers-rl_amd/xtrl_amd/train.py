@@ -16,6 +16,13 @@ from . import _lib as L
 from .params import FlatParams
 
 
+def ld_ff(ff):
+    """Row stride of the [T][ff] feed-forward activations (XtrlTrainDesc.ld_ff): ff + 16 when the row
+    is a multiple of 1 KiB (a power-of-two stride puts the FF1 epilogue's two store streams on the same
+    memory channels: 93 -> 82 us a launch at C3's ff = 1024, tools/epi_gemm_lab.cpp)."""
+    return ff + 16 if ff % 256 == 0 else ff
+
+
 def _off(flat, name):
     return flat.index[name][0] if name in flat.index else -1
 
@@ -68,6 +75,7 @@ class FusedTrainStep:
             return a0
 
         self.layers_py = []
+        self.ld_ff = lff = ld_ff(ff)
         layers = (L.TrainLayer * L_)()
         X = [E(T, d) for _ in range(L_ + 1)]
         max_qkv = 0
@@ -82,8 +90,8 @@ class FusedTrainStep:
             n_qkv = 3 * I + (I if c.gate_values else 0) + (H if mix else 0)
             max_qkv = max(max_qkv, n_qkv)
             bufs = dict(x_attn=X[li], x_ff=E(T, d), xn_attn=E(T, d), xn_ff=E(T, d), st_attn=E(T, 2), st_ff=E(T, 2),
-                        proj=E(T, n_qkv), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), u=E(T, ff),
-                        hd=E(T, ff))
+                        proj=E(T, n_qkv), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), u=E(T, lff),
+                        hd=E(T, lff))
             bufs['og'] = E(T, I) if c.gate_values else bufs['o']
             self.layers_py.append(bufs)
             Ly = layers[li]
@@ -102,7 +110,7 @@ class FusedTrainStep:
                         hp=E(T, ldp), z1=E(T, 4 * d), h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d),
                         raw=E(T, n_out), values=E(T, B), pred=E(T, 2 * (S + 1)), done=E(T),
                         d_raw=E(T, n_out), d_values=E(T, B), d_pred=E(T, 2 * (S + 1)), d_done=E(T),
-                        dx=E(T, d), dx2=E(T, d), dxn=E(T, d), dff=E(T, ff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
+                        dx=E(T, d), dx2=E(T, d), dxn=E(T, d), dff=E(T, lff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
         # the library states its own partial-sum needs (LayerNorm-backward row blocks, column sums)
@@ -128,6 +136,7 @@ class FusedTrainStep:
         D.part_floats = self.buf['part'].numel()
         D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
         D.layers = C.cast(layers, C.POINTER(L.TrainLayer))
+        D.ld_ff = lff
         self.D = D
 
     # ------------------------------------------------------------------------------------------
@@ -240,6 +249,7 @@ class FractalTrainStep(FusedTrainStep):
         le0 = off(enc + 'level_embedding.level_embeds')
         levels = (L.FractalTrainLevel * Lv)()
         self.levels_py = []
+        self.ld_ff = lff = ld_ff(ff)
         for li in range(Lv):
             pre = model.block_prefix(li)
             V = levels[li]
@@ -255,8 +265,8 @@ class FractalTrainStep(FusedTrainStep):
             V.w_proj, V.b_proj = off(enc + f'level_projections.{li}.weight'), off(enc + f'level_projections.{li}.bias')
             V.level_embed = le0 + li * d
             bufs = dict(xin=E(T, d), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), s1=E(T, d), x1=E(T, d),
-                        st1=E(T, 2), g=E(T, d), gv=E(T, I), s2=E(T, d), x2=E(T, d), st2=E(T, 2), h=E(T, ff),
-                        u=E(T, ff), s3=E(T, d), x3=E(T, d), st3=E(T, 2), mean=E(T, d))
+                        st1=E(T, 2), g=E(T, d), gv=E(T, I), s2=E(T, d), x2=E(T, d), st2=E(T, 2), h=E(T, lff),
+                        u=E(T, lff), s3=E(T, d), x3=E(T, d), st3=E(T, 2), mean=E(T, d))
             for k, t in bufs.items():
                 setattr(V, k, t.data_ptr())
             self.levels_py.append(bufs)
@@ -276,7 +286,7 @@ class FractalTrainStep(FusedTrainStep):
         self.scale_embeds = model.fractal_encoder.level_embedding.scale_embeds[:Lv].to(dev).float().contiguous()
         self.fbuf = dict(scale_embeds=self.scale_embeds, le=E(Lv, d), bias0=E(d), cat=E(T, (Lv + 1) * d),
                          hfa=E(T, 2 * d), dxa=E(T, d), dxb=E(T, d), ds=E(4, T, d), dmean=E(T, d), dga=E(T, d),
-                         dgb=E(T, d), dgv=E(T, I), dz=E(T, ff), dqkv=E(T, 3 * I), dob=E(T, I),
+                         dgb=E(T, d), dgv=E(T, I), dz=E(T, lff), dqkv=E(T, 3 * I), dob=E(T, I),
                          dcat=E(T, (Lv + 1) * d), dhfa=E(T, 2 * d))
 
         D = L.TrainDesc()
@@ -293,6 +303,7 @@ class FractalTrainStep(FusedTrainStep):
         D.part_floats = self.buf['part'].numel()
         D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
         D.layers = None
+        D.ld_ff = lff
         self.D = D
         Fd = L.FractalTrainDesc()
         Fd.levels = Lv
