@@ -24,17 +24,17 @@ static float time_us(const xtrl::GemmArgs& g, int epi) {
 int main() {
   const int M = 16384, N = 1024, K = 256;
   float *A, *B, *C, *D, *bias;
-  (void)hipMalloc(&A, (size_t)M * K * 4);
-  (void)hipMalloc(&B, (size_t)N * K * 4);
+  (void)hipMalloc(&A, (size_t)M * 768 * 4);
+  (void)hipMalloc(&B, (size_t)N * 768 * 4);
   (void)hipMalloc(&C, (size_t)M * (N + 64) * 4);
   (void)hipMalloc(&D, (size_t)M * (N + 64) * 4);
   (void)hipMalloc(&bias, (size_t)N * 4);
   {   // non-zero operands (zero inputs run at a higher clock and skip erf's slow branches)
-    std::vector<float> h((size_t)M * K);
+    std::vector<float> h((size_t)M * 768);
     uint32_t x = 1;
     for (auto& v : h) { x = x * 1664525u + 1013904223u; v = ((x >> 8) * 5.96e-8f - 0.5f) * 0.25f; }
     (void)hipMemcpy(A, h.data(), h.size() * 4, hipMemcpyHostToDevice);
-    (void)hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(B, h.data(), (size_t)N * 768 * 4, hipMemcpyHostToDevice);
   }
   (void)hipMemset(bias, 0, (size_t)N * 4);
   xtrl::GemmArgs g;
@@ -56,6 +56,15 @@ int main() {
            time_us(g, xtrl::EPI_NONE));
   }
   g.ldc = N; g.ld_aux_out = N;
-  // the derivative written to a second buffer only (no C store): the cost of each stream
+  // the heads' first layer (actor | critic, SiLU + saved derivative): K = 512 (C3) / 768 (C5)
+  g.drop_thresh = 0; g.drop_thresh8 = 0;
+  for (int k : {512, 768}) {
+    g.K = k; g.lda = k; g.ldb = k;
+    for (int pad : {0, 16}) {
+      g.ldc = N + pad; g.ld_aux_out = N + pad;
+      printf("silu_save K %d ld %4d  %7.1f us   (plain %7.1f us)\n", k, N + pad, time_us(g, xtrl::EPI_SILU_SAVE),
+             time_us(g, xtrl::EPI_NONE));
+    }
+  }
   return 0;
 }
