@@ -410,6 +410,11 @@ typedef struct XtrlTrainDesc {
    * >= ff, a multiple of 4; 0 = ff.  A stride off the 4 KiB power of two (e.g. ff + 16) spreads the
    * FF1 epilogue's two store streams over the memory channels */
   int ld_ff;
+  /* 1 (decoder step with the fused LayerNorms): the backward buffers the weight-gradient stream reads
+   * are per-layer planes — dx [L + 1][T][d], dx2 [L][T][d], dff [L][T][ld_ff], dproj [L][T][max n_qkv]
+   * — written once per backward, so the caller's stream never waits for the weight-gradient stream
+   * before the final join; 0: one plane each, reused layer by layer behind events */
+  int scratch_per_layer;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
@@ -457,11 +462,16 @@ typedef struct XtrlFractalTrainDesc {
   float* bias0;                    /* [d] scratch: input_embed.bias + le[0] */
   float* cat;                      /* [T][(levels + 1) d] level projections | final global state */
   float* hfa;                      /* [T][2d] ReLU(final_aggregation[0]) */
-  /* backward scratch [T][.] */
-  float* dxa; float* dxb; float* ds; float* dmean; float* dga; float* dgb;
-  float* dgv;                      /* [T][I] */
-  float* dz;                       /* [T][ff] */
-  float* dqkv;                     /* [T][3I] */
+  /* backward scratch; the planes a side-stream weight gradient reads are per level, so the main
+   * stream never waits for the side stream before the final join */
+  float* dxa; float* dxb; float* dmean;   /* [T][d] */
+  float* ds;                       /* [3 levels + 1][T][d]: per level the norm1 / norm2 / norm3 input
+                                    * gradients, then d features */
+  float* dga;                      /* [levels][T][d] gradient of each level's global state */
+  float* dgb;                      /* unused (NULL) */
+  float* dgv;                      /* [levels][T][I] */
+  float* dz;                       /* [levels][T][ld_ff] */
+  float* dqkv;                     /* [levels][T][3I] */
   float* dob;                      /* [T][I] */
   float* dcat;                     /* [T][(levels + 1) d] */
   float* dhfa;                     /* [T][2d] */

@@ -1150,8 +1150,10 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   if ((rc = heads_backward(c, cw, F))) return rc;
   // action-embedding gradient of the next-action input (and, below, of the previous action)
   // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
+  const bool per_layer = ln_fusable(D) && D->scratch_per_layer;
+  float* dx_top = per_layer ? D->dx + (int64_t)D->L * T * d : D->dx;   // (scratch_per_layer: slot L)
   if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
-                   c.P(D->ln_final), nullptr, D->dx, c.G(D->ln_final))))
+                   c.P(D->ln_final), nullptr, dx_top, c.G(D->ln_final))))
     return rc;
   if ((rc = bucket_done())) return rc;   // bucket 0: heads, state / gene embeddings, final norm
   // ---- decoder blocks, last to first.  Side events of the weight gradients whose dY buffer the
@@ -1164,27 +1166,44 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   // (read by the next FF2 weight gradient).
   const bool fuse = ln_fusable(D);
   XTRL_REQUIRE(!fuse || D->dx2, "train: fused LayerNorm backward needs dx2");
+  // scratch_per_layer (fused path): every buffer a side-stream weight gradient reads is a per-layer
+  // plane written once per backward — dx [L + 1][T][d] (slot l + 1: the gradient w.r.t. block l's
+  // output, slot 0 w.r.t. the embedding), dx2 [L][T][d] (w.r.t. block l's attention output), dff
+  // [L][T][ld_ff], dproj [L][T][max n_qkv] — so the main stream never waits for the side stream
+  // before the final join (the waits below are skipped)
+  const bool per = per_layer;
+  int maxq = 0;
+  for (int li = 0; li < D->L; ++li) maxq = std::max(maxq, D->layers[li].n_qkv);
+  const int64_t Td = (int64_t)T * d;
+  auto Gx = [&](int slot) { return per ? D->dx + slot * Td : D->dx; };
+  auto Gx2 = [&](int li) { return per ? D->dx2 + li * Td : D->dx2; };
+  auto Gff = [&](int li) { return per ? D->dff + (int64_t)li * T * lf : D->dff; };
+  auto Gpr = [&](int li) { return per ? D->dproj + (int64_t)li * T * maxq : D->dproj; };
+  auto wait = [&](hipEvent_t e) { return per ? XTRL_OK : F.wait(e); };
   hipEvent_t e_ff1 = nullptr, e_proj = nullptr, e_out_prev = nullptr;
   for (int li = D->L - 1; li >= 0; --li) {
     const XtrlTrainLayer& Ly = D->layers[li];
-    // FF2 (+ residual): dx is the gradient w.r.t. the block output
+    float* gout = Gx(li + 1);   // gradient w.r.t. the block output
+    float* dff = Gff(li);
+    float* dproj = Gpr(li);
+    // FF2 (+ residual)
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dx, d, Ly.hd, lf, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
+    if ((rc = wgrad(cw, gout, d, Ly.hd, lf, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
     hipEvent_t e_ff2 = F.mark();
-    if ((rc = F.wait(e_ff1))) return rc;
-    if ((rc = linear_dgrad(c, D->dx, d, c.P(Ly.w_ff2), D->dff, lf, T, d, ff, EPI_MUL_AUX, Ly.u, lf))) return rc;
+    if ((rc = wait(e_ff1))) return rc;
+    if ((rc = linear_dgrad(c, gout, d, c.P(Ly.w_ff2), dff, lf, T, d, ff, EPI_MUL_AUX, Ly.u, lf))) return rc;
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dff, lf, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = wgrad(cw, dff, lf, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
     e_ff1 = F.mark();
     float* xg = D->dx;   // gradient w.r.t. the attention block's output
     if (fuse) {
-      if ((rc = F.wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
-      if ((rc = dgrad_ln_bwd(c, D->dff, lf, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx2,
+      if ((rc = wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
+      if ((rc = dgrad_ln_bwd(c, dff, lf, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), gout, Gx2(li),
                              c.G(Ly.ln_ff))))
         return rc;
-      xg = D->dx2;
+      xg = Gx2(li);
     } else {
-      if ((rc = linear_dgrad(c, D->dff, lf, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+      if ((rc = linear_dgrad(c, dff, lf, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
       if ((rc = F.wait(e_ff2))) return rc;
       if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
         return rc;
@@ -1193,17 +1212,17 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = F.fork())) return rc;
     if ((rc = wgrad(cw, xg, d, D->gate_values ? Ly.og : Ly.o, I, c.G(Ly.w_out), T, d, I))) return rc;
     hipEvent_t e_out = F.mark();
-    if ((rc = F.wait(e_proj))) return rc;
+    if ((rc = wait(e_proj))) return rc;
     if (D->gate_values) {
       if ((rc = linear_dgrad(c, xg, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_DGATE, Ly.o, I, 1 << 30,
-                             Ly.proj + 3 * I, Ly.n_qkv, D->dproj + 3 * I, Ly.n_qkv)))
+                             Ly.proj + 3 * I, Ly.n_qkv, dproj + 3 * I, Ly.n_qkv)))
         return rc;
     } else {
       if ((rc = linear_dgrad(c, xg, d, c.P(Ly.w_out), D->dog, I, T, d, I, EPI_NONE))) return rc;
     }
     const AttnProblem ap = attn_problem(c, Ly, li);
-    if ((rc = attn_bwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse, D->dog, D->dproj, D->dproj + I,
-                          D->dproj + 2 * I, D->delta, s)))
+    if ((rc = attn_bwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse, D->dog, dproj, dproj + I,
+                          dproj + 2 * I, D->delta, s)))
       return rc;
     const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
     const bool any_mix = [&] {
@@ -1214,24 +1233,24 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     // dvfirst: the first mixing layer processed (the deepest) writes, the others accumulate
     bool deeper_mix = false;
     for (int j = li + 1; j < D->L; ++j) deeper_mix = deeper_mix || D->layers[j].mix;
-    PrepBwdArgs pb{D->dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
+    PrepBwdArgs pb{dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
                    Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
                    (li == 0 ? any_mix : deeper_mix) ? 1 : 0};
     hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, D->dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
+    if ((rc = wgrad(cw, dproj, Ly.n_qkv, Ly.xn_attn, d, c.G(Ly.w_proj), T, Ly.n_qkv, d, c.G(Ly.b_proj), 3 * I)))
       return rc;
     e_proj = F.mark();
     if (fuse) {
-      if ((rc = F.wait(e_ff2))) return rc;   // this block's FF2 weight gradient read dx
-      if ((rc = dgrad_ln_bwd(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), Ly.n_qkv, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn),
-                             D->dx2, D->dx, c.G(Ly.ln_attn))))
+      if ((rc = wait(e_ff2))) return rc;   // this block's FF2 weight gradient read dx
+      if ((rc = dgrad_ln_bwd(c, dproj, Ly.n_qkv, c.P(Ly.w_proj), Ly.n_qkv, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn),
+                             Gx2(li), Gx(li), c.G(Ly.ln_attn))))
         return rc;
       e_out_prev = e_out;
     } else {
-      if ((rc = linear_dgrad(c, D->dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
+      if ((rc = linear_dgrad(c, dproj, Ly.n_qkv, c.P(Ly.w_proj), D->dxn, d, T, Ly.n_qkv, d, EPI_NONE))) return rc;
       if ((rc = F.wait(e_out))) return rc;
       if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn), D->dx, D->dx,
                        c.G(Ly.ln_attn))))
@@ -1478,15 +1497,15 @@ int fractal_train_forward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F,
   return XTRL_OK;
 }
 
-// events one fractal backward takes (forks + marks): heads 4, action embedding 1, aggregation 1 + 2,
-// per level 7 forks + 7 marks, input embedding 1 + 1, final join 1
-constexpr size_t fractal_events_needed(int Lv) { return 14 * (size_t)Lv + 11; }
+// events one fractal backward takes: forks — heads 4, action embedding 1, aggregation 1, 7 per level,
+// input embedding 1 — and the final join's mark
+constexpr size_t fractal_events_needed(int Lv) { return 7 * (size_t)Lv + 8; }
 
 int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F, hipStream_t s) {
   if (int rc = validate_fractal(D, F)) return rc;
   XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "fractal train: missing loss gradients");
-  XTRL_REQUIRE(F->dxa && F->dxb && F->ds && F->dmean && F->dga && F->dgb && F->dgv && F->dz && F->dqkv && F->dob &&
-                   F->dcat && F->dhfa,
+  XTRL_REQUIRE(F->dxa && F->dxb && F->ds && F->dmean && F->dga && F->dgv && F->dz && F->dqkv && F->dob && F->dcat &&
+                   F->dhfa,
                "fractal train: missing backward scratch");
   const Ctx c{D, s, D->b * D->n};
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D), Lv = F->levels, S = D->S,
@@ -1504,7 +1523,9 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
   const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
   if ((rc = heads_backward(c, cw, Fk))) return rc;
   // d features = frac * dac[:, :d] + dewa[:, :d]  (frac_gradient: the actor / critic share scaled)
-  float* dfeat = F->ds + 3 * Td;   // ds holds 4 [T][d] planes: LN1 / LN2 / LN3 input gradients, d features
+  // every backward scratch plane a side-stream weight gradient reads is written once per backward
+  // (per-level planes): the main stream never waits for the side stream before the final join
+  float* dfeat = F->ds + 3 * (int64_t)Lv * Td;   // after the levels' [3][T][d] planes
   if ((rc = rows_axpb(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, dfeat, d, T, d))) return rc;
   // next-action embedding
   if (D->continuous) {
@@ -1534,59 +1555,50 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
   }
   // final aggregation: feat = hfa W_fa2^T + b; hfa = ReLU(cat W_fa0^T + b)
   if ((rc = wgrad(cw, dfeat, d, F->hfa, 2 * d, c.G(F->w_fa2), T, d, 2 * d, c.G(F->b_fa2)))) return rc;
-  Fk.mark();
   if ((rc = linear_dgrad(c, dfeat, d, c.P(F->w_fa2), F->dhfa, 2 * d, T, d, 2 * d, EPI_MASK_POS, F->hfa, 2 * d))) return rc;
   if ((rc = Fk.fork())) return rc;
   if ((rc = wgrad(cw, F->dhfa, 2 * d, F->cat, ldcat, c.G(F->w_fa0), T, 2 * d, ldcat, c.G(F->b_fa0)))) return rc;
-  Fk.mark();
   if ((rc = linear_dgrad(c, F->dhfa, 2 * d, c.P(F->w_fa0), F->dcat, ldcat, T, 2 * d, ldcat, EPI_NONE))) return rc;
   // levels, last to first.  dgn: gradient of g_{l+1} (the final g: cat's last d columns); dxn:
-  // gradient of x3_l from level l + 1's input (none for the last level).  Scratch a side-stream
-  // weight gradient still reads is not overwritten before its event: the LN planes of ds, dz, dgv and
-  // dqkv by the next (shallower) level, the dg buffers (alternating) two levels on.
+  // gradient of x3_l from level l + 1's input (none for the last level).
   // the chained post-norm LayerNorm backward epilogue (XTRL_FUSED_LN=0: separate launches)
   const bool post2 = ln_fusable_fractal(D);
   const float* dgn = F->dcat + Lv * d;
   int lddgn = ldcat;
   const float* dxn = nullptr;
-  float* ds1 = F->ds;
-  float* ds2 = F->ds + Td;
-  float* ds3 = F->ds + 2 * Td;
-  hipEvent_t e_gu_prev = nullptr, e_ff2 = nullptr, e_ff1 = nullptr, e_go = nullptr,
-             e_gv = nullptr, e_out = nullptr, e_qkv = nullptr;
   for (int l = Lv - 1; l >= 0; --l) {
     const XtrlFractalTrainLevel& V = F->level[l];
+    float* ds1 = F->ds + 3 * (int64_t)l * Td;   // this level's planes
+    float* ds2 = ds1 + Td;
+    float* ds3 = ds1 + 2 * Td;
+    float* dz = F->dz + (int64_t)l * T * lf;
+    float* dgv = F->dgv + (int64_t)l * T * I;
+    float* dqkv = F->dqkv + (int64_t)l * T * 3 * I;
+    float* dgc = F->dga + (int64_t)l * Td;
     // g_{l+1} = g_l + mean W_gu^T + b_gu;  cat[:, l d:] = mean W_p^T + b_p
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, dgn, lddgn, V.mean, d, c.G(F->w_gu), T, d, d, c.G(F->b_gu)))) return rc;
     if ((rc = wgrad(cw, F->dcat + l * d, ldcat, V.mean, d, c.G(V.w_proj), T, d, d, c.G(V.b_proj)))) return rc;
-    const hipEvent_t e_gu = Fk.mark();
     if ((rc = linear_dgrad(c, dgn, lddgn, c.P(F->w_gu), F->dmean, d, T, d, d, EPI_NONE))) return rc;
     if ((rc = dgrad_res(c, F->dcat + l * d, ldcat, c.P(V.w_proj), d, d, F->dmean, d, F->dmean, d))) return rc;
     // mean = causal running mean of x3: dx3 = dxn + reverse scan of dmean / (t + 1)
     if ((rc = causal_mean(c, F->dmean, d, dxn, d, F->dxa, d, true))) return rc;
     // norm3 backward -> ds3 (d gamma, d beta)
-    if ((rc = Fk.wait(e_ff2))) return rc;
     if ((rc = ln_bwd(c, F->dxa, d, 1.f, nullptr, 0, V.s3, V.st3, c.P(V.ln3_w), nullptr, ds3, c.G(V.ln3_w),
                      c.G(V.ln3_b))))
       return rc;
     // feed-forward: s3 = x2 + h W2^T + b2
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, ds3, d, V.h, lf, c.G(V.w_ff2), T, d, ff, c.G(V.b_ff2)))) return rc;
-    e_ff2 = Fk.mark();
-    if ((rc = Fk.wait(e_ff1))) return rc;
-    if ((rc = linear_dgrad(c, ds3, d, c.P(V.w_ff2), F->dz, lf, T, d, ff, EPI_MUL_AUX, V.u, lf))) return rc;
+    if ((rc = linear_dgrad(c, ds3, d, c.P(V.w_ff2), dz, lf, T, d, ff, EPI_MUL_AUX, V.u, lf))) return rc;
     if ((rc = Fk.fork())) return rc;
-    if ((rc = wgrad(cw, F->dz, lf, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
-    e_ff1 = Fk.mark();
+    if ((rc = wgrad(cw, dz, lf, V.x2, d, c.G(V.w_ff1), T, ff, d, c.G(V.b_ff1)))) return rc;
     // dx2 = ds3 + dz W1; norm2 backward -> ds2; norm1 backward (x1's whole gradient is ds2, the
     // residual path of s2) -> ds1: one launch (the LayerNorm backward of both in the epilogue)
-    if ((rc = Fk.wait(e_go))) return rc;
-    if ((rc = Fk.wait(e_out))) return rc;
     if (post2) {
-      if ((rc = dgrad_post_ln2(c, F->dz, lf, c.P(V.w_ff1), ds3, V, ds2, ds1))) return rc;
+      if ((rc = dgrad_post_ln2(c, dz, lf, c.P(V.w_ff1), ds3, V, ds2, ds1))) return rc;
     } else {
-      if ((rc = dgrad_res(c, F->dz, lf, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
+      if ((rc = dgrad_res(c, dz, lf, c.P(V.w_ff1), ff, d, ds3, d, F->dxb, d))) return rc;
       if ((rc = ln_bwd(c, F->dxb, d, 1.f, nullptr, 0, V.s2, V.st2, c.P(V.ln2_w), nullptr, ds2, c.G(V.ln2_w),
                        c.G(V.ln2_b))))
         return rc;
@@ -1597,42 +1609,31 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
     // cross-attention: s2 = x1 + gv W_go^T, gv = g W_gv^T
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, ds2, d, V.gv, I, c.G(V.w_go), T, d, I))) return rc;
-    e_go = Fk.mark();
-    if ((rc = Fk.wait(e_gv))) return rc;
-    if ((rc = linear_dgrad(c, ds2, d, c.P(V.w_go), F->dgv, I, T, d, I, EPI_NONE))) return rc;
+    if ((rc = linear_dgrad(c, ds2, d, c.P(V.w_go), dgv, I, T, d, I, EPI_NONE))) return rc;
     if ((rc = Fk.fork())) return rc;
-    if ((rc = wgrad(cw, F->dgv, I, V.g, d, c.G(V.w_gv), T, I, d))) return rc;
-    e_gv = Fk.mark();
-    // dg_l = dg_{l+1} + dgv W_gv into the dg buffer that held dg_{l+2}, which level l + 1's
-    // global-update weight gradient (event e_gu_prev) was the last to read
-    float* dgc = ((Lv - 1 - l) & 1) ? F->dgb : F->dga;
-    if ((rc = Fk.wait(e_gu_prev))) return rc;
-    if ((rc = dgrad_res(c, F->dgv, I, c.P(V.w_gv), I, d, dgn, lddgn, dgc, d))) return rc;
+    if ((rc = wgrad(cw, dgv, I, V.g, d, c.G(V.w_gv), T, I, d))) return rc;
+    // dg_l = dg_{l+1} + dgv W_gv
+    if ((rc = dgrad_res(c, dgv, I, c.P(V.w_gv), I, d, dgn, lddgn, dgc, d))) return rc;
     // self-attention: s1 = x_in + o W_out^T
     if ((rc = Fk.fork())) return rc;
     if ((rc = wgrad(cw, ds1, d, V.o, I, c.G(V.w_out), T, d, I))) return rc;
-    e_out = Fk.mark();
     if ((rc = linear_dgrad(c, ds1, d, c.P(V.w_out), F->dob, I, T, d, I, EPI_NONE))) return rc;
-    if ((rc = Fk.wait(e_qkv))) return rc;
     const AttnProblem ap = fractal_attn(c, l);
-    if ((rc = attn_bwd_ex(ap, V.qkv, V.qkv + I, V.qkv + 2 * I, V.o, V.lse, F->dob, F->dqkv, F->dqkv + I, F->dqkv + 2 * I,
+    if ((rc = attn_bwd_ex(ap, V.qkv, V.qkv + I, V.qkv + 2 * I, V.o, V.lse, F->dob, dqkv, dqkv + I, dqkv + 2 * I,
                           D->delta, s)))
       return rc;
     if ((rc = Fk.fork())) return rc;
-    if ((rc = wgrad(cw, F->dqkv, 3 * I, V.xin, d, c.G(V.w_qkv), T, 3 * I, d))) return rc;
-    e_qkv = Fk.mark();
+    if ((rc = wgrad(cw, dqkv, 3 * I, V.xin, d, c.G(V.w_qkv), T, 3 * I, d))) return rc;
     // d x_in = ds1 + dqkv W_qkv; the level embedding's gradient is its column sum
-    if ((rc = dgrad_res(c, F->dqkv, 3 * I, c.P(V.w_qkv), 3 * I, d, ds1, d, F->dxa, d))) return rc;
+    if ((rc = dgrad_res(c, dqkv, 3 * I, c.P(V.w_qkv), 3 * I, d, ds1, d, F->dxa, d))) return rc;
     if ((rc = colsum(c, F->dxa, d, T, d, c.G(V.level_embed)))) return rc;
     dxn = F->dxa;
     dgn = dgc;
     lddgn = d;
-    e_gu_prev = e_gu;
   }
   // input embedding (x_in,0 = state W_in^T + b_in + le[0]) and global_state_init (g_0 on every row)
   if ((rc = Fk.fork())) return rc;
   if ((rc = wgrad(cw, F->dxa, d, D->swr, S + 1, c.G(D->w_pin), T, d, S, c.G(F->b_in)))) return rc;
-  Fk.mark();
   if ((rc = colsum(c, dgn, lddgn, T, d, c.G(F->g_init)))) return rc;
   if ((rc = splitk_flush(skq, cw.s))) return rc;
   if ((rc = Fk.wait(Fk.mark()))) return rc;

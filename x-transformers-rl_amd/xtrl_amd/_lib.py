@@ -95,7 +95,8 @@ class TrainDesc(C.Structure):
                                     'dzp', 'dewa', 'delta', 'part')]
                 + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer)),
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P),
-                   ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32)])
+                   ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32),
+                   ('scratch_per_layer', I32)])
 
 
 class FractalTrainLevel(C.Structure):
@@ -108,7 +109,7 @@ class FractalTrainLevel(C.Structure):
 class FractalTrainDesc(C.Structure):
     _fields_ = ([('levels', I32)]
                 + [(n, I64) for n in ('b_in', 'g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2')]
-                + [(n, P) for n in ('scale_embeds', 'le', 'bias0', 'cat', 'hfa', 'dxa', 'dxb', 'ds', 'dmean',
+                + [(n, P) for n in ('scale_embeds', 'le', 'bias0', 'cat', 'hfa', 'dxa', 'dxb', 'dmean', 'ds',
                                     'dga', 'dgb', 'dgv', 'dz', 'dqkv', 'dob', 'dcat', 'dhfa')]
                 + [('level', C.POINTER(FractalTrainLevel))])
 

@@ -110,7 +110,8 @@ class FusedTrainStep:
                         hp=E(T, ldp), z1=E(T, 4 * d), h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d),
                         raw=E(T, n_out), values=E(T, B), pred=E(T, 2 * (S + 1)), done=E(T),
                         d_raw=E(T, n_out), d_values=E(T, B), d_pred=E(T, 2 * (S + 1)), d_done=E(T),
-                        dx=E(T, d), dx2=E(T, d), dxn=E(T, d), dff=E(T, lff), dproj=E(T, max_qkv), dog=E(T, I), dvfirst=E(T, I),
+                        dx=E(L_ + 1, T, d), dx2=E(L_, T, d), dxn=E(T, d), dff=E(L_, T, lff), dproj=E(L_, T, max_qkv),
+                        dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
         # the library states its own partial-sum needs (LayerNorm-backward row blocks, column sums)
@@ -137,6 +138,7 @@ class FusedTrainStep:
         D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
         D.layers = C.cast(layers, C.POINTER(L.TrainLayer))
         D.ld_ff = lff
+        D.scratch_per_layer = 1   # per-layer backward planes (no mid-backward stream waits)
         self.D = D
 
     # ------------------------------------------------------------------------------------------
@@ -285,8 +287,8 @@ class FractalTrainStep(FusedTrainStep):
         self.stats = torch.zeros(L.LOSS_STATS, **f32)
         self.scale_embeds = model.fractal_encoder.level_embedding.scale_embeds[:Lv].to(dev).float().contiguous()
         self.fbuf = dict(scale_embeds=self.scale_embeds, le=E(Lv, d), bias0=E(d), cat=E(T, (Lv + 1) * d),
-                         hfa=E(T, 2 * d), dxa=E(T, d), dxb=E(T, d), ds=E(4, T, d), dmean=E(T, d), dga=E(T, d),
-                         dgb=E(T, d), dgv=E(T, I), dz=E(T, lff), dqkv=E(T, 3 * I), dob=E(T, I),
+                         hfa=E(T, 2 * d), dxa=E(T, d), dxb=E(T, d), ds=E(3 * Lv + 1, T, d), dmean=E(T, d),
+                         dga=E(Lv, T, d), dgv=E(Lv, T, I), dz=E(Lv, T, lff), dqkv=E(Lv, T, 3 * I), dob=E(T, I),
                          dcat=E(T, (Lv + 1) * d), dhfa=E(T, 2 * d))
 
         D = L.TrainDesc()
