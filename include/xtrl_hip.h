@@ -227,26 +227,29 @@ int xtrl_dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, void
  * (the XtrlDecodeDesc's compaction, embedding (state_only = 1, b_pin = input_embed.bias + level
  * embedding 0), heads and sampling are reused; its layers[l] hold level l's K/V caches and
  * n_qkv = 3 I):
- *   for each level l: x <- x + level_embed[l] (l > 0)
- *     x1 = LN1(x + W_out attn(W_q x, W_k x, W_v x))      causal self-attention over the cache
- *     x2 = LN2(x1 + W_out_g W_v_g g)                    cross-attention to the one-token global state
- *     x3 = LN3(x2 + FF(x2))                             (softmax over one key == 1)
- *     m  = mean over this episode's steps 0..t of x3    (running sums per episode slot)
- *     g <- g + W_gu m + b_gu;  p_l = W_p,l m + b_p,l    (global state update, level projection)
- *     x <- x3
+ *   for each level l:
+ *     c  = W_c,l g  (W_c = W_out,g W_v,g; level 0: the constant row c0)   cross-attention to the one-token
+ *                                                                           global state (softmax over one key)
+ *     x2 = LN2(LN1(x + W_out attn(W_q x, W_k x, W_v x)) + c)               causal self-attention over the
+ *                                                                           cache; both add + LayerNorms in one
+ *     x3 = LN3(x2 + FF(x2)); m = mean over this episode's steps 0..t of x3 (running sums per slot);
+ *     x <- x3 + level_embed[l+1]                                           one launch
+ *     [g | p_l] = [g | 0] + m [W_gu; W_p,l]^T + [b_gu; b_p,l]               one GEMM
  *   features = W_fa2 ReLU(W_fa0 [p_0 | ... | p_{L-1} | g] + b) + b  -> ac_in[:, 0:d] -> heads
  * GEMM weights fragment-packed (xtrl_dgemm_pack); LayerNorms nn.LayerNorm (eps, weight, bias). */
 typedef struct XtrlFractalLevel {
   const float* w_qkv;                       /* [3I][d]  self_attn.to_q | to_k | to_v */
   const float* w_out;                       /* [d][I]   self_attn.to_out */
   const float* ln1_w; const float* ln1_b;   /* [d] norm1 */
-  const float* w_gv;                        /* [I][d]   global_attn.to_v */
-  const float* w_go;                        /* [d][I]   global_attn.to_out */
+  const float* w_c;                         /* [d][d]   global_attn.to_out . to_v (the one-key cross-attention,
+                                             *          one operand: W_out W_v g) */
   const float* ln2_w; const float* ln2_b;
   const float* w_ff1; const float* b_ff1;   /* [ff][d], [ff] */
   const float* w_ff2; const float* b_ff2;   /* [d][ff], [d] */
   const float* ln3_w; const float* ln3_b;
-  const float* w_proj; const float* b_proj; /* level_projections[l] [d][d], [d] */
+  const float* w_pg; const float* b_pg;     /* [2d][d], [2d]: global_state_update | level_projections[l] — one
+                                             * GEMM over the running mean: columns [0, d) update g in place,
+                                             * [d, 2d) the level's projection into allf */
   const float* level_emb;                   /* [d] level_embeds[l] + scale_embeds[l] (added for l > 0) */
   float* sums;                              /* [E][d] running sum of this level's outputs per episode slot */
 } XtrlFractalLevel;
@@ -255,12 +258,16 @@ typedef struct XtrlFractalDesc {
   int levels;
   float ln_eps;
   const XtrlFractalLevel* level;            /* HOST array of `levels` descriptors */
-  const float* g_init;                      /* [d] global_state_init */
-  const float* w_gu; const float* b_gu;     /* global_state_update [d][d], [d] */
+  const float* g_init;                      /* [2d] global_state_init | zeros */
+  const float* c0;                          /* [d] level 0's cross-attention row W_c,0 g_init (every row) */
   const float* w_fa0; const float* b_fa0;   /* final_aggregation.0 [2d][(L+1) d], [2d] */
   const float* w_fa2; const float* b_fa2;   /* final_aggregation.2 [d][2d], [d] */
-  float* g;                                 /* [E][d] global state of the step's rows */
-  float* x1; float* x2; float* x3; float* mean;   /* [E][d] */
+  float* g;                                 /* [E][2d] global state of the step's rows | zeros (the columns the
+                                             * fused update GEMM's residual reads for its projection half) */
+  float* c2;                                /* [E][d] cross-attention rows (levels > 0) */
+  float* tmp;                               /* [E][d] projection outputs before their add + LayerNorm */
+  float* x2;                                /* [E][d] norm2 output (the feed-forward input) */
+  float* mean;                              /* [E][d] the level's running mean */
   float* allf;                              /* [E][(L+1) d] */
   float* hagg;                              /* [E][2d] */
 } XtrlFractalDesc;

@@ -741,17 +741,83 @@ __global__ __launch_bounds__(256) void k_copy_rows(const float* src, int lds, fl
   if (r < M) dst[(int64_t)r * ldd + c] = src[(int64_t)r * lds + c];
 }
 
-__global__ __launch_bounds__(256) void k_running_mean(const XtrlDecodeDesc D, int t, const float* x, float* sums,
-                                                      float* mean) {
-  const int d = D.d;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int r = (int)(i / d), c = (int)(i - (int64_t)r * d);
+// fractal body, the post-norm rows of one level (wave per live row, the row in registers, nn.LayerNorm
+// as k_add_layernorm: two-pass variance, eps): x2 = LN2(LN1(x + o) + c) with c the row's
+// cross-attention read (ldc 0: one row for every live row)
+constexpr int FR_MAXF = 8;   // floats per lane: d <= 512
+__device__ __forceinline__ void fr_layernorm(float (&v)[FR_MAXF], int lane, int d, float eps, const float* g,
+                                             const float* b) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) s += v[j];
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    const float dl = c < d ? v[j] - mean : 0.f;
+    q += dl * dl;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + eps);
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < d ? (v[j] - mean) * rstd * g[c] + b[c] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fr_ln12(const XtrlDecodeDesc D, int t, const float* o, const float* cx,
+                                                 int ldcx, const float* g1, const float* b1, const float* g2,
+                                                 const float* b2, float* x2, float eps) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, d = D.d;
+  if (r >= D.live_count[t & 1]) return;
+  const float* xr = D.x + (int64_t)r * d;
+  const float* orow = o + (int64_t)r * d;
+  const float* crow = cx + (int64_t)r * ldcx;
+  float v[FR_MAXF], cv[FR_MAXF];
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < d ? xr[c] + orow[c] : 0.f;
+    cv[j] = c < d ? crow[c] : 0.f;
+  }
+  fr_layernorm(v, lane, d, eps, g1, b1);
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) v[j] += cv[j];
+  fr_layernorm(v, lane, d, eps, g2, b2);
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    if (c < d) x2[(int64_t)r * d + c] = v[j];
+  }
+}
+
+// x3 = LN3(x2 + f); the episode slot's running sum of x3 (restarting at t = 0) and the running mean
+// of the live row; the next level's input x3 + level_embed[l + 1] into D.x (xnext NULL: last level)
+__global__ __launch_bounds__(256) void k_fr_ln3_tail(const XtrlDecodeDesc D, int t, const float* x2, const float* f,
+                                                     const float* g3, const float* b3, float* sums, float* mean,
+                                                     const float* le_next, float eps) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, d = D.d;
   if (r >= D.live_count[t & 1]) return;
   const int e = rows_of(D, t)[r];
-  const float prev = sums[(int64_t)e * d + c];
-  const float s = (t > 0 ? prev : 0.f) + x[(int64_t)r * d + c];   // step 0 starts the episode's sum
-  sums[(int64_t)e * d + c] = s;
-  mean[(int64_t)r * d + c] = s / (float)(t + 1);
+  float v[FR_MAXF], sp[FR_MAXF];
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < d ? x2[(int64_t)r * d + c] + f[(int64_t)r * d + c] : 0.f;
+    sp[j] = (c < d && t > 0) ? sums[(int64_t)e * d + c] : 0.f;   // step 0 starts the episode's sum
+  }
+  fr_layernorm(v, lane, d, eps, g3, b3);
+#pragma unroll
+  for (int j = 0; j < FR_MAXF; ++j) {
+    const int c = lane + 64 * j;
+    if (c < d) {
+      const float sm = sp[j] + v[j];
+      sums[(int64_t)e * d + c] = sm;
+      mean[(int64_t)r * d + c] = sm / (float)(t + 1);
+      if (le_next) D.x[(int64_t)r * d + c] = v[j] + le_next[c];
+    }
+  }
 }
 
 int check_desc(const XtrlDecodeDesc* D) {
@@ -1176,50 +1242,45 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
     XTRL_REQUIRE(!D->layers[l].w_out_t, "fractal_decode: the attention output feeds a LayerNorm (w_out_t must be NULL)");
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "fractal_decode: t=%d outside [0, %d)", t, D->Tmax);
   XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs &&
-                   D->n_qkv == 3 * D->H * D->dh && D->d <= 512,
+                   D->n_qkv == 3 * D->H * D->dh && D->d <= 64 * FR_MAXF,
                "fractal_decode: the descriptor must describe plain attention (n_qkv = 3 I) with state_only = 1");
+  XTRL_REQUIRE(F->g_init && F->c0 && F->g && F->c2 && F->tmp && F->x2 && F->mean && F->allf && F->hagg,
+               "fractal_decode: missing buffers");
   const int E = D->E, d = D->d, I = D->H * D->dh, ff = D->ff, Lv = F->levels;
-  const int64_t Ed = (int64_t)E * d;
+  const dim3 rows_grid((E + 3) / 4), rows_blk(256);
   if (int rc = launch_embed(D, t, nullptr, s)) return rc;   // x = W_in s + b_in + le_0
-  rows_add_launch(nullptr, 0, F->g_init, F->g, d, E, d, s);   // per-step global state of every row starts at init
-  XTRL_LAUNCHED("rows_add");
   int rc;
   for (int l = 0; l < Lv; ++l) {
     const XtrlFractalLevel& Q = F->level[l];
-    const float* xin = D->x;
-    if (l > 0) {   // the previous level's output plus this level's embedding
-      rows_add_launch(F->x3, d, Q.level_emb, D->x, d, E, d, s);
-      XTRL_LAUNCHED("rows_add");
-    }
-    if ((rc = dproj(D, t, xin, d, Q.w_qkv, d, nullptr, nullptr, 0, nullptr, 0, D->qkv, D->n_qkv, 3 * I, EPI_NONE, s)))
+    // the cross-attention read of the global state (level 0: the same row c0 for every row)
+    if (l > 0 &&
+        (rc = dproj(D, t, F->g, 2 * d, Q.w_c, d, nullptr, nullptr, 0, nullptr, 0, F->c2, d, d, EPI_NONE, s)))
+      return rc;
+    if ((rc = dproj(D, t, D->x, d, Q.w_qkv, d, nullptr, nullptr, 0, nullptr, 0, D->qkv, D->n_qkv, 3 * I, EPI_NONE, s)))
       return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
     if ((rc = launch_attn_decode(D, l, t, s))) return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
-    if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s))) return rc;
-    add_layernorm_launch(xin, d, F->mean, d, Q.ln1_w, Q.ln1_b, F->x1, d, E, d, F->ln_eps, s);   // x1 = LN1(x + attn)
-    XTRL_LAUNCHED("add_layernorm");
-    // cross-attention to the one-token global state: W_out (W_v g)
-    if ((rc = dproj(D, t, F->g, d, Q.w_gv, d, nullptr, nullptr, 0, nullptr, 0, D->att, I, I, EPI_NONE, s))) return rc;
-    if ((rc = dproj(D, t, D->att, I, Q.w_go, I, nullptr, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s))) return rc;
-    add_layernorm_launch(F->x1, d, F->mean, d, Q.ln2_w, Q.ln2_b, F->x2, d, E, d, F->ln_eps, s);
-    XTRL_LAUNCHED("add_layernorm");
+    if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->tmp, d, d, EPI_NONE, s))) return rc;
+    // x2 = LN2(LN1(x + attn) + c)
+    hipLaunchKernelGGL(k_fr_ln12, rows_grid, rows_blk, 0, s, *D, t, F->tmp, l > 0 ? F->c2 : F->c0, l > 0 ? d : 0,
+                       Q.ln1_w, Q.ln1_b, Q.ln2_w, Q.ln2_b, F->x2, F->ln_eps);
+    XTRL_LAUNCHED("fractal ln12");
     if ((rc = dproj(D, t, F->x2, d, Q.w_ff1, d, Q.b_ff1, nullptr, 0, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
       return rc;
-    if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, nullptr, 0, F->mean, d, d, EPI_NONE, s)))
+    if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, nullptr, 0, F->tmp, d, d, EPI_NONE, s)))
       return rc;
-    add_layernorm_launch(F->x2, d, F->mean, d, Q.ln3_w, Q.ln3_b, F->x3, d, E, d, F->ln_eps, s);
-    XTRL_LAUNCHED("add_layernorm");
-    hipLaunchKernelGGL(k_running_mean, dim3((unsigned)((Ed + 255) / 256)), dim3(256), 0, s, *D, t, F->x3, Q.sums,
-                       F->mean);
-    XTRL_LAUNCHED("running_mean");
-    // level projection of the running mean, then the global-state update (after the block used g)
-    if ((rc = dproj(D, t, F->mean, d, Q.w_proj, d, Q.b_proj, nullptr, 0, nullptr, 0, F->allf + (int64_t)l * d,
-                    (Lv + 1) * d, d, EPI_NONE, s)))
+    // x3 = LN3(x2 + FF), its running mean, the next level's input
+    hipLaunchKernelGGL(k_fr_ln3_tail, rows_grid, rows_blk, 0, s, *D, t, F->x2, F->tmp, Q.ln3_w, Q.ln3_b, Q.sums, F->mean,
+                       l + 1 < Lv ? F->level[l + 1].level_emb : nullptr, F->ln_eps);
+    XTRL_LAUNCHED("fractal ln3 tail");
+    // [g | p_l] = [g | 0] + mean [W_gu; W_p,l]^T + [b_gu; b_p,l]: g in place (level 0 from g_init),
+    // the level projection into allf
+    if ((rc = dproj(D, t, F->mean, d, Q.w_pg, d, Q.b_pg, nullptr, 0, l > 0 ? F->g : F->g_init, l > 0 ? 2 * d : 0, F->g,
+                    2 * d, 2 * d, EPI_NONE, s, nullptr, d, F->allf + (int64_t)l * d, (Lv + 1) * d)))
       return rc;
-    if ((rc = dproj(D, t, F->mean, d, F->w_gu, d, F->b_gu, nullptr, 0, F->g, d, F->g, d, d, EPI_NONE, s))) return rc;
   }
-  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((Ed + 255) / 256)), dim3(256), 0, s, F->g, d,
+  hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)(((int64_t)E * d + 255) / 256)), dim3(256), 0, s, F->g, 2 * d,
                      F->allf + (int64_t)Lv * d, (Lv + 1) * d, E, d);
   XTRL_LAUNCHED("copy_rows");
   // final aggregation -> the heads' input row (no final norm: the encoder has none)

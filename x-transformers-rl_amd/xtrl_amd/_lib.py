@@ -53,14 +53,14 @@ class DecodeDesc(C.Structure):
 
 
 class FractalLevel(C.Structure):
-    _fields_ = [(n, P) for n in ('w_qkv', 'w_out', 'ln1_w', 'ln1_b', 'w_gv', 'w_go', 'ln2_w', 'ln2_b', 'w_ff1', 'b_ff1',
-                                 'w_ff2', 'b_ff2', 'ln3_w', 'ln3_b', 'w_proj', 'b_proj', 'level_emb', 'sums')]
+    _fields_ = [(n, P) for n in ('w_qkv', 'w_out', 'ln1_w', 'ln1_b', 'w_c', 'ln2_w', 'ln2_b', 'w_ff1', 'b_ff1',
+                                 'w_ff2', 'b_ff2', 'ln3_w', 'ln3_b', 'w_pg', 'b_pg', 'level_emb', 'sums')]
 
 
 class FractalDesc(C.Structure):
     _fields_ = ([('levels', I32), ('ln_eps', F32), ('level', C.POINTER(FractalLevel))]
-                + [(n, P) for n in ('g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2', 'g', 'x1', 'x2', 'x3',
-                                    'mean', 'allf', 'hagg')])
+                + [(n, P) for n in ('g_init', 'c0', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2', 'g', 'c2', 'tmp', 'x2', 'mean',
+                                    'allf', 'hagg')])
 
 
 class LossDesc(C.Structure):

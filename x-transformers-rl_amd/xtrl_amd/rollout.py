@@ -24,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib as L
+from . import ops
 from .model import WorldModelActorCritic
 
 SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
@@ -378,15 +379,17 @@ class FractalRolloutEngine(RolloutEngine):
     def _alloc_body(self, z):
         c, E, Lv = self.c, self.E, self.levels
         d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
-        self.w.update(b_pin=z(d), g_init=z(d), w_gu=z(d, d), b_gu=z(d), w_fa0=z(2 * d, (Lv + 1) * d), b_fa0=z(2 * d),
+        # g_init / g carry d zero columns after the state: the fused global-update | level-projection
+        # GEMM's residual reads them for its projection half (include/xtrl_hip.h XtrlFractalDesc)
+        self.w.update(b_pin=z(d), g_init=z(2 * d), c0=z(d), w_fa0=z(2 * d, (Lv + 1) * d), b_fa0=z(2 * d),
                       w_fa2=z(d, 2 * d), b_fa2=z(d))
-        self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), ln1_w=z(d), ln1_b=z(d), w_gv=z(I, d), w_go=z(d, I),
-                        ln2_w=z(d), ln2_b=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d),
-                        ln3_b=z(d), w_proj=z(d, d), b_proj=z(d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
-        self.fbuf = dict(g=z(E, d), x1=z(E, d), x2=z(E, d), x3=z(E, d), mean=z(E, d), allf=z(E, (Lv + 1) * d),
+        self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), ln1_w=z(d), ln1_b=z(d), w_c=z(d, d), ln2_w=z(d), ln2_b=z(d),
+                        w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d), ln3_b=z(d),
+                        w_pg=z(2 * d, d), b_pg=z(2 * d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
+        self.fbuf = dict(g=z(E, 2 * d), c2=z(E, d), tmp=z(E, d), x2=z(E, d), mean=z(E, d), allf=z(E, (Lv + 1) * d),
                          hagg=z(E, 2 * d))
-        self._pk_src += [(self.w, k) for k in ('w_gu', 'w_fa0', 'w_fa2')]
-        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_gv', 'w_go', 'w_ff1', 'w_ff2', 'w_proj')]
+        self._pk_src += [(self.w, k) for k in ('w_fa0', 'w_fa2')]
+        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_c', 'w_ff1', 'w_ff2', 'w_pg')]
 
     def _build_desc(self, clamp, hazard_log2):
         super()._build_desc(clamp, hazard_log2)
@@ -399,7 +402,7 @@ class FractalRolloutEngine(RolloutEngine):
         F_ = L.FractalDesc()
         F_.levels, F_.ln_eps = Lv, self.ln_eps
         F_.level = C.cast(levels, C.POINTER(L.FractalLevel))
-        for k in ('g_init', 'w_gu', 'b_gu', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2'):
+        for k in ('g_init', 'c0', 'w_fa0', 'b_fa0', 'w_fa2', 'b_fa2'):
             setattr(F_, k, self._wv(self.w, k))
         for k, t in self.fbuf.items():
             setattr(F_, k, L.ptr(t))
@@ -413,9 +416,9 @@ class FractalRolloutEngine(RolloutEngine):
         w['w_pin'].copy_(enc.input_embed.weight)
         w['b_pin'].copy_(enc.input_embed.bias + model.level_embed(0))   # level 0's embedding folded in
         self._pack_common(model, rs_mean, rs_var)
-        w['g_init'].copy_(enc.global_state_init.reshape(-1))
-        w['w_gu'].copy_(enc.global_state_update.weight)
-        w['b_gu'].copy_(enc.global_state_update.bias)
+        d = self.c.dim
+        w['g_init'][:d].copy_(enc.global_state_init.reshape(-1))
+        gu = enc.global_state_update
         fa0, fa2 = enc.final_aggregation[0], enc.final_aggregation[2]
         w['w_fa0'].copy_(fa0.weight)
         w['b_fa0'].copy_(fa0.bias)
@@ -426,8 +429,8 @@ class FractalRolloutEngine(RolloutEngine):
             sa, ga = blk.self_attn, blk.global_attn
             torch.cat((sa.to_q.weight, sa.to_k.weight, sa.to_v.weight), out=wl['w_qkv'])
             wl['w_out'].copy_(sa.to_out.weight)
-            wl['w_gv'].copy_(ga.to_v.weight)
-            wl['w_go'].copy_(ga.to_out.weight)
+            # the one-key cross-attention W_out (W_v g) as one operand W_c = W_out W_v (library GEMM)
+            ops.gemm(ga.to_out.weight, ga.to_v.weight.t().contiguous(), out=wl['w_c'])
             for j, nm in ((1, blk.norm1), (2, blk.norm2), (3, blk.norm3)):
                 wl[f'ln{j}_w'].copy_(nm.weight)
                 wl[f'ln{j}_b'].copy_(nm.bias)
@@ -437,9 +440,11 @@ class FractalRolloutEngine(RolloutEngine):
             wl['w_ff2'].copy_(ff2.weight)
             wl['b_ff2'].copy_(ff2.bias)
             pj = enc.level_projections[li]
-            wl['w_proj'].copy_(pj.weight)
-            wl['b_proj'].copy_(pj.bias)
+            torch.cat((gu.weight, pj.weight), out=wl['w_pg'])
+            torch.cat((gu.bias, pj.bias), out=wl['b_pg'])
             wl['level_emb'].copy_(model.level_embed(li))
+        # level 0's cross-attention row: every row's global state is global_state_init there
+        ops.gemm(w['g_init'][None, :d], self.wl[0]['w_c'], out=w['c0'][None])
         self._pack_gemm_weights()
 
     def step(self, t):
