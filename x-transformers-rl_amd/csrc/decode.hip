@@ -792,11 +792,11 @@ __global__ __launch_bounds__(256) void k_fr_ln12(const XtrlDecodeDesc D, int t, 
   }
 }
 
-// x3 = LN3(x2 + f); the episode slot's running sum of x3 (restarting at t = 0) and the running mean
+// x3 = LN3(s3) (s3 = x2 + FF(x2)); the episode slot's running sum of x3 (restarting at t = 0) and the running mean
 // of the live row; the next level's input x3 + level_embed[l + 1] into D.x (xnext NULL: last level)
-__global__ __launch_bounds__(256) void k_fr_ln3_tail(const XtrlDecodeDesc D, int t, const float* x2, const float* f,
-                                                     const float* g3, const float* b3, float* sums, float* mean,
-                                                     const float* le_next, float eps) {
+__global__ __launch_bounds__(256) void k_fr_ln3_tail(const XtrlDecodeDesc D, int t, const float* s3, const float* g3,
+                                                     const float* b3, float* sums, float* mean, const float* le_next,
+                                                     float eps) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63, d = D.d;
   if (r >= D.live_count[t & 1]) return;
   const int e = rows_of(D, t)[r];
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) void k_fr_ln3_tail(const XtrlDecodeDesc D, int
 #pragma unroll
   for (int j = 0; j < FR_MAXF; ++j) {
     const int c = lane + 64 * j;
-    v[j] = c < d ? x2[(int64_t)r * d + c] + f[(int64_t)r * d + c] : 0.f;
+    v[j] = c < d ? s3[(int64_t)r * d + c] : 0.f;
     sp[j] = (c < d && t > 0) ? sums[(int64_t)e * d + c] : 0.f;   // step 0 starts the episode's sum
   }
   fr_layernorm(v, lane, d, eps, g3, b3);
@@ -909,8 +909,9 @@ __device__ __forceinline__ f32x4v mfma_x6(const bf16x8 (&a)[3], const uint4 (&b)
 }
 
 template <int NT2, int MT>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
-__global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, float* C,
-                                             int ldc, const float* g_next, float* Y, int ldy) {
+__global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
+                                             const float* res, float* C, int ldc, const float* g_next, float* Y,
+                                             int ldy) {
   constexpr int d = 64 * NT2, NT1 = MLP_HW / 64, BM = 16 * MT;
   constexpr int LDA = d + 4, JS1 = d / 32;              // FF1: K = d, 32-deep k steps
   constexpr int LDH = MLP_HW + 4, JSC = MLP_HW / 32;    // FF2: the chunk's 128 k
@@ -927,7 +928,7 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
   //      chunk (all of K in one batch), b1
   if (4 * lane < d)
     for (int r = w; r < BM; r += 4)
-      __builtin_amdgcn_global_load_lds((const void*)(D.xn + (int64_t)min(m0 + r, M - 1) * d + 4 * lane),
+      __builtin_amdgcn_global_load_lds((const void*)(xin + (int64_t)min(m0 + r, M - 1) * d + 4 * lane),
                                        (lds_void*)(A1 + r * LDA), 16, 0, 0);
   const uint4* w1 = reinterpret_cast<const uint4*>(Ly.w_ff1x);
   const int64_t P1 = (int64_t)D.ff / 16 * JS1 * 64;   // slots per piece plane
@@ -1035,7 +1036,7 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int e = tid + 256 * k, r = e / d, col = e - r * d;
-    v[k] = D.x[(int64_t)min(m0 + r, M - 1) * d + col] + Ly.b_ff2[col];
+    v[k] = res[(int64_t)min(m0 + r, M - 1) * d + col] + Ly.b_ff2[col];
   }
   for (int cc = 0; cc < HC; ++cc)
 #pragma unroll
@@ -1051,7 +1052,9 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
     A1[r * LDA + col] = v[k];   // (A1 is free: every wave is past its FF1)
   }
   // the next pre-norm of the completed rows (the next layer's attention LayerNorm, or the final norm
-  // in the heads' input row), two-pass as the GEMM prologue: one wave per BM / 4 rows
+  // in the heads' input row), two-pass as the GEMM prologue: one wave per BM / 4 rows (Y NULL: none,
+  // the fractal body's post-norm follows in its own row kernel)
+  if (!Y) return;
   __syncthreads();
 #pragma unroll
   for (int rr = 0; rr < BM / 4; ++rr) {
@@ -1096,19 +1099,18 @@ bool mlp_fused(const XtrlDecodeDesc* D, int l) {
 
 // layer l's feed-forward: x += FF(xn), then the next pre-norm of the rows — the last layer writes only
 // the final-normed row into the heads' input (nothing reads its raw output), the others x and xn
-int launch_mlp(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
+// the one-launch feed-forward over the live rows: C = res + FF(xin) (C NULL: not stored), then
+// (Y non-NULL) the pre-norm LN(C) g into Y
+int launch_mlp_rows(const XtrlDecodeDesc* D, int l, int t, const float* xin, const float* res, float* C, int ldc,
+                    const float* g, float* Y, int ldy, hipStream_t s) {
   const int bm = mlp_rows();
   const dim3 grid(D->ff / MLP_HW, (D->E + bm - 1) / bm);
   const XtrlDecodeLayer& Ly = D->layers[l];
-  const bool last = l == D->L - 1;
-  float* C = last ? nullptr : D->x;
-  const float* g = last ? D->ln_final : D->layers[l + 1].ln_attn;
-  float* Y = last ? D->ac_in : D->xn;
-  const int ldc = D->d, ldy = last ? D->in_dim : D->d;
 #define XTRL_MLP(NT2)                                                                              \
   do {                                                                                             \
-    if (bm == 32) hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, C, ldc, g, Y, ldy); \
-    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, C, ldc, g, Y, ldy);          \
+    if (bm == 32)                                                                                  \
+      hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy); \
+    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy); \
   } while (0)
   switch (D->d / 64) {
     case 1: XTRL_MLP(1); break;
@@ -1119,6 +1121,13 @@ int launch_mlp(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
 #undef XTRL_MLP
   XTRL_LAUNCHED("mlp");
   return XTRL_OK;
+}
+
+int launch_mlp(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
+  const bool last = l == D->L - 1;
+  return launch_mlp_rows(D, l, t, D->xn, D->x, last ? nullptr : D->x, D->d,
+                         last ? D->ln_final : D->layers[l + 1].ln_attn, last ? D->ac_in : D->xn,
+                         last ? D->in_dim : D->d, s);
 }
 
 int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
@@ -1266,12 +1275,20 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
     hipLaunchKernelGGL(k_fr_ln12, rows_grid, rows_blk, 0, s, *D, t, F->tmp, l > 0 ? F->c2 : F->c0, l > 0 ? d : 0,
                        Q.ln1_w, Q.ln1_b, Q.ln2_w, Q.ln2_b, F->x2, F->ln_eps);
     XTRL_LAUNCHED("fractal ln12");
-    if ((rc = dproj(D, t, F->x2, d, Q.w_ff1, d, Q.b_ff1, nullptr, 0, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
-      return rc;
-    if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, nullptr, 0, F->tmp, d, d, EPI_NONE, s)))
-      return rc;
-    // x3 = LN3(x2 + FF), its running mean, the next level's input
-    hipLaunchKernelGGL(k_fr_ln3_tail, rows_grid, rows_blk, 0, s, *D, t, F->x2, F->tmp, Q.ln3_w, Q.ln3_b, Q.sums, F->mean,
+    // s3 = x2 + FF(x2): one launch (k_mlp, split-bf16 weight images) or the two projections
+    const XtrlDecodeLayer& Ly = D->layers[l];
+    const bool mlp = D->mlp_part && D->mlp_cnt && Ly.w_ff1x && Ly.w_ff2x && d % 64 == 0 && d <= 256 &&
+                     ff % MLP_HW == 0;
+    if (mlp) {
+      if ((rc = launch_mlp_rows(D, l, t, F->x2, F->x2, F->tmp, d, nullptr, nullptr, 0, s))) return rc;
+    } else {
+      if ((rc = dproj(D, t, F->x2, d, Q.w_ff1, d, Q.b_ff1, nullptr, 0, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
+        return rc;
+      if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, F->x2, d, F->tmp, d, d, EPI_NONE, s)))
+        return rc;
+    }
+    // x3 = LN3(s3), its running mean, the next level's input
+    hipLaunchKernelGGL(k_fr_ln3_tail, rows_grid, rows_blk, 0, s, *D, t, F->tmp, Q.ln3_w, Q.ln3_b, Q.sums, F->mean,
                        l + 1 < Lv ? F->level[l + 1].level_emb : nullptr, F->ln_eps);
     XTRL_LAUNCHED("fractal ln3 tail");
     // [g | p_l] = [g | 0] + mean [W_gu; W_p,l]^T + [b_gu; b_p,l]: g in place (level 0 from g_init),

@@ -386,6 +386,10 @@ class FractalRolloutEngine(RolloutEngine):
         self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), ln1_w=z(d), ln1_b=z(d), w_c=z(d, d), ln2_w=z(d), ln2_b=z(d),
                         w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d), ln3_b=z(d),
                         w_pg=z(2 * d, d), b_pg=z(2 * d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
+        if ff % 128 == 0 and d % 64 == 0 and d <= 256:   # split-bf16 images for the one-launch feed-forward
+            n1, n2 = (int(L.lib().xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
+            for wl in self.wl:
+                wl['w_ff1x'], wl['w_ff2x'] = z(n1, dt=torch.int16), z(n2, dt=torch.int16)
         self.fbuf = dict(g=z(E, 2 * d), c2=z(E, d), tmp=z(E, d), x2=z(E, d), mean=z(E, d), allf=z(E, (Lv + 1) * d),
                          hagg=z(E, 2 * d))
         self._pk_src += [(self.w, k) for k in ('w_fa0', 'w_fa2')]
