@@ -275,9 +275,19 @@ __device__ __forceinline__ float kpi_sum(float v) {
 // cache rows: float4 columns 4 lane + 256 j), the H partial rows meet in LDS and are summed in head
 // order onto the residual row x[r] — the out-projection GEMM launch of the layer is gone.
 // FJ = ceil(d / 256) float4 column groups per lane (FJ = 0: not fused, the output goes to D.att)
+// FrPost (fractal body, g1 non-NULL): the fused tail forms the post-norm rows instead —
+// out = LN2(LN1(x + attn W_out^T) g1 + b1 + c[r] ) g2 + b2 (nn.LayerNorm, eps), x itself is not
+// stored (nothing reads it) and no pre-norm is written
+struct FrPost {
+  const float *g1 = nullptr, *b1 = nullptr, *g2 = nullptr, *b2 = nullptr, *c = nullptr;
+  int ldc = 0;
+  float* out = nullptr;
+  float eps = 1e-5f;
+};
+
 template <int DH, int FJ>
 __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int layer,
-                                                      int t) {
+                                                      int t, const FrPost fp) {
   constexpr int CK = DH <= 32 ? 128 : 64;          // keys per chunk
   constexpr int KL = CK / 64, F4 = DH / 4;         // keys per lane (scores), float4 per key row
   constexpr int LPK = DH / 4, KPI = 64 / LPK;      // P.V: lanes per key row, keys per load instruction
@@ -295,6 +305,8 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
   // fused out-projection operands: this head's rows of W_out^T and the residual row
   float4 wt[FUSE ? FJ : 1][FUSE ? DH : 1];
   float4 xres[FUSE ? FJ : 1], gff[FUSE ? FJ : 1];   // wave 0: the residual row and FF1's LayerNorm gain
+  float4 pg1[FUSE ? FJ : 1], pb1[FUSE ? FJ : 1], pg2[FUSE ? FJ : 1], pb2[FUSE ? FJ : 1], pc[FUSE ? FJ : 1];
+  const bool post = fp.g1 != nullptr;
   if constexpr (FUSE) {
 #pragma unroll
     for (int j = 0; j < FJ; ++j) {
@@ -304,7 +316,17 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
         wt[j][c] = *reinterpret_cast<const float4*>(Ly.w_out_t + (int64_t)(h * DH + c) * d + n);
       if (w == 0) {
         xres[j] = *reinterpret_cast<const float4*>(D.x + (int64_t)r * d + n);
-        gff[j] = *reinterpret_cast<const float4*>(Ly.ln_ff + n);
+        if (post) {
+          if constexpr (FJ == 1) {   // (prefetched with the residual row; FJ = 2 loads them in the tail)
+            pg1[j] = *reinterpret_cast<const float4*>(fp.g1 + n);
+            pb1[j] = *reinterpret_cast<const float4*>(fp.b1 + n);
+            pg2[j] = *reinterpret_cast<const float4*>(fp.g2 + n);
+            pb2[j] = *reinterpret_cast<const float4*>(fp.b2 + n);
+            pc[j] = *reinterpret_cast<const float4*>(fp.c + (int64_t)r * fp.ldc + n);
+          }
+        } else {
+          gff[j] = *reinterpret_cast<const float4*>(Ly.ln_ff + n);
+        }
       }
     }
   }
@@ -490,11 +512,51 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
             y[j].z += p.z;
             y[j].w += p.w;
           }
-          *reinterpret_cast<float4*>(D.x + (int64_t)r * d + n) = y[j];
+          if (!post) *reinterpret_cast<float4*>(D.x + (int64_t)r * d + n) = y[j];
           sm += (y[j].x + y[j].y) + (y[j].z + y[j].w);
         }
       }
-      if (D.xn) {
+      if (post) {   // LN1 (affine), + the cross-attention row, LN2 (affine) -> out
+        if constexpr (FJ > 1) {
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) {
+            const int n = min(4 * lane + 256 * j, d - 4);
+            pg1[j] = *reinterpret_cast<const float4*>(fp.g1 + n);
+            pb1[j] = *reinterpret_cast<const float4*>(fp.b1 + n);
+            pg2[j] = *reinterpret_cast<const float4*>(fp.g2 + n);
+            pb2[j] = *reinterpret_cast<const float4*>(fp.b2 + n);
+            pc[j] = *reinterpret_cast<const float4*>(fp.c + (int64_t)r * fp.ldc + n);
+          }
+        }
+        auto affine_ln = [&](float4 (&v)[FJ], float s1, const float4 (&g)[FJ], const float4 (&b)[FJ]) {
+          const float mean = wave_sum_dpp(s1) / (float)d;
+          float qq = 0.f;
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+            if (4 * lane + 256 * j < d) {
+              const float4 dl = make_float4(v[j].x - mean, v[j].y - mean, v[j].z - mean, v[j].w - mean);
+              qq += (dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w);
+            }
+          const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + fp.eps);
+#pragma unroll
+          for (int j = 0; j < FJ; ++j)
+            v[j] = make_float4((v[j].x - mean) * rstd * g[j].x + b[j].x, (v[j].y - mean) * rstd * g[j].y + b[j].y,
+                               (v[j].z - mean) * rstd * g[j].z + b[j].z, (v[j].w - mean) * rstd * g[j].w + b[j].w);
+        };
+        affine_ln(y, sm, pg1, pb1);
+        float s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          y[j] = make_float4(y[j].x + pc[j].x, y[j].y + pc[j].y, y[j].z + pc[j].z, y[j].w + pc[j].w);
+          if (4 * lane + 256 * j < d) s2 += (y[j].x + y[j].y) + (y[j].z + y[j].w);
+        }
+        affine_ln(y, s2, pg2, pb2);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          const int n = 4 * lane + 256 * j;
+          if (n < d) *reinterpret_cast<float4*>(fp.out + (int64_t)r * d + n) = y[j];
+        }
+      } else if (D.xn) {
         const float mean = wave_sum_dpp(sm) / (float)d;
         float qq = 0.f;
 #pragma unroll
@@ -1130,12 +1192,12 @@ int launch_mlp(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
                          last ? D->in_dim : D->d, s);
 }
 
-int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
+int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s, const FrPost& fp = FrPost{}) {
   if (attn_fused(D, l)) {   // one workgroup of H waves per live row
     const size_t lds = ((size_t)D->H * (D->Tmax + 3 * D->dh) + (size_t)D->H * D->d) * sizeof(float);
     const dim3 grid(D->E), blk(64 * D->H);
-    if (D->d > 256) hipLaunchKernelGGL((k_attn_decode<16, 2>), grid, blk, lds, s, *D, D->layers[l], l, t);
-    else hipLaunchKernelGGL((k_attn_decode<16, 1>), grid, blk, lds, s, *D, D->layers[l], l, t);
+    if (D->d > 256) hipLaunchKernelGGL((k_attn_decode<16, 2>), grid, blk, lds, s, *D, D->layers[l], l, t, fp);
+    else hipLaunchKernelGGL((k_attn_decode<16, 1>), grid, blk, lds, s, *D, D->layers[l], l, t, fp);
     XTRL_LAUNCHED("attn_decode");
     return XTRL_OK;
   }
@@ -1144,11 +1206,11 @@ int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s) {
   XTRL_REQUIRE(lds <= 160 * 1024, "attn_decode: Tmax %d too large for LDS", D->Tmax);
   dim3 grid((waves + 3) / 4);
   if (D->dh == 16)
-    hipLaunchKernelGGL((k_attn_decode<16, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<16, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t, fp);
   else if (D->dh == 32)
-    hipLaunchKernelGGL((k_attn_decode<32, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<32, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t, fp);
   else
-    hipLaunchKernelGGL((k_attn_decode<64, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t);
+    hipLaunchKernelGGL((k_attn_decode<64, 0>), grid, dim3(256), lds, s, *D, D->layers[l], l, t, fp);
   XTRL_LAUNCHED("attn_decode");
   return XTRL_OK;
 }
@@ -1247,8 +1309,6 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
 int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t, hipStream_t s) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(F && F->level && F->levels == D->L && F->levels > 0, "fractal_decode: levels mismatch");
-  for (int l = 0; l < D->L; ++l)
-    XTRL_REQUIRE(!D->layers[l].w_out_t, "fractal_decode: the attention output feeds a LayerNorm (w_out_t must be NULL)");
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "fractal_decode: t=%d outside [0, %d)", t, D->Tmax);
   XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs &&
                    D->n_qkv == 3 * D->H * D->dh && D->d <= 64 * FR_MAXF,
@@ -1267,14 +1327,22 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
       return rc;
     if ((rc = dproj(D, t, D->x, d, Q.w_qkv, d, nullptr, nullptr, 0, nullptr, 0, D->qkv, D->n_qkv, 3 * I, EPI_NONE, s)))
       return rc;
+    // x2 = LN2(LN1(x + attn W_out^T) + c): inside the attention launch (one workgroup per live row,
+    // the head partials of the out-projection meeting in LDS) or as projection + row kernel
+    FrPost fp;
+    fp.g1 = Q.ln1_w; fp.b1 = Q.ln1_b; fp.g2 = Q.ln2_w; fp.b2 = Q.ln2_b;
+    fp.c = l > 0 ? F->c2 : F->c0; fp.ldc = l > 0 ? d : 0; fp.out = F->x2; fp.eps = F->ln_eps;
+    const bool fused = attn_fused(D, l);
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l)], s);
-    if ((rc = launch_attn_decode(D, l, t, s))) return rc;
+    if ((rc = launch_attn_decode(D, l, t, s, fused ? fp : FrPost{}))) return rc;
     if (D->prof_events) (void)hipEventRecord((hipEvent_t)D->prof_events[2 * (t * D->L + l) + 1], s);
-    if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->tmp, d, d, EPI_NONE, s))) return rc;
-    // x2 = LN2(LN1(x + attn) + c)
-    hipLaunchKernelGGL(k_fr_ln12, rows_grid, rows_blk, 0, s, *D, t, F->tmp, l > 0 ? F->c2 : F->c0, l > 0 ? d : 0,
-                       Q.ln1_w, Q.ln1_b, Q.ln2_w, Q.ln2_b, F->x2, F->ln_eps);
-    XTRL_LAUNCHED("fractal ln12");
+    if (!fused) {
+      if ((rc = dproj(D, t, D->att, I, Q.w_out, I, nullptr, nullptr, 0, nullptr, 0, F->tmp, d, d, EPI_NONE, s)))
+        return rc;
+      hipLaunchKernelGGL(k_fr_ln12, rows_grid, rows_blk, 0, s, *D, t, F->tmp, l > 0 ? F->c2 : F->c0, l > 0 ? d : 0,
+                         Q.ln1_w, Q.ln1_b, Q.ln2_w, Q.ln2_b, F->x2, F->ln_eps);
+      XTRL_LAUNCHED("fractal ln12");
+    }
     // s3 = x2 + FF(x2): one launch (k_mlp, split-bf16 weight images) or the two projections
     const XtrlDecodeLayer& Ly = D->layers[l];
     const bool mlp = D->mlp_part && D->mlp_cnt && Ly.w_ff1x && Ly.w_ff2x && d % 64 == 0 && d <= 256 &&

@@ -383,7 +383,9 @@ class FractalRolloutEngine(RolloutEngine):
         # GEMM's residual reads them for its projection half (include/xtrl_hip.h XtrlFractalDesc)
         self.w.update(b_pin=z(d), g_init=z(2 * d), c0=z(d), w_fa0=z(2 * d, (Lv + 1) * d), b_fa0=z(2 * d),
                       w_fa2=z(d, 2 * d), b_fa2=z(d))
-        self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), ln1_w=z(d), ln1_b=z(d), w_c=z(d, d), ln2_w=z(d), ln2_b=z(d),
+        # w_out_t: to_out transposed for the attention kernel's fused out-projection + post-norms
+        self.wl = [dict(w_qkv=z(3 * I, d), w_out=z(d, I), w_out_t=z(I, d), ln1_w=z(d), ln1_b=z(d), w_c=z(d, d),
+                        ln2_w=z(d), ln2_b=z(d),
                         w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d), ln3_b=z(d),
                         w_pg=z(2 * d, d), b_pg=z(2 * d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
         if ff % 128 == 0 and d % 64 == 0 and d <= 256:   # split-bf16 images for the one-launch feed-forward
@@ -433,6 +435,7 @@ class FractalRolloutEngine(RolloutEngine):
             sa, ga = blk.self_attn, blk.global_attn
             torch.cat((sa.to_q.weight, sa.to_k.weight, sa.to_v.weight), out=wl['w_qkv'])
             wl['w_out'].copy_(sa.to_out.weight)
+            wl['w_out_t'].copy_(sa.to_out.weight.t())
             # the one-key cross-attention W_out (W_v g) as one operand W_c = W_out W_v (library GEMM)
             ops.gemm(ga.to_out.weight, ga.to_v.weight.t().contiguous(), out=wl['w_c'])
             for j, nm in ((1, blk.norm1), (2, blk.norm2), (3, blk.norm3)):
