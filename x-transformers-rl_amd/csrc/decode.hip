@@ -970,10 +970,22 @@ __device__ __forceinline__ f32x4v mfma_x6(const bf16x8 (&a)[3], const uint4 (&b)
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bh, c, 0, 0, 0);
 }
 
+// FrMlp (fractal body, g3 non-NULL): the tail forms x3 = LN3(s3) g3 + b3 (nn.LayerNorm, eps) of the
+// completed rows instead of a pre-norm, adds it to the episode slot's running sum (restarting at
+// t = 0), stores the running mean and, for all but the last level, the next level's input
+// x3 + le_next into D.x
+struct FrMlp {
+  const float *g3 = nullptr, *b3 = nullptr;
+  float* sums = nullptr;
+  float* mean = nullptr;
+  const float* le_next = nullptr;
+  float eps = 1e-5f;
+};
+
 template <int NT2, int MT>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
 __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
                                              const float* res, float* C, int ldc, const float* g_next, float* Y,
-                                             int ldy) {
+                                             int ldy, const FrMlp fm) {
   constexpr int d = 64 * NT2, NT1 = MLP_HW / 64, BM = 16 * MT;
   constexpr int LDA = d + 4, JS1 = d / 32;              // FF1: K = d, 32-deep k steps
   constexpr int LDH = MLP_HW + 4, JSC = MLP_HW / 32;    // FF2: the chunk's 128 k
@@ -1114,8 +1126,49 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
     A1[r * LDA + col] = v[k];   // (A1 is free: every wave is past its FF1)
   }
   // the next pre-norm of the completed rows (the next layer's attention LayerNorm, or the final norm
-  // in the heads' input row), two-pass as the GEMM prologue: one wave per BM / 4 rows (Y NULL: none,
-  // the fractal body's post-norm follows in its own row kernel)
+  // in the heads' input row), two-pass as the GEMM prologue: one wave per BM / 4 rows (Y NULL: none)
+  if (fm.g3) {   // fractal: LayerNorm 3, the running sums / mean and the next level's input
+    __syncthreads();
+    float g3v[NT2], b3v[NT2], lev[NT2];
+#pragma unroll
+    for (int j = 0; j < NT2; ++j) {
+      g3v[j] = fm.g3[lane + 64 * j];
+      b3v[j] = fm.b3[lane + 64 * j];
+      lev[j] = fm.le_next ? fm.le_next[lane + 64 * j] : 0.f;
+    }
+    const int32_t* slots = rows_of(D, t);
+#pragma unroll
+    for (int rr = 0; rr < BM / 4; ++rr) {
+      const int r = (BM / 4) * w + rr, m = m0 + r;
+      const int e = slots[min(m, M - 1)];
+      float xv[NT2], sp[NT2], sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT2; ++j) {
+        xv[j] = A1[r * LDA + lane + 64 * j];
+        sp[j] = t > 0 ? fm.sums[(int64_t)e * d + lane + 64 * j] : 0.f;
+        sm += xv[j];
+      }
+      const float mean = wave_sum_dpp(sm) / (float)d;
+      float qq = 0.f;
+#pragma unroll
+      for (int j = 0; j < NT2; ++j) {
+        const float dl = xv[j] - mean;
+        qq += dl * dl;
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + fm.eps);
+      if (m < M)
+#pragma unroll
+        for (int j = 0; j < NT2; ++j) {
+          const int col = lane + 64 * j;
+          const float x3 = (xv[j] - mean) * rstd * g3v[j] + b3v[j];
+          const float s2 = sp[j] + x3;
+          fm.sums[(int64_t)e * d + col] = s2;
+          fm.mean[(int64_t)m * d + col] = s2 / (float)(t + 1);
+          if (fm.le_next) D.x[(int64_t)m * d + col] = x3 + lev[j];
+        }
+    }
+    return;
+  }
   if (!Y) return;
   __syncthreads();
 #pragma unroll
@@ -1164,15 +1217,15 @@ bool mlp_fused(const XtrlDecodeDesc* D, int l) {
 // the one-launch feed-forward over the live rows: C = res + FF(xin) (C NULL: not stored), then
 // (Y non-NULL) the pre-norm LN(C) g into Y
 int launch_mlp_rows(const XtrlDecodeDesc* D, int l, int t, const float* xin, const float* res, float* C, int ldc,
-                    const float* g, float* Y, int ldy, hipStream_t s) {
+                    const float* g, float* Y, int ldy, hipStream_t s, const FrMlp& fm = FrMlp{}) {
   const int bm = mlp_rows();
   const dim3 grid(D->ff / MLP_HW, (D->E + bm - 1) / bm);
   const XtrlDecodeLayer& Ly = D->layers[l];
 #define XTRL_MLP(NT2)                                                                              \
   do {                                                                                             \
     if (bm == 32)                                                                                  \
-      hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy); \
-    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy); \
+      hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
   } while (0)
   switch (D->d / 64) {
     case 1: XTRL_MLP(1); break;
@@ -1347,18 +1400,21 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
     const XtrlDecodeLayer& Ly = D->layers[l];
     const bool mlp = D->mlp_part && D->mlp_cnt && Ly.w_ff1x && Ly.w_ff2x && d % 64 == 0 && d <= 256 &&
                      ff % MLP_HW == 0;
+    // x3 = LN3(s3), its running mean, the next level's input: in the k_mlp tail, or a row kernel
+    const float* le_next = l + 1 < Lv ? F->level[l + 1].level_emb : nullptr;
     if (mlp) {
-      if ((rc = launch_mlp_rows(D, l, t, F->x2, F->x2, F->tmp, d, nullptr, nullptr, 0, s))) return rc;
+      FrMlp fm;
+      fm.g3 = Q.ln3_w; fm.b3 = Q.ln3_b; fm.sums = Q.sums; fm.mean = F->mean; fm.le_next = le_next; fm.eps = F->ln_eps;
+      if ((rc = launch_mlp_rows(D, l, t, F->x2, F->x2, nullptr, d, nullptr, nullptr, 0, s, fm))) return rc;
     } else {
       if ((rc = dproj(D, t, F->x2, d, Q.w_ff1, d, Q.b_ff1, nullptr, 0, nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
         return rc;
       if ((rc = dproj(D, t, D->hff, ff, Q.w_ff2, ff, Q.b_ff2, nullptr, 0, F->x2, d, F->tmp, d, d, EPI_NONE, s)))
         return rc;
+      hipLaunchKernelGGL(k_fr_ln3_tail, rows_grid, rows_blk, 0, s, *D, t, F->tmp, Q.ln3_w, Q.ln3_b, Q.sums, F->mean,
+                         le_next, F->ln_eps);
+      XTRL_LAUNCHED("fractal ln3 tail");
     }
-    // x3 = LN3(s3), its running mean, the next level's input
-    hipLaunchKernelGGL(k_fr_ln3_tail, rows_grid, rows_blk, 0, s, *D, t, F->tmp, Q.ln3_w, Q.ln3_b, Q.sums, F->mean,
-                       l + 1 < Lv ? F->level[l + 1].level_emb : nullptr, F->ln_eps);
-    XTRL_LAUNCHED("fractal ln3 tail");
     // [g | p_l] = [g | 0] + mean [W_gu; W_p,l]^T + [b_gu; b_p,l]: g in place (level 0 from g_init),
     // the level projection into allf
     if ((rc = dproj(D, t, F->mean, d, Q.w_pg, d, Q.b_pg, nullptr, 0, l > 0 ? F->g : F->g_init, l > 0 ? 2 * d : 0, F->g,
