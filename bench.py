@@ -504,8 +504,9 @@ def main():
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
         achieved = timer.bytes / timer.launches / avg_s / 1e9
-        attn_roofline = dict(kernel='k_attn_decode (rollout decode attention over the KV cache, with the fused '
-                                    'out-projection + residual + FF1 LayerNorm of its rows)', bound='hbm',
+        tail = ('the fused out-projection and both post-norm add + LayerNorms of its rows (fractal body)'
+                if cfg.get('fractal') else 'the fused out-projection + residual + FF1 LayerNorm of its rows')
+        attn_roofline = dict(kernel=f'k_attn_decode (rollout decode attention over the KV cache, with {tail})', bound='hbm',
                              achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit='GB/s',
                              frac=round(achieved / HBM_PEAK_GBS, 4), traffic=prof(pmc_traffic, 'k_attn_decode'),
                              avg_launch_us=round(avg_s * 1e6, 2), bytes_per_launch=round(timer.bytes / timer.launches))
