@@ -833,10 +833,14 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       const int row = wave + 8 * rr, mc = min(m0 + row, M - 1);
       g[rr] = *reinterpret_cast<const float4*>(tile + row * LDT + cc);
       xv[rr] = ld4(a.ln_x + (int64_t)mc * N);
-      if constexpr (X) dr[rr] = a.ln_gpre ? ld4(a.ln_gpre + (int64_t)mc * N) : z4;
+      if constexpr (X) dr[rr] = a.ln_gpre ? ld4(a.ln_gpre + (int64_t)mc * (a.ln_ldg ? a.ln_ldg : N)) : z4;
       else dr[rr] = a.ln_dres ? ld4(a.ln_dres + (int64_t)mc * N) : z4;
       st[rr] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (int64_t)mc);
-      if constexpr (X) g[rr] = make_float4(g[rr].x + dr[rr].x, g[rr].y + dr[rr].y, g[rr].z + dr[rr].z, g[rr].w + dr[rr].w);
+      if constexpr (X) {
+        const float gs = a.ln_gscale;
+        g[rr] = make_float4(g[rr].x * gs + dr[rr].x, g[rr].y * gs + dr[rr].y, g[rr].z * gs + dr[rr].z,
+                            g[rr].w * gs + dr[rr].w);
+      }
       if (!cok) g[rr] = z4;
     }
     float4 dg = z4, db = z4;
@@ -1442,6 +1446,7 @@ int ln_gemm_run(const GemmArgs& a, int trans_a, int trans_b, int epi, bool vec, 
     else launch_ws<false, true, EPI_LN_BWD, false, 64, 256, true>(a, s);
   } else {
     XTRL_REQUIRE(trans_b && !res && a.ln_x && a.ln_part && (!a.ln_gpre || ((uintptr_t)a.ln_gpre & 15u) == 0) &&
+                     a.ln_ldg % 4 == 0 &&
                      (!a.ln2_out || (a.ln2_g && a.ln2_x && a.ln2_stats && a.ln2_part && a.ln2_part_b &&
                                      ((uintptr_t)a.ln2_out & 15u) == 0 && ((uintptr_t)a.ln2_g & 15u) == 0)) &&
                      a.ldc == a.N,

@@ -74,6 +74,8 @@ struct GemmArgs {
   float* ln_part = nullptr;       // LN_BWD: d gamma partials [ceil(M / BM)][N]
   // EPI_LN_BWD2 (partial rows of stride ln_pstride: the four partial sets of one row tile side by side)
   const float* ln_gpre = nullptr; // gradient added to the GEMM output before the LayerNorm backward [M][N]
+  int ln_ldg = 0;                 //   its row stride (0: N)
+  float ln_gscale = 1.f;          // the GEMM output scaled by this before the add (frac_gradient)
   float* ln_part_b = nullptr;     // d beta partials
   int ln_pstride = 0;
   const float* ln2_g = nullptr;   // the chained LayerNorm: gamma, input, (mean, rstd), output, partials

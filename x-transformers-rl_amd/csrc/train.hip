@@ -994,7 +994,7 @@ int heads_forward(const Ctx& c) {
 
 // heads backward -> dac (gradient of ac_in), dewa (of ewa); the weight gradients of the heads, the
 // state embedding and the gene conditioning (c: main stream, cw: weight-gradient stream)
-int heads_backward(const Ctx& c, const Ctx& cw, Fork& F) {
+int heads_backward(const Ctx& c, const Ctx& cw, Fork& F, bool embed_cols = true) {
   const XtrlTrainDesc* D = c.D;
   const int T = c.T, d = D->d, ldp = d + 4, S1x2 = 2 * (D->S + 1);
   const hipStream_t s = c.s;
@@ -1011,7 +1011,14 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F) {
     return rc;
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->dz1, 4 * d, D->ac_in, D->in_dim, c.G(D->w_h1), T, 4 * d, D->in_dim, c.G(D->b_h1)))) return rc;
-  if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
+  if (embed_cols) {
+    if ((rc = linear_dgrad(c, D->dz1, 4 * d, c.P(D->w_h1), D->dac, D->in_dim, T, 4 * d, D->in_dim, EPI_NONE))) return rc;
+  } else {   // columns [d, in_dim) only: the caller folds the embed columns into its final-norm backward
+    GemmArgs g;
+    g.A = D->dz1; g.lda = 4 * d; g.B = c.P(D->w_h1) + d; g.ldb = D->in_dim; g.C = D->dac + d; g.ldc = D->in_dim;
+    g.M = T; g.N = D->in_dim - d; g.K = 4 * d;
+    if ((rc = gemm_run(g, 0, 1, EPI_NONE, c.s))) return rc;
+  }
   // state embedding and gene conditioning
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->dac + d, D->in_dim, D->swr, D->S + 1, c.G(D->w_se), T, d, D->S, c.G(D->b_se)))) return rc;
@@ -1147,14 +1154,29 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     ++bucket;
     return XTRL_OK;
   };
-  if ((rc = heads_backward(c, cw, F))) return rc;
-  // action-embedding gradient of the next-action input (and, below, of the previous action)
-  // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d]
   const bool per_layer = ln_fusable(D) && D->scratch_per_layer;
   float* dx_top = per_layer ? D->dx + (int64_t)D->L * T * d : D->dx;   // (scratch_per_layer: slot L)
-  if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
-                   c.P(D->ln_final), nullptr, dx_top, c.G(D->ln_final))))
+  // ---- final norm: d embed = frac * dac[:, :d] + dewa[:, :d].  Fused: the embed columns of the
+  // actor | critic input gradient finish the final norm's backward in their GEMM's epilogue (no
+  // LayerNorm launch); otherwise dac in full, then k_ln_bwd
+  const bool fold = ln_fusable(D);
+  if ((rc = heads_backward(c, cw, F, !fold))) return rc;
+  if (fold) {
+    const int nb = (T + gemm_ln_rows(d) - 1) / gemm_ln_rows(d);
+    XTRL_REQUIRE((int64_t)nb * d <= D->part_floats, "train: partial-sum workspace too small");
+    GemmArgs g;
+    g.A = D->dz1; g.lda = 4 * d; g.B = c.P(D->w_h1); g.ldb = D->in_dim; g.C = dx_top; g.ldc = d;
+    g.M = T; g.N = d; g.K = 4 * d;
+    g.ln_g = c.P(D->ln_final); g.ln_x = D->x_final; g.ln_stats = D->st_final;
+    g.ln_gpre = D->dewa; g.ln_ldg = 2 * d; g.ln_gscale = D->frac_head_grad; g.ln_part = D->part;
+    if ((rc = gemm_run(g, 0, 1, EPI_LN_BWD2, s))) return rc;
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, s, D->part, nb, d,
+                       c.G(D->ln_final));
+    XTRL_LAUNCHED("train final-norm backward");
+  } else if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
+                          c.P(D->ln_final), nullptr, dx_top, c.G(D->ln_final)))) {
     return rc;
+  }
   if ((rc = bucket_done())) return rc;   // bucket 0: heads, state / gene embeddings, final norm
   // ---- decoder blocks, last to first.  Side events of the weight gradients whose dY buffer the
   // main stream overwrites later: dx (FF2 / out-projection), dff (FF1, by the next layer's FF2
