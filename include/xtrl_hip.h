@@ -295,8 +295,10 @@ int xtrl_hlgauss_gae(const float* logits, int64_t ld_row, const float* rewards, 
  * Training attention (x-transformers Attend with causal + key-padding mask, post-softmax dropout)
  *   q, k, v: [b][H][n][dh]; lens[b] valid keys per row; out o [b][H][n][dh]; lse [b][H][n]
  * ------------------------------------------------------------------------------------------- */
-/* dropout keep(b, h, i, j) = word (i & 3) of philox(seed; i >> 2, j, offset + b * H + h,
- * (6 << 24) | sub) >= p * 2^32; sub (< 2^24) names the decoder layer */
+/* dropout keep(b, h, i, j), c2 = offset + b * H + h: when 256 p is an integer (p = 0.25), byte (i & 3)
+ * of word ((j >> 4) & 3) of philox(seed; i >> 2, 16 (j >> 6) + (j & 15), c2, (6 << 24) | sub | 1 << 23)
+ * >= 256 p; otherwise word (i & 3) of philox(seed; i >> 2, j, c2, (6 << 24) | sub) >= p * 2^32;
+ * sub (< 2^23) names the decoder layer */
 int xtrl_attn_fwd(const float* q, const float* k, const float* v, const int32_t* lens, float* o, float* lse,
                   int b, int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset,
                   uint32_t sub, void* stream);

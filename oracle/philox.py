@@ -143,10 +143,21 @@ def _thresh32(p):
 
 
 def attn_dropout_keep(b, H, n, p, seed, offset, layer):
-    """bool [b][H][n][n]: keep(e, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + e H + h,
-    FIELD_DROPOUT << 24 | layer; seed) >= p 2^32 (one Philox block per 4 query rows)."""
+    """bool [b][H][n][n] attention keep mask (x-transformers-rl_amd/csrc/attn.hip), c2 = offset + e H + h.
+    p a multiple of 1/256 (byte mode): byte (i & 3) of word ((j >> 4) & 3) of philox4x32(i >> 2,
+    16 (j >> 6) + (j & 15), c2, FIELD_DROPOUT << 24 | (layer | 1 << 23); seed) >= 256 p (one block per
+    4 query rows x 4 keys 16 apart); otherwise word (i & 3) of philox4x32(i >> 2, j, c2,
+    FIELD_DROPOUT << 24 | layer; seed) >= p 2^32."""
     n4 = (n + 3) // 4
     c2 = (np.uint64(offset) + np.arange(b * H, dtype=np.uint64))[:, None, None]
+    if float(p * 256).is_integer():
+        J = 16 * ((n + 63) // 64)
+        words = np.stack(philox4x32(np.arange(n4)[None, :, None], np.arange(J)[None, None, :], c2,
+                                    _c3(FIELD_DROPOUT, layer | (1 << 23)), seed), axis=1)   # [bH][word][i >> 2][c1]
+        i, j = np.arange(n)[:, None], np.arange(n)[None, :]
+        w = words[:, (j >> 4) & 3, i >> 2, 16 * (j >> 6) + (j & 15)]                         # [bH][n][n]
+        byte = (w >> (8 * (i & 3)).astype(np.uint32)) & np.uint32(0xFF)
+        return (byte >= np.uint32(int(p * 256))).reshape(b, H, n, n)
     words = philox4x32(np.arange(n4)[None, :, None], np.arange(n)[None, None, :], c2,
                        _c3(FIELD_DROPOUT, layer), seed)
     w = np.stack(words, axis=2).reshape(b * H, 4 * n4, n)[:, :n]     # row i = 4 (i >> 2) + (i & 3)

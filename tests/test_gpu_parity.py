@@ -268,26 +268,31 @@ def test_attention_dropout_consistent():
     assert abs(float(o0.mean()) - 1.0) < 0.05
 
 
-def test_attention_dropout_mask_is_host_philox_stream():
-    """The kept attention probabilities are exactly the host Philox stream's (oracle/philox.py):
-    keep(b, h, i, j) = word (i & 3) of philox4x32(i >> 2, j, offset + b H + h, FIELD_DROPOUT << 24 | layer;
-    seed) >= p 2^32.  Forward against a double reference that applies that mask after the softmax, and
-    q / k / v gradients against its autograd (the backward kernels draw the same words, grouped
-    differently: one Philox block per 4 rows, dealt out by a quad transpose in dK / dV)."""
+@pytest.mark.parametrize('p', [0.25, 0.1])
+def test_attention_dropout_mask_is_host_philox_stream(p):
+    """The kept attention probabilities are exactly the host Philox stream's (oracle/philox.py
+    attn_dropout_keep): byte mode at p = 0.25 (one block per 4 query rows x 4 keys 16 apart), word mode
+    at p = 0.1 (word (i & 3) of the block of (i >> 2, j)).  Forward against a double reference that
+    applies that mask after the softmax, and q / k / v gradients against its autograd (the backward
+    kernels draw the same bits, grouped differently: dealt out by a quad transpose in dK / dV).  The
+    word-mode mask is also rebuilt here from the raw stream, independently of attn_dropout_keep."""
     from xtrl_amd import ops
     from oracle import philox as P
     g = torch.Generator().manual_seed(9)
     b, H, n, dh = 2, 2, 70, 16
     q, k, v, do = (torch.randn(b, H, n, dh, generator=g) for _ in range(4))
     lens = torch.tensor([70, 45], dtype=torch.int32)
-    p, seed, offset, scale, layer = 0.25, 1234567, 5, dh ** -0.5, 3
-    thresh = np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
-    i, j = np.arange(n)[:, None], np.arange(n)[None, :]
-    keep = np.zeros((b, H, n, n), dtype=bool)
-    for bb in range(b):
-        for hh in range(H):
-            words = P.philox4x32(i >> 2, j, offset + bb * H + hh, P._c3(P.FIELD_DROPOUT, layer), seed)
-            keep[bb, hh] = np.choose(np.broadcast_to(i & 3, (n, n)), [np.broadcast_to(w, (n, n)) for w in words]) >= thresh
+    seed, offset, scale, layer = 1234567, 5, dh ** -0.5, 3
+    keep = P.attn_dropout_keep(b, H, n, p, seed, offset, layer)
+    if not float(p * 256).is_integer():
+        thresh = np.uint32(min(int(p * 2 ** 32), 2 ** 32 - 1))
+        i, j = np.arange(n)[:, None], np.arange(n)[None, :]
+        for bb in range(b):
+            for hh in range(H):
+                words = P.philox4x32(i >> 2, j, offset + bb * H + hh, P._c3(P.FIELD_DROPOUT, layer), seed)
+                ref_keep = np.choose(np.broadcast_to(i & 3, (n, n)), [np.broadcast_to(w, (n, n)) for w in words]) >= thresh
+                assert (keep[bb, hh] == ref_keep).all()
+    assert abs(keep.mean() - (1 - p)) < 0.02
     keep_t = torch.from_numpy(keep).double() / (1 - p)
     qd, kd, vd = (t.double().requires_grad_() for t in (q, k, v))
     s = torch.einsum('bhid,bhjd->bhij', qd, kd) * scale

@@ -66,5 +66,25 @@ int main() {
              time_us(g, xtrl::EPI_NONE));
     }
   }
+  // the world-model heads' input gradient: dewa[T][2d] = dzp[T][d + 1] . W_pd[d + 1][2d] (K = d + 1
+  // ragged) against the aligned K = d
+  {
+    xtrl::GemmArgs h;
+    h.A = A; h.lda = 260; h.B = B; h.ldb = 512; h.C = C; h.ldc = 512; h.M = M; h.N = 512;
+    for (int k : {257, 256, 260}) {
+      h.K = k;
+      hipEvent_t s0, s1;
+      (void)hipEventCreate(&s0);
+      (void)hipEventCreate(&s1);
+      xtrl::gemm_run(h, 0, 1, xtrl::EPI_NONE, nullptr);
+      (void)hipEventRecord(s0, nullptr);
+      for (int i = 0; i < 20; ++i) xtrl::gemm_run(h, 0, 1, xtrl::EPI_NONE, nullptr);
+      (void)hipEventRecord(s1, nullptr);
+      (void)hipEventSynchronize(s1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, s0, s1);
+      printf("dgrad NT M %d N 512 K %d      %7.1f us\n", M, k, ms / 20 * 1e3f);
+    }
+  }
   return 0;
 }

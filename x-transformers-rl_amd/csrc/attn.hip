@@ -8,8 +8,12 @@
 // Geometry: 64-row tiles, 4 waves x 16 rows; K/V (or Q/dO) tiles staged in LDS with a 2-float
 // row pad; the probability tile crosses LDS once per wave to turn the MFMA C layout (rows on
 // lane groups) into the A layout (rows on lanes), in a 66-float-stride image (conflict-free read).
-// Dropout keep bits: philox(seed; c0 = i >> 2, c1 = j, c2 = offset + b*H + h,
-// c3 = FIELD_DROPOUT << 24 | sub) word (i & 3); sub = the decoder layer.
+// Dropout keep bits, with c2 = offset + b*H + h (sub = the decoder layer / fractal level):
+//   byte mode (256 p an integer, e.g. p = 0.25): byte (i & 3) of word ((j >> 4) & 3) of
+//     philox(seed; i >> 2, 16 (j >> 6) + (j & 15), c2, FIELD_DROPOUT << 24 | (sub | 1 << 23)) >= 256 p —
+//     one block covers rows 4 (i >> 2) + 0..3 and columns j, j + 16, j + 32, j + 48 of a 64-key tile:
+//     exactly the 16 scores one lane holds in the forward and dQ kernels (one block per lane and tile)
+//   word mode: word (i & 3) of philox(seed; i >> 2, j, c2, FIELD_DROPOUT << 24 | sub) >= p 2^32.
 #include "kernels.h"
 #include "philox.h"
 
@@ -32,6 +36,10 @@ __device__ __forceinline__ uint32_t keep_word(uint64_t seed, uint32_t off, uint3
 __device__ __forceinline__ uint32_t qword(const u32x4_t& u, int r) {
   return r == 0 ? u.x : (r == 1 ? u.y : (r == 2 ? u.z : u.w));
 }
+// byte-mode keep byte (row & 3) of word (16-column group) of a lane's block
+__device__ __forceinline__ uint32_t qbyte(const u32x4_t& u, int word, int r) {
+  return (qword(u, word) >> (8 * r)) & 0xFFu;
+}
 
 struct AttnArgs {
   const float *Q, *K, *V, *O, *LSE, *dO, *Dl, *G;
@@ -41,9 +49,10 @@ struct AttnArgs {
   AttnLayout in, out, grad, gate;   // q/k/v; o/do/og; dq/dk/dv; gate
   float scale, inv_keep;
   uint32_t thresh;    // keep iff word >= thresh (thresh = 0: no dropout)
+  uint32_t thresh8;   // != 0: byte mode, keep iff byte >= thresh8
   uint64_t seed;
   uint32_t offset;
-  uint32_t c3;        // rng_c3(FIELD_DROPOUT, layer)
+  uint32_t c3;        // rng_c3(FIELD_DROPOUT, layer); byte mode: rng_c3(FIELD_DROPOUT, layer | 1 << 23)
   int causal;
 };
 
@@ -98,7 +107,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
     // keep words: this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block per key column
     // (word = row & 3), so one block per column instead of one per element
     u32x4_t kws[4] = {};
-    if (a.thresh) {
+    if (a.thresh8) {   // byte mode: one block holds all 16 keep bytes of this lane's scores
+      kws[0] = philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)(kt * 16 + lr), off, a.c3, a.seed);
+    } else if (a.thresh) {
 #pragma unroll
       for (int sub = 0; sub < 4; ++sub)
         kws[sub] = philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)(kt * TK + 16 * sub + lr), off,
@@ -126,7 +137,8 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
         const float p = (sv[sub] == -INFINITY) ? 0.f : expf(sv[sub] - mnew);
         rs += p;
         float pd = p;
-        if (a.thresh) pd = (qword(kws[sub], r) >= a.thresh) ? p * a.inv_keep : 0.f;
+        if (a.thresh8) pd = (qbyte(kws[0], sub, r) >= a.thresh8) ? p * a.inv_keep : 0.f;
+        else if (a.thresh) pd = (qword(kws[sub], r) >= a.thresh) ? p * a.inv_keep : 0.f;
         Ps[w][4 * lg + r][16 * sub + lr] = pd;
       }
 #pragma unroll
@@ -236,8 +248,17 @@ __global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const A
         // keep words of row i at key columns j0 + 16 w + 4 lg + 0..3: the four lanes of a quad hold
         // rows 4 (i >> 2) + 0..3; lane c computes the block of column 4 lg + c (its four words are
         // the quad's four rows) and a quad transpose hands every lane its row's word of each column
+        // (byte mode: lane c computes the block of column class 4 lg + c, takes word w — this wave's
+        // 16-column group — and the quad transpose deals byte (row & 3) of each column's word)
         uint32_t kq[4] = {0u, 0u, 0u, 0u};
-        if (a.thresh) {
+        if (a.thresh8) {
+          const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)((j0 >> 6) * 16 + 4 * lg + (lr & 3)), off,
+                                           a.c3, a.seed);
+          const uint32_t wd = qword(kb, w);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) kq[c] = (wd >> (8 * c)) & 0xFFu;
+          quad_transpose(kq, lane);
+        } else if (a.thresh) {
           const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)(j0 + 16 * w + 4 * lg + (lr & 3)), off,
                                            a.c3, a.seed);
           kq[0] = kb.x;
@@ -252,7 +273,8 @@ __global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const A
           const bool ok = (j <= i) && (j < len) && (i < n);
           const float p = ok ? expf(st[r] * a.scale - Ls[il]) : 0.f;
           float z = 1.f;
-          if (a.thresh && ok) z = (kq[r] >= a.thresh) ? a.inv_keep : 0.f;
+          if (a.thresh8 && ok) z = (kq[r] >= a.thresh8) ? a.inv_keep : 0.f;
+          else if (a.thresh && ok) z = (kq[r] >= a.thresh) ? a.inv_keep : 0.f;
           Ps[w][4 * lg + r][il] = p * z;
           dsr[sub][r] = p * (dpt[r] * z - Dls[il]);
         }
@@ -332,6 +354,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
       Vs[j][c] = jj < n ? a.V[ib + (int64_t)jj * isi + c] : 0.f;
     }
     __syncthreads();
+    // byte mode: one block per lane and key tile holds all 16 keep bytes of its scores
+    const u32x4_t kb8 = a.thresh8 ? philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)(kt * 16 + lr),
+                                                  off, a.c3, a.seed)
+                                  : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int sub = 0; sub < 4; ++sub) {
       f32x4v s_ = f32x4v{0.f, 0.f, 0.f, 0.f}, dp = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -342,16 +368,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
       }
       const int jl = 16 * sub + lr, j = kt * TK + jl;
       // this lane's rows q0 + 16 w + 4 lg + 0..3 share one Philox block (word = row & 3)
-      const u32x4_t kw = a.thresh ? philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)j, off,
-                                                  a.c3, a.seed)
-                                  : u32x4_t{0u, 0u, 0u, 0u};
+      const u32x4_t kw = (a.thresh && !a.thresh8) ? philox4x32_10((uint32_t)((q0 + 16 * w + 4 * lg) >> 2), (uint32_t)j,
+                                                                  off, a.c3, a.seed)
+                                                  : u32x4_t{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = q0 + 16 * w + 4 * lg + r;
         const bool ok = (j <= i) && (j < len) && (i < n);
         const float p = ok ? expf(s_[r] * a.scale - lse[r]) : 0.f;
         float z = 1.f;
-        if (a.thresh && ok) z = (qword(kw, r) >= a.thresh) ? a.inv_keep : 0.f;
+        if (a.thresh8 && ok) z = (qbyte(kb8, sub, r) >= a.thresh8) ? a.inv_keep : 0.f;
+        else if (a.thresh && ok) z = (qword(kw, r) >= a.thresh) ? a.inv_keep : 0.f;
         Ds[w][4 * lg + r][jl] = p * (dp[r] * z - dl[r]);
       }
     }
@@ -386,10 +413,11 @@ int fill_args(AttnArgs& a, const AttnProblem& p) {
   a.scale = p.scale;
   a.inv_keep = p.dropout > 0.f ? 1.f / (1.f - p.dropout) : 1.f;
   a.thresh = dropout_thresh(p.dropout);
+  a.thresh8 = dropout_thresh8(p.dropout);
   a.seed = p.seed;
   a.offset = p.offset;
-  XTRL_REQUIRE(p.sub < (1u << 24), "attn: dropout stream sub-index %u does not fit 24 bits", p.sub);
-  a.c3 = rng_c3(FIELD_DROPOUT, p.sub);
+  XTRL_REQUIRE(p.sub < (1u << 23), "attn: dropout stream sub-index %u does not fit 23 bits", p.sub);
+  a.c3 = rng_c3(FIELD_DROPOUT, a.thresh8 ? (p.sub | (1u << 23)) : p.sub);
   a.causal = p.causal;
   return XTRL_OK;
 }
