@@ -195,7 +195,8 @@ class OracleFractalPolicy(nn.Module):
     """Causal fractal actor-critic on the reference's parameter names (fractal_rl.py:349-446 layout,
     separate blocks per level).  ``cfg``: oracle.ref_port.ModelConfig."""
 
-    def __init__(self, cfg, levels, ff_mult=4):
+    def __init__(self, cfg, levels, ff_mult=None):
+        ff_mult = getattr(cfg, 'ff_mult', 4) if ff_mult is None else ff_mult
         super().__init__()
         from . import thirdparty as tp
         self.cfg, self.levels = cfg, levels

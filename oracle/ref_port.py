@@ -218,6 +218,7 @@ class ModelConfig:
     gate_values: bool = False
     value_residual: bool = False
     learned_mix: bool = False
+    ff_mult: int = 4          # x-transformers FeedForward mult, reached through world_model['ff_mult']
 
 
 class OracleWMAC(nn.Module):
@@ -233,7 +234,7 @@ class OracleWMAC(nn.Module):
                                    rotary_pos_emb=True, attn_dropout=cfg.dropout, ff_dropout=cfg.dropout,
                                    verbose=False, attn_gate_values=cfg.gate_values,
                                    add_value_residual=cfg.value_residual,
-                                   learned_value_residual_mix=cfg.learned_mix))
+                                   learned_value_residual_mix=cfg.learned_mix, ff_mult=cfg.ff_mult))
         self.reward_embed = nn.Parameter(torch.ones(d) * 1e-2)
         if cfg.continuous:
             self.action_embeds = nn.Linear(cfg.num_actions, d)
@@ -492,6 +493,7 @@ class LearnerConfig:
     gate_values: bool = False
     value_residual: bool = False
     learned_mix: bool = False
+    ff_mult: int = 4
     continuous: bool = False
     squash: bool = True
     clamp: tuple | None = None
@@ -545,7 +547,7 @@ class OracleLearner:
                          c.reward_range, 100, c.continuous, c.squash, c.evolutionary,
                          self.gp['dim'] if c.evolutionary else 0, c.frac_head_grad, c.beta_s, c.eps_clip,
                          c.value_clip, c.dropout, c.reward_dropout, True, c.gate_values, c.value_residual,
-                         c.learned_mix)
+                         c.learned_mix, c.ff_mult)
         self.model = model_factory(mc) if model_factory is not None else OracleWMAC(mc)
         if init_state_dict is not None:
             self.model.load_state_dict(init_state_dict)

@@ -340,8 +340,10 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
-                 hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None):
-    """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides."""
+                 hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None,
+                 ff_mult=4):
+    """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides.
+    ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult)."""
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(seed)
     factory = None
@@ -350,6 +352,8 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
         agent_extra = dict(agent_extra or {}, policy_body='fractal', fractal_levels=fractal_levels)
         factory = lambda mc: FR.OracleFractalPolicy(mc, fractal_levels)   # noqa: E731
     wm = dict(attn_dim_head=16, heads=4, depth=depth)
+    if ff_mult != 4:
+        wm['ff_mult'] = ff_mult
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     gp = dict(dim=gene_dim, num_genes_per_island=3, num_selected=2, tournament_size=2)
@@ -371,7 +375,7 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
                         learned_mix=gates, continuous=cont, clamp=(-1., 1.) if cont else None, evolutionary=evo,
                         evolve_every=1, evolve_after_step=0, gene_pool=gp, max_timesteps=T, batch_size=batch,
                         num_episodes_per_update=episodes, sim_mode=mode, hazard_log2=hazard, seed=seed,
-                        reward_dropout=reward_dropout)
+                        reward_dropout=reward_dropout, ff_mult=ff_mult)
     sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
     genes = learner.agent.gene_pool.genes.clone() if evo else None
     oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes, model_factory=factory)
@@ -423,10 +427,12 @@ def test_rollout_matches_oracle(depth, gates, evo):
         tol(learner.fitness(cum, torch.tensor([g for _, g in learner.episode_genes])), fitness, 1e-5, 1e-5)
 
 
-def test_rollout_d256_matches_oracle():
+@pytest.mark.parametrize('ff', [4, 2])
+def test_rollout_d256_matches_oracle(ff):
     """The C3 width (d = 256, 4 x 16 heads; the decode embedding kernel's fused layer-0 pre-norm, the
-    decode GEMM geometries of that shape) reproduces the oracle's batch-1 rollout."""
-    learner, env, oracle = make_learner(depth=2, gates=True, dim=256, episodes=20)
+    decode GEMM geometries of that shape) reproduces the oracle's batch-1 rollout; ff = 2: the one-launch
+    feed-forward kernel at world_model['ff_mult'] = 2 (4 hidden-unit workgroups per row panel instead of 8)."""
+    learner, env, oracle = make_learner(depth=2, gates=True, dim=256, episodes=20, ff_mult=ff)
     traj, lens, _, _ = learner.rollout_device(env, 0, 12)
     torch.cuda.synchronize()
     episodes, _ = oracle.rollout(0)
@@ -684,15 +690,18 @@ def oracle_minibatch_tensors(episodes):
     return states, actions, old_lp, rewards, bounds, values, lens, genes
 
 
-@pytest.mark.parametrize('evo,gates,cont,frac', [(False, False, False, None), (True, True, False, None),
-                                                  (False, True, True, None), (False, False, False, 2),
-                                                  (True, False, True, 3)])
-def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac):
+@pytest.mark.parametrize('evo,gates,cont,frac,ff', [(False, False, False, None, 4), (True, True, False, None, 4),
+                                                     (False, True, True, None, 4), (False, False, False, 2, 4),
+                                                     (True, False, True, 3, 4), (False, True, False, None, 2),
+                                                     (False, True, False, None, 3), (False, False, False, 2, 3)])
+def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac, ff):
     """BASELINE metric 'PPO loss delta vs CPU ref': for every minibatch of two learning updates the
     oracle recomputes loss and gradients with the GPU's current weights / RSNorm / genes on the
-    same minibatch; loss within 1e-4 relative, gradients within 1e-4 of the gradient scale."""
+    same minibatch; loss within 1e-4 relative, gradients within 1e-4 of the gradient scale.
+    ff != 4: world_model['ff_mult'] (feed-forward width 2d / 3d; 3d = 144 is not a multiple of the
+    decode feed-forward kernel's column tile, so the rollout takes its two-GEMM path)."""
     learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, cont=cont, T=10, episodes=6, batch=2, seed=5,
-                                        hazard=2, fractal_levels=frac)
+                                        hazard=2, fractal_levels=frac, ff_mult=ff)
     agent = learner.agent
     c = oracle.c
     worst = [0.]

@@ -97,7 +97,7 @@ class Agent(nn.Module):
         dev = self.accelerator.device
         wm = dict(world_model)
         known = {'attn_dim_head', 'heads', 'depth', 'attn_gate_values', 'add_value_residual',
-                 'learned_value_residual_mix'}
+                 'learned_value_residual_mix', 'ff_mult'}
         unknown = set(wm) - known
         if unknown:
             raise NotImplementedError(f'world_model options {sorted(unknown)} are not supported by the MI355X decoder')
@@ -112,7 +112,8 @@ class Agent(nn.Module):
                         frac_head_grad=frac_actor_critic_head_gradient, entropy_weight=beta_s, eps_clip=eps_clip,
                         value_clip=value_clip, dropout=dropout, reward_dropout=reward_dropout,
                         gate_values=wm.get('attn_gate_values', False), value_residual=wm.get('add_value_residual', False),
-                        learned_mix=wm.get('learned_value_residual_mix', False), rotary_abs_rollout=rotary_abs_rollout,
+                        learned_mix=wm.get('learned_value_residual_mix', False), ff_mult=int(wm.get('ff_mult', 4)),
+                        rotary_abs_rollout=rotary_abs_rollout,
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
         # policy body: the x-transformers Decoder (x_transformers_rl.py) or the per-timestep causal
