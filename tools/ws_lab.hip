@@ -20,13 +20,15 @@ int check_launch(const char*) { return hipGetLastError() == hipSuccess ? 0 : 1; 
 int main(int argc, char** argv) {
   int M = argc > 1 ? atoi(argv[1]) : 16384, N = argc > 2 ? atoi(argv[2]) : 256, K = argc > 3 ? atoi(argv[3]) : 1024;
   int ta = argc > 4 ? atoi(argv[4]) : 0, tb = argc > 5 ? atoi(argv[5]) : 0, mode = argc > 6 ? atoi(argv[6]) : 0;
+  const int kspan = argc > 7 ? atoi(argv[7]) : 0;   // > 0: cross-workgroup split of K (as gemm_wgrad)
+  const int splits = kspan > 0 ? (K + kspan - 1) / kspan : 1;
   float *A, *B, *C;
-  CK(hipMalloc(&A, (size_t)M * K * 4)); CK(hipMalloc(&B, (size_t)N * K * 4)); CK(hipMalloc(&C, (size_t)M * N * 4));
+  CK(hipMalloc(&A, (size_t)M * K * 4)); CK(hipMalloc(&B, (size_t)N * K * 4)); CK(hipMalloc(&C, (size_t)splits * M * N * 4));
   std::vector<float> h((size_t)std::max(M, N) * K);
   for (auto& v : h) v = (float)rand() / RAND_MAX - 0.5f;
   CK(hipMemcpy(A, h.data(), (size_t)M * K * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice));
-  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
   uint64_t* diag;
   CK(hipMalloc(&diag, (size_t)tiles * 2 * 4096 * 8));
   CK(hipMemset(diag, 0, (size_t)tiles * 2 * 4096 * 8));
@@ -35,6 +37,7 @@ int main(int argc, char** argv) {
   xtrl::GemmArgs a;
   a.A = A; a.B = B; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = N;
   a.lda = ta ? M : K; a.ldb = tb ? N : K;
+  if (kspan > 0) { a.kspan = kspan; a.c_split = (int64_t)M * N; }
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto run = [&]() {
     if (!ta && !tb) xtrl::launch_ws<false, false, xtrl::EPI_NONE, false>(a, 0);
@@ -44,10 +47,10 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 3; ++i) run();
   CK(hipEventRecord(e0)); for (int i = 0; i < 10; ++i) run(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-  printf("mode %d M=%d N=%d K=%d ta=%d tb=%d: %.1f us/launch, %.1f TF (diag build)\n", mode, M, N, K, ta, tb, ms * 100, 2.0 * M * N * K / (ms / 10 * 1e-3) / 1e12);
+  printf("mode %d M=%d N=%d K=%d ta=%d tb=%d splits=%d: %.1f us/launch, %.1f TF (diag build)\n", mode, M, N, K, ta, tb, splits, ms * 100, 2.0 * M * N * K / (ms / 10 * 1e-3) / 1e12);
   std::vector<uint64_t> d((size_t)tiles * 2 * 4096);
   CK(hipMemcpy(d.data(), diag, d.size() * 8, hipMemcpyDeviceToHost));
-  const int nk = K / 32, nsteps = 3 * ((nk + 2) / 3);
+  const int nk = (kspan > 0 ? kspan : K) / 32, nsteps = 3 * ((nk + 2) / 3);
   // per step averages (over workgroups) in s_memtime ticks
   double cc = 0, cw = 0, pc = 0, pl = 0, pw = 0; int n = 0;
   std::vector<double> per_c(nk, 0), per_p(nk, 0);
