@@ -1,5 +1,7 @@
 // Diagnostic build of the warp-specialised X6 GEMM (not part of the library): per-step
-// s_memtime stamps of one consumer and one producer wave per workgroup.
+// s_memtime stamps of one consumer and one producer wave per workgroup (-DXTRL_WS_DIAG), or, without
+// stamps, one mode fixed at compile time (-DXTRL_WS_MODE=m: 1 consumers skip the MFMAs, 2 producers
+// skip loads + splits, 3 producers load but do not split; production code otherwise).
 //   hipcc -O3 -std=c++17 -fno-slp-vectorize --offload-arch=gfx950 -DXTRL_WS_DIAG \
 //         -Ix-transformers-rl_amd/csrc tools/ws_lab.hip -o /tmp/ws_lab && /tmp/ws_lab M N K [ta tb]
 #include "../x-transformers-rl_amd/csrc/gemm.hip"
@@ -29,11 +31,13 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(A, h.data(), (size_t)M * K * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(B, h.data(), (size_t)N * K * 4, hipMemcpyHostToDevice));
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128) * splits;
+#ifdef XTRL_WS_DIAG
   uint64_t* diag;
   CK(hipMalloc(&diag, (size_t)tiles * 2 * 4096 * 8));
   CK(hipMemset(diag, 0, (size_t)tiles * 2 * 4096 * 8));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(xtrl::g_ws_diag), &diag, sizeof(diag)));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(xtrl::g_ws_mode), &mode, sizeof(mode)));
+#endif
   xtrl::GemmArgs a;
   a.A = A; a.B = B; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = N;
   a.lda = ta ? M : K; a.ldb = tb ? N : K;
@@ -47,7 +51,16 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 3; ++i) run();
   CK(hipEventRecord(e0)); for (int i = 0; i < 10; ++i) run(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+#ifndef XTRL_WS_DIAG
+#ifdef XTRL_WS_MODE
+  mode = XTRL_WS_MODE;
+#endif
+#endif
   printf("mode %d M=%d N=%d K=%d ta=%d tb=%d splits=%d: %.1f us/launch, %.1f TF (diag build)\n", mode, M, N, K, ta, tb, splits, ms * 100, 2.0 * M * N * K / (ms / 10 * 1e-3) / 1e12);
+#ifndef XTRL_WS_DIAG
+  (void)tiles;
+  return 0;
+#else
   std::vector<uint64_t> d((size_t)tiles * 2 * 4096);
   CK(hipMemcpy(d.data(), diag, d.size() * 8, hipMemcpyDeviceToHost));
   const int nk = (kspan > 0 ? kspan : K) / 32, nsteps = 3 * ((nk + 2) / 3);
@@ -74,4 +87,5 @@ int main(int argc, char** argv) {
   printf("wg0 loop span %llu ticks for %d steps; all-wg loop span %llu\n", (unsigned long long)(c0[(nk + (nk & 1)) * 4] - c0[0]), nk,
          (unsigned long long)(tmax - tmin));
   return 0;
+#endif
 }

@@ -1156,6 +1156,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
     __syncthreads();
 #ifdef XTRL_WS_DIAG
     const int mode = g_ws_mode;
+#elif defined(XTRL_WS_MODE)   // tools/ws_lab.hip stamp-free builds: the same modes, fixed at compile time
+    constexpr int mode = XTRL_WS_MODE;
 #else
     constexpr int mode = 0;
 #endif
@@ -1201,6 +1203,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
       WS_STAMP(t, 0);
 #ifdef XTRL_WS_DIAG
       if (t < nk && g_ws_mode != 1) compute(smem + (t & 1) * IMG);
+#elif defined(XTRL_WS_MODE)
+      if (t < nk && XTRL_WS_MODE != 1) compute(smem + (t & 1) * IMG);
 #else
       if (t < nk) compute(smem + (t & 1) * IMG);
 #endif
