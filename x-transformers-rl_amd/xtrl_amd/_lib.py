@@ -193,7 +193,8 @@ def load():
             raise RuntimeError(f'libxtrl_hip ABI {lib.xtrl_abi_version()} != {ABI_VERSION}')
         from ._srchash import source_hash
         built, here = lib.xtrl_source_hash().decode(), source_hash()
-        if built != here:   # a library compiled from other sources than the ones in this tree
+        # (an explicit XTRL_LIB — A/B experiments against a saved build — is taken as chosen)
+        if built != here and 'XTRL_LIB' not in os.environ:   # compiled from other sources than this tree's
             raise RuntimeError(f'{LIB_PATH} was built from sources {built}, the tree holds {here}: rebuild it '
                                f'with `make -C x-transformers-rl_amd` or __graft_entry__.build()')
         for cname, py in STRUCTS.items():   # a stale build against an edited header fails here
