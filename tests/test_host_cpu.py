@@ -230,3 +230,15 @@ def test_vector_env_info_dict_is_read_per_env():
         ns, r, term, trunc = step(np.zeros(W, dtype=np.int32), np.ones(W, dtype=bool))
         assert trunc.tolist() == want, (info, trunc)
         assert term.tolist() == [False, True, False, False]
+
+
+def test_world_model_option_validation():
+    """x-transformers Decoder kwargs: implementation switches (attn_flash) are accepted, options the
+    MI355X decoder does not implement are refused loudly (xtrl.py:721-734 splats world_model)."""
+    from xtrl_amd import Learner
+    kw = dict(num_episodes_per_update=2, batch_size=2, accelerate_kwargs=dict(device='cpu'),
+              agent_kwargs=dict(hidden_dim=16), use_graph=False)
+    a = Learner(5, 2, (-1., 1.), world_model=dict(attn_dim_head=16, heads=4, depth=1, attn_flash=True), **kw).agent
+    assert a.cfg.depth == 1 and a.cfg.heads == 4
+    with pytest.raises(NotImplementedError):
+        Learner(5, 2, (-1., 1.), world_model=dict(attn_dim_head=16, heads=4, depth=1, ff_glu=True), **kw)

@@ -96,6 +96,11 @@ class Agent(nn.Module):
         self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
         dev = self.accelerator.device
         wm = dict(world_model)
+        # x-transformers switches that select an implementation, not the math: accepted and ignored
+        # (attn_flash: fused scaled-dot-product attention instead of the explicit softmax — the same
+        # function; the learn step's attention here is always the fused HIP kernel)
+        for k in ('attn_flash',):
+            wm.pop(k, None)
         known = {'attn_dim_head', 'heads', 'depth', 'attn_gate_values', 'add_value_residual',
                  'learned_value_residual_mix', 'ff_mult'}
         unknown = set(wm) - known
