@@ -102,7 +102,10 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
 // k_embed with layer 0's attention pre-norm folded in (d <= 256: thread c owns column c): per
 // batch of EMB_U tokens the row sums and the centred sums of squares meet through LDS (two
 // barriers), then x0, LN(x0) gamma and (mean, rstd) are stored — k_ln_fwd's arithmetic (two-pass
-// variance, eps 1e-5) with the row sum associated per wave, then over the 4 waves
+// variance, eps 1e-5) with the row sum associated per wave, then over the 4 waves.  One batch per
+// workgroup (EMB_LN_TOK = EMB_U): the batches' load / barrier round trips run in parallel
+// workgroups instead of one after another (C3: 2048 workgroups, 45 -> see DESIGN §7 a launch)
+constexpr int EMB_LN_TOK = EMB_U;
 template <int S_>
 __global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
   constexpr int MS = S_ > 0 ? S_ : EMB_MAXS;
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
   const float bse = a.b_se[cc], re = a.reward_embed[cc], gam = on ? a.ln_g[cc] : 0.f;
   const float bemb = a.continuous ? a.act_emb_b[cc] : 0.f;
   const float inv_d = 1.0f / (float)a.d;
-  for (int t0 = blockIdx.x * EMB_TOK; t0 < min(a.T, (int)(blockIdx.x + 1) * EMB_TOK); t0 += EMB_U) {
+  for (int t0 = blockIdx.x * EMB_LN_TOK; t0 < min(a.T, (int)(blockIdx.x + 1) * EMB_LN_TOK); t0 += EMB_U) {
     float x[EMB_U], se[EMB_U], an[EMB_U], le[EMB_U];
 #pragma unroll
     for (int u = 0; u < EMB_U; ++u) {
@@ -470,11 +473,11 @@ __global__ __launch_bounds__(256) void k_colsum_part(const float* src, int ld, i
 // lane owns (column lane % CS_COLS, chunk group) and sums its chunks in four chains (loads in flight),
 // then the CS_G group totals of a column are added in a fixed order (deterministic)
 constexpr int CS_WAVES = 16, CS_COLS = 16, CS_G = 64 * CS_WAVES / CS_COLS;
-__global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
+__device__ __forceinline__ void colsum_final_body(const float* part, int chunks, int cols, float* dst, int bx) {
   __shared__ float red[CS_G][CS_COLS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int cl = lane % CS_COLS, g = w * (64 / CS_COLS) + lane / CS_COLS;
-  const int c = blockIdx.x * CS_COLS + cl;
+  const int c = bx * CS_COLS + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < cols) {
     int k = g;
@@ -489,7 +492,7 @@ __global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* par
   red[g][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (threadIdx.x < CS_COLS) {
-    const int cc = blockIdx.x * CS_COLS + threadIdx.x;
+    const int cc = bx * CS_COLS + threadIdx.x;
     if (cc < cols) {
       float v = 0.f;
 #pragma unroll 8
@@ -498,6 +501,61 @@ __global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* par
     }
   }
 }
+__global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final(const float* part, int chunks, int cols, float* dst) {
+  colsum_final_body(part, chunks, cols, dst, blockIdx.x);
+}
+
+// the LayerNorm d gamma column sums of a backward, deferred: each fused LayerNorm-backward GEMM
+// epilogue writes its row-tile partials into a plane of its own, and ONE launch (blockIdx.y = job)
+// finishes them all — each sum exactly k_colsum_final's, into a distinct gamma (bit-identical)
+constexpr int kMaxColsumJobs = 16;
+struct ColsumJobs {
+  const float* part[kMaxColsumJobs];
+  float* dst[kMaxColsumJobs];
+  int chunks[kMaxColsumJobs];
+  int cols[kMaxColsumJobs];
+};
+__global__ __launch_bounds__(64 * CS_WAVES) void k_colsum_final_multi(const ColsumJobs J) {
+  const int j = blockIdx.y;
+  if ((int)blockIdx.x * CS_COLS >= J.cols[j]) return;   // (workgroup-uniform)
+  colsum_final_body(J.part[j], J.chunks[j], J.cols[j], J.dst[j], blockIdx.x);
+}
+struct ColsumQueue {
+  ColsumJobs J{};
+  int n = 0, max_cols = 0;
+  float* base = nullptr;
+  int64_t cap = 0, used = 0;
+  // a plane of chunks x cols partials whose column sums go to dst, or NULL (full: sum now)
+  // the plane, flushing the queued jobs first when it is full (their planes are then free)
+  float* take_or_flush(int chunks, int cols, float* dst, hipStream_t s, int* rc) {
+    *rc = XTRL_OK;
+    float* P = take(chunks, cols, dst);
+    if (!P && base && n > 0) {
+      if ((*rc = flush(s))) return nullptr;
+      P = take(chunks, cols, dst);
+    }
+    return P;
+  }
+  float* take(int chunks, int cols, float* dst) {
+    const int64_t need = (int64_t)chunks * cols;
+    if (!base || n == kMaxColsumJobs || used + need > cap) return nullptr;
+    float* P = base + used;
+    used += (need + 3) & ~(int64_t)3;
+    J.part[n] = P; J.dst[n] = dst; J.chunks[n] = chunks; J.cols[n] = cols;
+    ++n;
+    max_cols = std::max(max_cols, cols);
+    return P;
+  }
+  int flush(hipStream_t s) {
+    if (n > 0) {
+      hipLaunchKernelGGL(k_colsum_final_multi, dim3((max_cols + CS_COLS - 1) / CS_COLS, n), dim3(64 * CS_WAVES), 0, s,
+                         J);
+      XTRL_LAUNCHED("colsum_final_multi");
+    }
+    n = 0; max_cols = 0; used = 0;
+    return XTRL_OK;
+  }
+};
 
 // discrete action-embedding gradient: part[chunk][a][c] = sum over rows of the chunk with
 // prev[r] == a of g1[r][c]  +  rows with next[r] == a of g2[r][c]   (A <= EMB_MAXA, registers)
@@ -914,14 +972,18 @@ int linear_res_ln(const Ctx& c, const float* A, int lda, const float* W, const f
 // dx = LN_backward(dY W; x, stats, gamma) + dres in one launch; d gamma accumulated from the
 // per-row-tile partials
 int dgrad_ln_bwd(const Ctx& c, const float* dY, int ldy, const float* W, int N, const float* x, const float* st,
-                 const float* gamma, const float* dres, float* dx, float* dgamma) {
+                 const float* gamma, const float* dres, float* dx, float* dgamma, ColsumQueue* cq = nullptr) {
   const int d = c.D->d, nb = (c.T + gemm_ln_rows(d) - 1) / gemm_ln_rows(d);
   XTRL_REQUIRE((int64_t)nb * d <= c.D->part_floats, "train: partial-sum workspace too small");
+  int rc = XTRL_OK;
+  float* P = cq ? cq->take_or_flush(nb, d, dgamma, c.s, &rc) : nullptr;   // deferred: the queue's one launch
+  if (rc) return rc;
   GemmArgs g;
   g.A = dY; g.lda = ldy; g.B = W; g.ldb = d; g.C = dx; g.ldc = d; g.M = c.T; g.N = d; g.K = N;
-  g.ln_g = gamma; g.ln_x = x; g.ln_stats = const_cast<float*>(st); g.ln_dres = dres; g.ln_part = c.D->part;
-  if (int rc = gemm_run(g, 0, 1, EPI_LN_BWD, c.s)) return rc;
-  hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
+  g.ln_g = gamma; g.ln_x = x; g.ln_stats = const_cast<float*>(st); g.ln_dres = dres; g.ln_part = P ? P : c.D->part;
+  if ((rc = gemm_run(g, 0, 1, EPI_LN_BWD, c.s))) return rc;
+  if (!P)
+    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
   XTRL_LAUNCHED("train dgrad_ln_bwd");
   return XTRL_OK;
 }
@@ -1064,8 +1126,8 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
     ea.ln_g = c.P(L0.ln_attn);
     ea.xn = L0.xn_attn;
     ea.st = L0.st_attn;
-    if (D->S == 8) hipLaunchKernelGGL(k_embed_ln<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
-    else hipLaunchKernelGGL(k_embed_ln<0>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
+    if (D->S == 8) hipLaunchKernelGGL(k_embed_ln<8>, dim3(blocks(T, EMB_LN_TOK)), dim3(256), 0, s, ea);
+    else hipLaunchKernelGGL(k_embed_ln<0>, dim3(blocks(T, EMB_LN_TOK)), dim3(256), 0, s, ea);
   } else if (D->S == 8) {
     hipLaunchKernelGGL(k_embed<8>, dim3(blocks(T, EMB_TOK)), dim3(256), 0, s, ea);
   } else {
@@ -1139,12 +1201,25 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     const char* e = getenv("XTRL_SPLITK_DEFER");
     return !(e && atoi(e) == 0);
   }();
+  // the LayerNorm d gamma sums of the final norm and the decoder blocks: deferred to one launch after
+  // the blocks (nothing else writes the partial workspace until the embeddings), or at each gradient
+  // bucket; XTRL_LN_COLSUM_DEFER=0: a column-sum launch after every LayerNorm-backward GEMM
+  static const bool cs_defer = [] {
+    const char* e = getenv("XTRL_LN_COLSUM_DEFER");
+    return !(e && atoi(e) == 0);
+  }();
+  ColsumQueue csq;
+  if (cs_defer && ln_fusable(D) && D->scratch_per_layer) {
+    csq.base = D->part;
+    csq.cap = D->part_floats;
+  }
   SplitKQueue skq;
   const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
   // data-parallel gradient buckets: flush the bucket's deferred reductions, then record its events
   int bucket = 0;
   auto bucket_done = [&]() -> int {
     if (!D->grad_events) return XTRL_OK;
+    if (int rc = csq.flush(s)) return rc;
     if (int rc = splitk_flush(skq, cw.s)) return rc;
     if (hipEventRecord((hipEvent_t)D->grad_events[2 * bucket], s) != hipSuccess ||
         hipEventRecord((hipEvent_t)D->grad_events[2 * bucket + 1], cw.s) != hipSuccess) {
@@ -1168,10 +1243,13 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     g.A = D->dz1; g.lda = 4 * d; g.B = c.P(D->w_h1); g.ldb = D->in_dim; g.C = dx_top; g.ldc = d;
     g.M = T; g.N = d; g.K = 4 * d;
     g.ln_g = c.P(D->ln_final); g.ln_x = D->x_final; g.ln_stats = D->st_final;
-    g.ln_gpre = D->dewa; g.ln_ldg = 2 * d; g.ln_gscale = D->frac_head_grad; g.ln_part = D->part;
+    float* P = csq.take_or_flush(nb, d, c.G(D->ln_final), s, &rc);
+    if (rc) return rc;
+    g.ln_gpre = D->dewa; g.ln_ldg = 2 * d; g.ln_gscale = D->frac_head_grad; g.ln_part = P ? P : D->part;
     if ((rc = gemm_run(g, 0, 1, EPI_LN_BWD2, s))) return rc;
-    hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, s, D->part, nb, d,
-                       c.G(D->ln_final));
+    if (!P)
+      hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, s, D->part, nb, d,
+                         c.G(D->ln_final));
     XTRL_LAUNCHED("train final-norm backward");
   } else if ((rc = ln_bwd(c, D->dac, D->in_dim, D->frac_head_grad, D->dewa, 2 * d, D->x_final, D->st_final,
                           c.P(D->ln_final), nullptr, dx_top, c.G(D->ln_final)))) {
@@ -1221,7 +1299,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if (fuse) {
       if ((rc = wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
       if ((rc = dgrad_ln_bwd(c, dff, lf, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), gout, Gx2(li),
-                             c.G(Ly.ln_ff))))
+                             c.G(Ly.ln_ff), &csq)))
         return rc;
       xg = Gx2(li);
     } else {
@@ -1268,7 +1346,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if (fuse) {
       if ((rc = wait(e_ff2))) return rc;   // this block's FF2 weight gradient read dx
       if ((rc = dgrad_ln_bwd(c, dproj, Ly.n_qkv, c.P(Ly.w_proj), Ly.n_qkv, Ly.x_attn, Ly.st_attn, c.P(Ly.ln_attn),
-                             Gx2(li), Gx(li), c.G(Ly.ln_attn))))
+                             Gx2(li), Gx(li), c.G(Ly.ln_attn), &csq)))
         return rc;
       e_out_prev = e_out;
     } else {
@@ -1280,6 +1358,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     }
     if ((rc = bucket_done())) return rc;   // bucket L - li: decoder block li
   }
+  if ((rc = csq.flush(s))) return rc;   // (before the embeddings reuse the partial workspace)
   // ---- embeddings: dx is d x0
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
