@@ -399,6 +399,178 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused backward for short episodes (n <= FB_MAXN, dh = 16): one workgroup per (episode, head)
+// walks its key tiles; per (key tile, query tile) pair it forms P, P~ and dS ONCE and takes dV, dK
+// (as k_attn_bwd_dkdv) and dQ from them — the dQ kernel's second pass over the same pairs (scores,
+// softmax, keep bits and dP recomputed) is gone.  dQ: after the four waves' dS images of the pair are
+// in LDS, wave w multiplies rows 16 w .. 16 w + 15 of dS (queries) by the key tile (staged in LDS)
+// into its register accumulator of that query tile; the pairs are visited in (key tile, query tile)
+// order, the same for every workgroup (deterministic).  Keep bits, masks and D = rowsum(dO * O) as
+// k_attn_bwd_dkdv (bit-identical dK / dV; dQ sums key tiles in ascending order like k_attn_bwd_dq).
+constexpr int FB_MAXN = 128, FB_QT = FB_MAXN / TQ;
+template <int DH>
+__global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
+  constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
+  __shared__ float Qs[TQ][KST], dOs[TQ][KST], Ks[TK][KST];
+  __shared__ float Ls[TQ], Dls[TQ];
+  __shared__ float Ps[4][16][PST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int bh = blockIdx.x, b = bh / a.H, n = a.n;
+  const int len = a.lens[b];
+  const int h = bh - b * a.H;
+  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
+  const int lr = lane & 15, lg = lane >> 4;
+  const uint32_t off = a.offset + (uint32_t)bh;
+  const int nq = (n + TQ - 1) / TQ;
+
+  f32x4v dq[FB_QT][ND];
+#pragma unroll
+  for (int q = 0; q < FB_QT; ++q)
+#pragma unroll
+    for (int d = 0; d < ND; ++d) dq[q][d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  for (int kt = 0; kt < nq; ++kt) {
+    const int j0 = kt * TK;
+    float ka[KS], va[KS];
+    {
+      const int j = j0 + 16 * w + lr;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        ka[s] = (j < n) ? a.K[ib + (int64_t)j * isi + 4 * s + lg] : 0.f;
+        va[s] = (j < n) ? a.V[ib + (int64_t)j * isi + 4 * s + lg] : 0.f;
+      }
+    }
+    f32x4v dk[ND], dv[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      dk[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      dv[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    if (j0 < len) {
+#pragma unroll
+      for (int qt = 0; qt < FB_QT; ++qt) {
+        if (qt < kt || qt >= nq) continue;   // (workgroup-uniform) causal: query tiles from the key tile on
+        __syncthreads();
+        for (int x = tid; x < TQ * DH; x += 256) {
+          const int i = x / DH, c = x - i * DH, ii = qt * TQ + i, jj = j0 + i;
+          Qs[i][c] = ii < n ? a.Q[ib + (int64_t)ii * isi + c] : 0.f;
+          dOs[i][c] = ii < n ? a.dO[ob + (int64_t)ii * osi + c] : 0.f;
+          Ks[i][c] = jj < n ? a.K[ib + (int64_t)jj * isi + c] : 0.f;
+        }
+        float orow[DH];
+        if (tid < TQ) {
+          const int ii = qt * TQ + tid;
+          Ls[tid] = ii < n ? a.LSE[(int64_t)bh * n + ii] : 0.f;
+#pragma unroll
+          for (int c = 0; c < DH; ++c) orow[c] = ii < n ? a.O[ob + (int64_t)ii * osi + c] : 0.f;
+        }
+        __syncthreads();
+        if (tid < TQ) {
+          float dsum = 0.f;
+#pragma unroll
+          for (int c = 0; c < DH; ++c) dsum += dOs[tid][c] * orow[c];
+          Dls[tid] = dsum;
+        }
+        __syncthreads();
+        float dsr[4][4];
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) {
+          f32x4v st = f32x4v{0.f, 0.f, 0.f, 0.f}, dpt = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            st = mfma16(ka[s], Qs[16 * sub + lr][4 * s + lg], st);
+            dpt = mfma16(va[s], dOs[16 * sub + lr][4 * s + lg], dpt);
+          }
+          const int il = 16 * sub + lr, i = qt * TQ + il;
+          uint32_t kq[4] = {0u, 0u, 0u, 0u};
+          if (a.thresh8) {
+            const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)((j0 >> 6) * 16 + 4 * lg + (lr & 3)), off,
+                                             a.c3, a.seed);
+            const uint32_t wd = qword(kb, w);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kq[c] = (wd >> (8 * c)) & 0xFFu;
+            quad_transpose(kq, lane);
+          } else if (a.thresh) {
+            const u32x4_t kb = philox4x32_10((uint32_t)(i >> 2), (uint32_t)(j0 + 16 * w + 4 * lg + (lr & 3)), off,
+                                             a.c3, a.seed);
+            kq[0] = kb.x;
+            kq[1] = kb.y;
+            kq[2] = kb.z;
+            kq[3] = kb.w;
+            quad_transpose(kq, lane);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = j0 + 16 * w + 4 * lg + r;
+            const bool ok = (j <= i) && (j < len) && (i < n);
+            const float p = ok ? expf(st[r] * a.scale - Ls[il]) : 0.f;
+            float z = 1.f;
+            if (a.thresh8 && ok) z = (kq[r] >= a.thresh8) ? a.inv_keep : 0.f;
+            else if (a.thresh && ok) z = (kq[r] >= a.thresh) ? a.inv_keep : 0.f;
+            Ps[w][4 * lg + r][il] = p * z;
+            dsr[sub][r] = p * (dpt[r] * z - Dls[il]);
+          }
+        }
+        wave_sync();
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+          for (int s = 0; s < TQ / 4; ++s) dv[d] = mfma16(Ps[w][lr][4 * s + lg], dOs[4 * s + lg][16 * d + lr], dv[d]);
+        wave_sync();
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Ps[w][4 * lg + r][16 * sub + lr] = dsr[sub][r];
+        wave_sync();
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+          for (int s = 0; s < TQ / 4; ++s) dk[d] = mfma16(Ps[w][lr][4 * s + lg], Qs[4 * s + lg][16 * d + lr], dk[d]);
+        __syncthreads();   // every wave's dS image of the pair is in LDS
+        // dQ rows 16 w .. 16 w + 15 of this query tile: dS[query][key] = image [key / 16][key % 16][query]
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+#pragma unroll
+          for (int s = 0; s < TK / 4; ++s) {
+            const int j = 4 * s + lg;
+            dq[qt][d] = mfma16(Ps[j >> 4][j & 15][16 * w + lr], Ks[j][16 * d + lr], dq[qt][d]);
+          }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = j0 + 16 * w + 4 * lg + r;
+      if (j < n) {
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          a.dK[gb + (int64_t)j * gsi + 16 * d + lr] = dk[d][r] * a.scale;
+          a.dV[gb + (int64_t)j * gsi + 16 * d + lr] = dv[d][r];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int qt = 0; qt < FB_QT; ++qt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = qt * TQ + 16 * w + 4 * lg + r;
+      if (qt < nq && i < n) {
+#pragma unroll
+        for (int d = 0; d < ND; ++d) a.dQ[gb + (int64_t)i * gsi + 16 * d + lr] = dq[qt][d][r] * a.scale;
+      }
+    }
+}
+
+bool attn_fused_bwd_on() {   // XTRL_ATTN_FUSED_BWD=1: the fused backward (opt-in)
+  static const bool on = [] {
+    const char* e = getenv("XTRL_ATTN_FUSED_BWD");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+
 int fill_args(AttnArgs& a, const AttnProblem& p) {
   XTRL_REQUIRE(p.dh == 16 || p.dh == 32 || p.dh == 64, "attn: dim_head %d unsupported (16/32/64)", p.dh);
   XTRL_REQUIRE(p.lens && p.H > 0 && p.n > 0 && p.b > 0, "attn: bad arguments");
@@ -465,7 +637,9 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
   a.dV = dv;
   // (D = rowsum(dO * O) is formed inside k_attn_bwd_dkdv, whose key-tile-0 workgroups store it for dq)
   dim3 grid((p.n + TQ - 1) / TQ, p.b * p.H);
-  if (p.dh == 16) {
+  if (p.dh == 16 && p.n <= FB_MAXN && attn_fused_bwd_on()) {   // short episodes: one fused launch
+    hipLaunchKernelGGL(k_attn_bwd_fused<16>, dim3(p.b * p.H), dim3(256), 0, s, a);
+  } else if (p.dh == 16) {
     hipLaunchKernelGGL(k_attn_bwd_dkdv<16>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_attn_bwd_dq<16>, grid, dim3(256), 0, s, a);
   } else if (p.dh == 32) {
