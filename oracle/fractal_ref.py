@@ -71,9 +71,11 @@ def _layernorm(x, sd, name):
 
 
 def _block(x, g, sd, pre, heads, dim_head, key_mask=None):
-    """FractalProcessingBlock.forward (fractal_rl.py:120-136), use_global_attention=True."""
+    """FractalProcessingBlock.forward (fractal_rl.py:120-136), use_global_attention=True; ``g`` None
+    skips the global-state read and its norm (:126)."""
     x = _layernorm(x + _attention(x, x, sd, pre + '.self_attn', heads, dim_head, key_mask), sd, pre + '.norm1')
-    x = _layernorm(x + _attention(x, g, sd, pre + '.global_attn', heads, dim_head), sd, pre + '.norm2')
+    if g is not None:
+        x = _layernorm(x + _attention(x, g, sd, pre + '.global_attn', heads, dim_head), sd, pre + '.norm2')
     h = F.gelu(_linear(x, sd, pre + '.ff.ff.0.0'))
     return _layernorm(x + _linear(h, sd, pre + '.ff.ff.2'), sd, pre + '.norm3')
 

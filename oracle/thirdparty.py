@@ -269,6 +269,41 @@ class FeedForward(nn.Module):
         return self.ff(x)
 
 
+class XAttention(nn.Module):
+    """x-transformers ``Attention`` as fractal_rl.py builds and calls it (:87-102, :123, :127):
+    ``Attention(dim, heads, dim_head, dropout, dim_context=None)``, ``forward(x, context=None,
+    mask=None)``; not causal, no rotary, no gates.  q from x, k / v from ``context`` (default x);
+    ``mask`` masks keys only when there is no context (upstream: ``input_mask = context_mask``, else
+    ``mask`` for self-attention), by -finfo.max; post-softmax dropout; heads merged, ``to_out``."""
+
+    def __init__(self, dim, heads=8, dim_head=64, dropout=0., dim_context=None, **unsupported):
+        super().__init__()
+        if unsupported:
+            raise NotImplementedError(f'restated Attention does not model {sorted(unsupported)}')
+        inner, ctx = heads * dim_head, dim_context or dim
+        self.heads, self.dim_head = heads, dim_head
+        self.to_q = nn.Linear(dim, inner, bias=False)
+        self.to_k = nn.Linear(ctx, inner, bias=False)
+        self.to_v = nn.Linear(ctx, inner, bias=False)
+        self.to_out = nn.Linear(inner, dim, bias=False)
+        self.attn_dropout = nn.Dropout(dropout)
+
+    def forward(self, x, context=None, mask=None, context_mask=None):
+        b, i, _ = x.shape
+        kv = x if context is None else context
+        j = kv.shape[1]
+        h, dh = self.heads, self.dim_head
+        q = self.to_q(x).reshape(b, i, h, dh).transpose(1, 2)
+        k = self.to_k(kv).reshape(b, j, h, dh).transpose(1, 2)
+        v = self.to_v(kv).reshape(b, j, h, dh).transpose(1, 2)
+        sim = q @ k.transpose(-1, -2) * dh ** -0.5
+        key_mask = context_mask if context is not None else mask
+        if key_mask is not None:
+            sim = sim.masked_fill(~key_mask[:, None, None, :], -torch.finfo(sim.dtype).max)
+        out = self.attn_dropout(sim.softmax(dim=-1)) @ v
+        return self.to_out(out.transpose(1, 2).reshape(b, i, h * dh))
+
+
 class _Residual(nn.Module):
     def forward(self, out, residual):
         return out + residual

@@ -41,13 +41,14 @@ def load_reference():
     mod('einx', multiply=tp.einx.multiply, less=tp.einx.less, where=tp.einx.where)
     mod('assoc_scan', AssocScan=tp.AssocScan)
     mod('hl_gauss_pytorch', HLGaussLoss=tp.HLGaussLoss)
-    mod('x_transformers', Decoder=tp.Decoder, ContinuousTransformerWrapper=tp.ContinuousTransformerWrapper)
+    mod('x_transformers', Decoder=tp.Decoder, ContinuousTransformerWrapper=tp.ContinuousTransformerWrapper,
+        Attention=tp.XAttention, FeedForward=tp.FeedForward)
     mod('ema_pytorch', EMA=tp.EMA)
     mod('adam_atan2_pytorch', AdoptAtan2=tp.AdoptAtan2)
     pkg = mod('x_transformers_rl')
     pkg.__path__ = [str(REF)]
     out = {}
-    for name in ('distributed', 'evolution', 'x_transformers_rl'):
+    for name in ('distributed', 'evolution', 'x_transformers_rl', 'fractal_rl'):
         spec = importlib.util.spec_from_file_location(f'x_transformers_rl.{name}', REF / f'{name}.py')
         m = importlib.util.module_from_spec(spec)
         sys.modules[spec.name] = m
@@ -222,6 +223,74 @@ def gen_evolve(X, E):
     save('evolve', **out)
 
 
+def _perturb(module, seed):
+    """Non-trivial weights for a fixture: every parameter redrawn (LayerNorm gains around 1), so the
+    level embeddings, the global-state init and the norms all matter."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            scale = 1.0 / p.shape[-1] ** 0.5 if p.ndim > 1 else 0.3
+            base = 1.0 if ('norm' in name and name.endswith('weight')) else 0.0
+            p.copy_(torch.randn(p.shape, generator=g) * scale + base)
+
+
+def gen_fractal(Fr):
+    """The reference's own fractal modules (fractal_rl.py), eval mode, x-transformers Attention /
+    FeedForward restated (oracle/thirdparty.py XAttention / FeedForward):
+      FractalLevelEmbedding.forward            :63-67
+      FractalProcessingBlock.forward           :116-132 (with and without the global state, ragged mask)
+      FractalEncoder.forward                   :276-346 (separate / shared / hypernetwork blocks)
+      FractalWorldModelActorCritic.forward     :548-619 (discrete + gene, continuous; n = 8 and n = 1)"""
+    torch.manual_seed(21)
+    g = torch.Generator().manual_seed(21)
+    out = {}
+    le = Fr.FractalLevelEmbedding(24, 5)
+    _perturb(le, 1)
+    out.update(sd_arrays('le.', le.state_dict()))
+    out['le.out'] = torch.stack([le(i) for i in range(5)])
+
+    blk = Fr.FractalProcessingBlock(32, heads=4, dim_head=8, dropout=0.1).eval()
+    _perturb(blk, 2)
+    x = torch.randn(3, 7, 32, generator=g)
+    gs = torch.randn(3, 1, 32, generator=g)
+    mask = torch.arange(7)[None] < torch.tensor([7, 4, 1])[:, None]
+    with torch.no_grad():
+        out.update(sd_arrays('blk.', blk.state_dict()))
+        out.update({'blk.x': x, 'blk.g': gs, 'blk.mask': mask, 'blk.out': blk(x, gs, mask),
+                    'blk.out_nomask': blk(x, gs), 'blk.out_noglobal': blk(x, None, mask)})
+
+    xs = torch.randn(3, 9, 6, generator=g)
+    emask = torch.arange(9)[None] < torch.tensor([9, 5, 1])[:, None]
+    out.update({'enc.x': xs, 'enc.mask': emask})
+    for tag, kw in (('sep', {}), ('share', dict(share_weights=True)), ('hyper', dict(use_hypernetwork=True))):
+        enc = Fr.FractalEncoder(6, embed_dim=32, num_levels=3, heads=4, dim_head=8, dropout=0.1, **kw).eval()
+        _perturb(enc, 3)
+        with torch.no_grad():
+            agg, levels = enc(xs, mask=emask if tag == 'sep' else None, return_all_levels=True)
+        out.update(sd_arrays(f'enc_{tag}.', enc.state_dict()))
+        out[f'enc_{tag}.agg'] = agg
+        out[f'enc_{tag}.levels'] = torch.stack(levels)
+
+    for tag, cont, evo in (('wm_d', False, True), ('wm_c', True, False)):
+        wm = Fr.FractalWorldModelActorCritic(6, 4, 100, (-2., 2.), embed_dim=32, num_fractal_levels=2, heads=4,
+                                             dim_head=8, dropout=0.1, continuous_actions=cont, squash_continuous=cont,
+                                             evolutionary=evo, dim_latent_gene=8 if evo else None).eval()
+        _perturb(wm, 4)
+        out.update(sd_arrays(f'{tag}.', wm.state_dict()))
+        for n in (8, 1):
+            st = torch.randn(3, n, 6, generator=g)
+            nxt = torch.rand(3, 4, generator=g) * 1.8 - 0.9 if cont else torch.tensor([2, -1, 0])
+            lat = torch.nn.functional.normalize(torch.randn(3, 8, generator=g), dim=-1) if evo else None
+            with torch.no_grad():
+                raw, val, sp, dn, cache = wm(st, next_actions=nxt, latent_gene=lat)
+            p = f'{tag}.n{n}.'
+            out.update({p + 'state': st, p + 'next_actions': nxt, p + 'raw': raw, p + 'values': val,
+                        p + 'state_pred': sp, p + 'dones': dn, p + 'levels': torch.stack(cache['fractal_levels'])})
+            if evo:
+                out[p + 'latent'] = lat
+    save('fractal', **out)
+
+
 # --------------------------------------------------------------------------------------------
 # full Learner: the reference's own rollout + learn, with the shared-uniform protocol patched in
 # --------------------------------------------------------------------------------------------
@@ -339,6 +408,9 @@ def gen_learner(X, name, *, seed, S, A, T, depth, gates, evolutionary, episodes,
 def main():
     mods = load_reference()
     X, E = mods['x_transformers_rl'], mods['evolution']
+    gen_fractal(mods['fractal_rl'])
+    if sys.argv[1:] == ['fractal']:     # only the fractal fixtures
+        return
     gen_gae(X)
     gen_rsnorm(X)
     gen_normalize_and_dists(X)

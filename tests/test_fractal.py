@@ -3,9 +3,13 @@
 Pins: the parameter counts printed by the reference's comprehensive_demo.py (:338-357) for its three
 architectures, and the parameter names / shapes of the committed checkpoint
 fractal_experiments/frala_easy_final/final_fractal_agent.pt (tests/golden/fractal_easy_layout.json,
-made by tests/golden/make_fractal_layout.py).  Forward numerics of the x-transformers modules are
-"parity unpinned" (no reference output exists in the container): the GPU tests compare the HIP
-path with oracle/fractal_ref.py, an fp64 restatement, within 1e-4 of the output scale."""
+made by tests/golden/make_fractal_layout.py).  The forward numerics of the reference's own fractal
+arithmetic (level embedding, post-norm block order, global-state update, level projections, final
+aggregation, heads) are pinned by tests/test_fractal_golden.py: oracle/fractal_ref.py reproduces the
+reference's fractal_rl.py run in the build container (tests/golden/fractal.npz) to fp32 rounding.
+Only the x-transformers Attention / FeedForward internals inside those modules remain the
+restatement's (x-transformers is absent).  The GPU tests compare the HIP path with that oracle, in
+fp64, within 1e-4 of the output scale."""
 import json
 import math
 from pathlib import Path
