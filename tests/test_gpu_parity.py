@@ -341,7 +341,7 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
                  hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None,
-                 ff_mult=4):
+                 ff_mult=4, genes=3, shard_by_gene=False):
     """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides.
     ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult)."""
     from xtrl_amd import Learner, SynthVecSim
@@ -356,14 +356,14 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
         wm['ff_mult'] = ff_mult
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
-    gp = dict(dim=gene_dim, num_genes_per_island=3, num_selected=2, tournament_size=2)
+    gp = dict(dim=gene_dim, num_genes_per_island=genes, num_selected=2, tournament_size=2)
     learner = Learner(state_dim=S, num_actions=A, reward_range=(-2., 2.), world_model=wm, max_timesteps=T,
                       batch_size=batch, num_episodes_per_update=episodes, evolutionary=evo, evolve_every=1,
                       evolve_after_step=0, latent_gene_pool=gp, continuous_actions=cont,
                       continuous_actions_clamp=(-1., 1.) if cont else None,
                       agent_kwargs=dict(dropout=0., seed=seed, hidden_dim=dim, reward_dropout=reward_dropout,
                                         **(agent_extra or {})),
-                      use_graph=False)
+                      use_graph=False, shard_by_gene=shard_by_gene)
     with torch.no_grad():   # non-trivial gate / mix weights (their init is constant)
         g = torch.Generator().manual_seed(seed + 1)
         for name, p in learner.agent.model.named_parameters():
@@ -998,7 +998,52 @@ def _bench_learner(cfg):
     from bench import CONFIGS
     c = CONFIGS[cfg]
     return make_learner(depth=c['depth'], gates=c['gates'], evo=c['evo'], T=c['T'], episodes=c['episodes'],
-                        batch=c['batch'], seed=4, hazard=c['hazard_log2'], dim=c['dim'], gene_dim=32)
+                        batch=c['batch'], seed=4, hazard=c['hazard_log2'], dim=c['dim'], gene_dim=32,
+                        genes=c.get('genes', 3), fractal_levels=c.get('fractal'))
+
+
+def _full_width_rollout(cfg):
+    """The bench rollout of ``cfg`` at full width through the captured hipGraph vs the oracle's
+    batch-1 loop: every (episode, gene) pair's first 4 steps, and 16 whole episodes (the longest ones
+    and a spread of slots) over the full KV-cache length."""
+    learner, env, oracle = _bench_learner(cfg)
+    learner.use_graph = True
+    learner._engine = None
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 128)
+    torch.cuda.synchronize()
+    assert len(learner.episode_genes) == 1024
+    episodes, fitness = oracle.rollout(0, max_timesteps=4)
+    compare_rollout(traj, lens, episodes, prefix=4)
+    lens_c = lens.cpu()
+    longest = torch.argsort(lens_c, descending=True, stable=True)[:8].tolist()
+    spread = [int(x) for x in torch.linspace(5, 1019, 8).round().long().tolist()]
+    rows = sorted(set(longest + spread))
+    episodes, _ = oracle.rollout(0, slots=rows)
+    compare_rollout(traj, lens, episodes, rows=rows)
+    assert int(lens_c.max()) == 128 and int((lens_c == 128).sum()) > 50
+    return learner, traj, lens, genes, cum
+
+
+def test_c5_full_width_fractal_rollout_matches_oracle():
+    """The C5 bench rollout at full width: 1024 (episode, gene) pairs of EPO population 8, the
+    fractal policy body (4 levels, d 256) — 37 launches per step through the captured hipGraph,
+    k_mlp's fractal last arriver (LN3, running level means, next level input) and the split-output
+    global-state / level-projection GEMM at up to 1024 live rows — against the streaming oracle;
+    the per-gene fitness sums against the oracle's sequential ones."""
+    learner, traj, lens, genes, cum = _full_width_rollout('c5')
+    assert sorted(set(genes.cpu().tolist())) == list(range(8))
+
+
+def test_c5_bench_minibatch_learn_matches_oracle():
+    """The C5 learn step as the bench runs it — 1024 pairs, minibatches of 128 episodes x 128
+    steps, 4 fractal levels at d 256, 8 genes of 32 dims, the hand-scheduled fractal train step —
+    against the streaming fractal oracle on identical weights and minibatch (dropout 0: the fractal
+    oracle body is dropout-free): loss at 1e-4 relative and every gradient at 1e-4 of the gradient
+    scale, for two minibatches (the second after one optimiser step)."""
+    learner, env, oracle = _bench_learner('c5')
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 128)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2)
+    assert [s[0] for s in seen] == [128, 128] and all(s[3] == 128 for s in seen)
 
 
 def test_c3_full_width_rollout_matches_oracle():

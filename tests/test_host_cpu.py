@@ -194,6 +194,18 @@ def test_full_checkpoint_roundtrip(tmp_path):
                  (a.rs_mean, b.rs_mean), (a.rs_var, b.rs_var), (a.gene_pool.genes, b.gene_pool.genes)):
         assert torch.equal(x, y)
     assert (b.opt_first, b.ema_step, b.ema_initted, b.rs_step, b.step, b.gene_pool.step) == (False, 37, True, 9, 4, 2)
+    # the flat-layout buffers are stored per parameter name, so a build whose flat order differs
+    # restores every parameter's own moments / EMA weights
+    data = torch.load(str(tmp_path / 'ppo.pt'), weights_only=True)
+    assert data['format'] == 'xtrl_amd/2' and sorted(data['opt_m']) == sorted(a.flat.index)
+    name0 = a.flat.names[0]
+    lo, hi = a.flat.index[name0]
+    assert torch.equal(data['opt_m'][name0].reshape(-1), a.opt_m[lo:hi])
+    # a format-1 file (positional flat buffers, order unrecorded) is refused, not mis-paired
+    data.update(format='xtrl_amd/1', opt_m=a.opt_m.clone())
+    torch.save(data, str(tmp_path / 'v1.pt'))
+    with pytest.raises(ValueError, match='flat order'):
+        b.load_checkpoint(tmp_path / 'v1.pt')
     # reference format: weights only (xtrl.py:792-806)
     a.save()
     c = Learner(5, 2, (-1., 1.), **kw).agent

@@ -214,17 +214,31 @@ class Agent(nn.Module):
                 self.model.state_dict()[k].copy_(v)
 
     # ---- full training state (improves on the reference, which saves the model only) ----------------
+    FULL_FORMAT = 'xtrl_amd/2'
+
+    def _by_name(self, flat):
+        """A flat-layout buffer as {parameter name: its slice}: a checkpoint independent of the flat
+        order, which follows the backward's completion order and changes with the kernels."""
+        return {n: flat[a:b].detach().clone() for n, (a, b) in self.flat.index.items()}
+
+    def _from_name(self, flat, saved, what):
+        if sorted(saved) != sorted(self.flat.index):
+            raise ValueError(f'checkpoint {what}: parameter names differ from this model')
+        for n, (a, b) in self.flat.index.items():
+            flat[a:b].copy_(saved[n].reshape(-1).to(flat.device))
+
     def state_dict_full(self):
         """Everything needed to resume bit-for-bit: model (reference key names), the AdoptAtan2
         moments and regen anchor, the EMA weights and schedule, RSNorm statistics, the gene pool,
-        the update counter and seed."""
-        out = dict(model=self.model.state_dict(), format='xtrl_amd/1',
-                   opt_m=self.opt_m, opt_v=self.opt_v, opt_first=torch.tensor(int(self.opt_first)),
-                   ema_flat=self.ema_flat, ema_step=torch.tensor(self.ema_step),
+        the update counter and seed.  Flat-layout buffers are stored per parameter name."""
+        out = dict(model=self.model.state_dict(), format=self.FULL_FORMAT,
+                   opt_m=self._by_name(self.opt_m), opt_v=self._by_name(self.opt_v),
+                   opt_first=torch.tensor(int(self.opt_first)),
+                   ema_flat=self._by_name(self.ema_flat), ema_step=torch.tensor(self.ema_step),
                    ema_initted=torch.tensor(int(self.ema_initted)), rs_mean=self.rs_mean, rs_var=self.rs_var,
                    rs_step=torch.tensor(self.rs_step), step=torch.tensor(self.step), seed=torch.tensor(self.seed))
         if self.opt_p_init is not None:
-            out['opt_p_init'] = self.opt_p_init
+            out['opt_p_init'] = self._by_name(self.opt_p_init)
         if self.gene_pool is not None:
             out.update(genes=self.gene_pool.genes, gene_step=torch.tensor(self.gene_pool.step))
         return out
@@ -232,23 +246,29 @@ class Agent(nn.Module):
     def save_checkpoint(self, path=None):
         if not self.accelerator.is_main_process:
             return
-        torch.save({k: (v.detach().cpu() if isinstance(v, torch.Tensor) else v)
-                    for k, v in self.state_dict_full().items()}, str(path or self.save_path))
+        cpu = lambda v: {n: t.detach().cpu() for n, t in v.items()} if isinstance(v, dict) else (   # noqa: E731
+            v.detach().cpu() if isinstance(v, torch.Tensor) else v)
+        torch.save({k: cpu(v) for k, v in self.state_dict_full().items()}, str(path or self.save_path))
 
     def load_checkpoint(self, path=None):
         data = torch.load(str(path or self.save_path), weights_only=True, map_location='cpu')
         dev = self.device
+        if 'opt_m' in data and data.get('format') != self.FULL_FORMAT:
+            # format 1 stored the flat buffers positionally in a flat order that has since changed:
+            # pairing them by position would silently give parameters other parameters' moments
+            raise ValueError(f"full checkpoint format {data.get('format')!r} stores the optimiser / EMA buffers in "
+                             f"an unrecorded flat order; this build reads {self.FULL_FORMAT!r} (per-parameter names)")
         with torch.no_grad():
             for k, v in data['model'].items():
                 self.model.state_dict()[k].copy_(v)
             if 'opt_m' not in data:    # a reference-format checkpoint: weights only
                 return
-            self.opt_m.copy_(data['opt_m'])
-            self.opt_v.copy_(data['opt_v'])
+            self._from_name(self.opt_m, data['opt_m'], 'opt_m')
+            self._from_name(self.opt_v, data['opt_v'], 'opt_v')
             if self.opt_p_init is not None and 'opt_p_init' in data:
-                self.opt_p_init.copy_(data['opt_p_init'])
+                self._from_name(self.opt_p_init, data['opt_p_init'], 'opt_p_init')
             self.opt_first = bool(int(data['opt_first']))
-            self.ema_flat.copy_(data['ema_flat'].to(dev))
+            self._from_name(self.ema_flat, data['ema_flat'], 'ema_flat')
             self.ema_step, self.ema_initted = int(data['ema_step']), bool(int(data['ema_initted']))
             self.rs_mean = data['rs_mean'].to(dev).clone()
             self.rs_var = data['rs_var'].to(dev).clone()
@@ -647,13 +667,19 @@ class Learner(nn.Module):
         agent = self.agent
         if not agent.evolutionary:
             return None
-        # per-gene sums on the device (one small GEMV in a fixed order; fp64 episode returns), the
-        # rank sum (xtrl.py:1362) on the device too: one device->host copy per update, for evolve_
+        # the reference's order: per episode a double sum of its rewards (xtrl.py:1282, 1310), then
+        # fitnesses[gene] += that sum on an fp32 tensor, episode after episode (xtrl.py:1346) — an fp32
+        # add of the fp32-rounded return, sequential per gene in pair order (np.add.at is unbuffered
+        # and in index order).  One device->host copy of the episode returns per update; the rank sum
+        # (xtrl.py:1362) is the only collective.
         G = agent.gene_pool.num_genes
-        cum = cum_reward.to(self.device, torch.float64)
-        onehot = (genes.to(self.device)[None, :] == torch.arange(G, device=self.device)[:, None]).to(torch.float64)
-        fit = (onehot @ cum).to(torch.float32)
-        return dist_.sum_(fit).cpu()
+        cum = cum_reward.detach().to('cpu', torch.float64).numpy().astype(np.float32)
+        fit = np.zeros(G, dtype=np.float32)
+        np.add.at(fit, genes.detach().cpu().numpy(), cum)
+        fit = torch.from_numpy(fit)
+        if dist_.is_distributed():
+            fit = dist_.sum_(fit.to(self.device)).cpu()
+        return fit
 
     def forward(self, env, num_learning_updates: int, seed=None, max_timesteps=None):
         T = max_timesteps or self.max_timesteps
