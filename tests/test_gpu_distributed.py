@@ -35,7 +35,7 @@ def _free_port():
     return port
 
 
-def _make(world, shard_by_gene=False, genes=3, episodes=4, fractal=None):
+def _make(world, shard_by_gene=False, genes=3, episodes=4, fractal=None, evo=True):
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(3)
     wm = dict(attn_dim_head=16, heads=4, depth=2)
@@ -45,7 +45,7 @@ def _make(world, shard_by_gene=False, genes=3, episodes=4, fractal=None):
     else:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     learner = Learner(8, 4, (-2., 2.), world_model=wm, max_timesteps=20, batch_size=2,
-                      num_episodes_per_update=episodes, evolutionary=True, evolve_every=1, evolve_after_step=0,
+                      num_episodes_per_update=episodes, evolutionary=evo, evolve_every=1, evolve_after_step=0,
                       latent_gene_pool=dict(dim=8, num_genes_per_island=genes, num_selected=2, tournament_size=2),
                       agent_kwargs=dict(dropout=0.1, seed=7, hidden_dim=48, save_path='/tmp/xtrl_dp_test.pt', **extra),
                       use_graph=False, shard_by_gene=shard_by_gene)
@@ -69,19 +69,25 @@ def _worker(rank, world, port, out_dir, mode):
         gene_mode = mode in ('genes', 'c5')
         if mode == 'c5':     # population 8 over 4 ranks (2 genes each), fractal body
             learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
+        elif mode == 'c4':   # the C4 partition: one policy, the episodes split 8 ways (torch.chunk)
+            learner, env = _make(world, episodes=16, evo=False)
         else:
             learner, env = _make(world, shard_by_gene=gene_mode, genes=4 if gene_mode else 3)
         a = learner.agent
         traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
         first = dict(actions=traj['actions'].cpu().clone(), lens=lens.cpu().clone(), fit=learner.fitness(cum, genes))
         grads = []
-        if mode == 'grad':
+        if mode in ('grad', 'c4'):
+            lr = a.opt_cfg['lr']
             a.opt_cfg['lr'] = 0.     # weights fixed: every minibatch gradient at the same point
             a.learn(traj, lens, genes, first['fit'], update=0, probe=_grad_probe(a, grads))
+            if mode == 'c4':         # then one full learning update: the ranks must stay in lockstep
+                a.opt_cfg['lr'] = lr
+                learner(env, 1)
         else:
             learner(env, 2)
         torch.save(dict(flat=a.flat.flat.cpu(), ema=a.ema_flat.cpu(), rs_mean=a.rs_mean.cpu(), rs_var=a.rs_var.cpu(),
-                        genes=a.gene_pool.genes.clone(), first=first, pairs=learner.episode_genes_for_process,
+                        genes=a.gene_pool.genes.clone() if a.gene_pool is not None else torch.zeros(1), first=first, pairs=learner.episode_genes_for_process,
                         slots=learner.pair_slots, grads=grads),
                    os.path.join(out_dir, f'rank{rank}.pt'))
     finally:
@@ -187,3 +193,51 @@ def test_c5_gene_sharded_population8_four_ranks(tmp_path):
         assert torch.equal(r[rank]['first']['lens'], lens.cpu()[slots])
         assert torch.equal(r[rank]['first']['actions'], traj['actions'].cpu()[slots])
         torch.testing.assert_close(r[rank]['first']['fit'], fit, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_c4_eight_ranks_dp_partition(tmp_path):
+    """The C4 partition (BASELINE configs[3]: one policy, the episodes sharded 8-way, a gradient
+    all-reduce per optimiser step) with 8 ranks on one GPU over gloo, at reduced size (16 episodes,
+    2 per rank).  The concatenated rank rollouts equal the single-process rollout; every rank holds
+    the same all-reduced gradient at every optimiser step, equal to the mean of the 8 per-rank
+    minibatch gradients a single process computes; after a full learning update the 8 ranks'
+    weights, EMA and RSNorm statistics are bitwise identical."""
+    world = 8
+    r = _run(tmp_path, 'c4', world=world)
+    learner, env = _make(1, episodes=16, evo=False)
+    a = learner.agent
+    a.opt_cfg['lr'] = 0.
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    assert torch.equal(torch.cat([r[i]['first']['lens'] for i in range(world)]), lens.cpu())
+    assert torch.equal(torch.cat([r[i]['first']['actions'] for i in range(world)]), traj['actions'].cpu())
+    n0 = len(r[0]['pairs'])
+    assert n0 * world == lens.numel() == 16
+    steps = len(r[0]['grads'])
+    assert steps > 0
+    for i in range(1, world):
+        assert len(r[i]['grads']) == steps
+        for g0, gi in zip(r[0]['grads'], r[i]['grads']):
+            assert torch.equal(g0, gi)
+    flat0 = a.flat.flat.clone()
+    rs0 = (a.rs_mean.clone(), a.rs_var.clone(), a.rs_step)
+    per_rank = []
+    for rank in range(world):
+        a.rs_mean, a.rs_var, a.rs_step = rs0[0].clone(), rs0[1].clone(), rs0[2]
+        a.step = 0
+        rows = slice(rank * n0, (rank + 1) * n0)
+        sub = {k: (v[rows].contiguous() if v is not None else None) for k, v in traj.items()}
+        grads = []
+        a.learn(sub, lens[rows].contiguous(), genes[rows].contiguous(), None, update=0, probe=_grad_probe(a, grads))
+        assert torch.equal(a.flat.flat, flat0)
+        assert len(grads) == steps
+        per_rank.append(grads)
+    for i in range(steps):
+        want = sum(per_rank[k][i] for k in range(world)) / world
+        got = r[0]['grads'][i]
+        scale = float(want.abs().max())
+        assert float((got - want).abs().max()) <= 1e-6 * scale + 1e-9, i
+    for k in ('flat', 'ema', 'rs_mean', 'rs_var'):
+        for rank in range(1, world):
+            assert torch.equal(r[0][k], r[rank][k]), (k, rank)
+    assert torch.isfinite(r[0]['flat']).all() and not torch.equal(r[0]['flat'], flat0.cpu())
