@@ -57,11 +57,40 @@ CONFIGS = {
                         'heads, causal per timestep), batch 128 episodes, 4 epochs, dropout 0.25',
                S=8, A=4, episodes=128, genes=8, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=False, evo=True,
                fractal=4, batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
+    # the literal drop-in path (train_lander.py:22-70): a scalar host env stepped one action at a time
+    # through Learner.rollout_host (the reference's env contract), at train_lander's model shape
+    'lander_host': dict(workload='drop-in: train_lander.py shape (EPO 3 genes x 64 episodes, depth 4, d 48, 4x16 heads, '
+                                 'batch 8, actor_loss_weight 0.5, frac head gradient 0.1) on a scalar host env '
+                                 '(numpy LunarLander-shaped Sim, S=8, A=4, hazard 1/64) through Learner.rollout_host, '
+                                 'one env.step per action as the reference loop (xtrl.py:1220-1341)',
+                        S=8, A=4, episodes=64, T=500, depth=4, dim=48, heads=4, dim_head=16, gates=True, evo=True,
+                        batch=8, hazard_log2=6, dropout=0.25, mode='lander', host=True),
     # configs[0] — README Sim plumbing case
     'c1': dict(workload='C1: README Sim (S=5, A=2, T=10), depth 1, d=48, 64 episodes, batch 8',
                S=5, A=2, episodes=64, T=10, depth=1, dim=48, heads=4, dim_head=16, gates=False, evo=False,
                batch=8, hazard_log2=0, dropout=0.25, mode='readme'),
 }
+
+
+class HostLanderSim:
+    """A scalar host env with the reference's contract (reset(seed=?) -> (state, info); step(action) ->
+    (state, reward, terminated, truncated, info), train_lander.py's gym interface): LunarLander-shaped
+    (S = 8 N(0, 1) states, A = 4 actions, action-dependent N(0, 1) rewards, termination hazard
+    2^-hazard_log2), numpy on the host — one Python call per env step, as gym's LunarLander."""
+
+    def __init__(self, S, A, hazard_log2, seed=0):
+        self.S, self.A, self.p = S, A, 2.0 ** -hazard_log2
+        self.rng = np.random.default_rng(seed)
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(int(seed))
+        return self.rng.standard_normal(self.S).astype(np.float32), {}
+
+    def step(self, action):
+        state = self.rng.standard_normal(self.S).astype(np.float32)
+        reward = float(self.rng.standard_normal() + 0.1 * (int(action) - self.A / 2))
+        return state, reward, bool(self.rng.random() < self.p), False, {}
 
 
 def build_learner(cfg, seed, use_graph=True, world=1):
@@ -70,6 +99,8 @@ def build_learner(cfg, seed, use_graph=True, world=1):
     if cfg['gates']:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     extra = dict(policy_body='fractal', fractal_levels=cfg['fractal']) if cfg.get('fractal') else {}
+    if cfg.get('host'):   # train_lander.py:42-49
+        extra.update(actor_loss_weight=0.5)
     learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
                       max_timesteps=cfg['T'], batch_size=cfg['batch'],
                       num_episodes_per_update=cfg['episodes'] * world,   # weak scaling: episodes per GPU fixed
@@ -78,8 +109,11 @@ def build_learner(cfg, seed, use_graph=True, world=1):
                                             tournament_size=2),
                       agent_kwargs=dict(hidden_dim=cfg['dim'], dropout=cfg['dropout'], seed=seed,
                                         save_path='/tmp/xtrl_bench_ppo.pt', **extra),
-                      use_graph=use_graph, shard_by_gene=bool(cfg.get('fractal')))
+                      use_graph=use_graph, shard_by_gene=bool(cfg.get('fractal')),
+                      **(dict(frac_actor_critic_head_gradient=0.1) if cfg.get('host') else {}))
     # (C5: episodes per update = 128 x world over 8 genes, gene-sharded: 1024 pairs per GPU at any N)
+    if cfg.get('host'):
+        return learner, HostLanderSim(cfg['S'], cfg['A'], cfg['hazard_log2'], seed)
     env = SynthVecSim(cfg['S'], cfg['A'], cfg['mode'], cfg['hazard_log2'])
     return learner, env
 
@@ -93,7 +127,12 @@ def one_update(learner, env, T, probe=None, phases=False):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if phases else None
     if ev:
         ev[0].record()
-    traj, lens, genes, cum = learner.rollout_device(env, u, T)
+    if isinstance(env, HostLanderSim):   # the reference's scalar env contract (Learner.forward's host branch)
+        g = torch.Generator().manual_seed(agent.seed * 31 + u)
+        seeds = torch.randint(0, int(1e7), (learner.num_episodes_per_update,), generator=g) if agent.evolutionary else None
+        traj, lens, genes, cum = learner.rollout_host(env, u, T, seeds)
+    else:
+        traj, lens, genes, cum = learner.rollout_device(env, u, T)
     if ev:
         ev[1].record()
     fit = learner.fitness(cum, genes)
@@ -430,21 +469,39 @@ def main():
 
     for _ in range(args.warmup):
         one_update(learner, env, T)
-    # roofline timers: HIP events around the decode attention launches and the learn step's
-    # weight-gradient GEMM launches (both policy bodies)
-    timer = None if args.no_roofline else DecodeAttnTimer(learner, env, T)
-    gtimer = None
-    if timer is not None:
-        # untimed: capture the rollout graph with the event records inside, and count the
-        # weight-gradient launches of one update to size the timed region's event pool exactly
+    host = bool(cfg.get('host'))
+    # Roofline timers — HIP events around every decode-attention launch (inside the captured rollout
+    # graph) and every weight-gradient GEMM launch of the learn step — run in a PROBED pass of
+    # untimed updates before the headline region (value_probed: its rate), then come out again; the
+    # headline region below carries no probe events.
+    timer = gtimer = None
+    value_probed = None
+    if not args.no_roofline and not host:
+        timer = DecodeAttnTimer(learner, env, T)
+        # capture the rollout graph with the event records inside, and count the weight-gradient
+        # launches of one update to size the probed pass's event pool exactly
         probe_timer = WgradGemmTimer(learner.agent, T, cap=1 << 14)
         probe_timer.attach()
         one_update(learner, env, T)
         per_update = probe_timer.n.value
         probe_timer.detach()
         timer.ms, timer.launches, timer.bytes = 0.0, 0, 0.0
-        gtimer = WgradGemmTimer(learner.agent, T, cap=per_update * args.steps + 64)
+        n_probed = max(1, min(args.steps, 3))
+        gtimer = WgradGemmTimer(learner.agent, T, cap=per_update * n_probed + 64)
         gtimer.attach()
+        torch.cuda.synchronize()
+        tp0 = time.perf_counter()
+        probed_steps = torch.zeros((), device='cuda', dtype=torch.int64)
+        for _ in range(n_probed):
+            steps, lens_p = one_update(learner, env, T)
+            probed_steps += steps
+        torch.cuda.synchronize()
+        value_probed = float(probed_steps) / (time.perf_counter() - tp0)
+        timer.collect(lens_p)          # the event pairs hold the last probed update's T*L launches
+        gtimer.collect()
+        gtimer.detach()
+        timer.detach()
+        one_update(learner, env, T)    # re-capture the rollout graph without the event records
     if world > 1:
         dist.barrier()
     from xtrl_amd import distributed as dist_
@@ -452,19 +509,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     total = torch.zeros((), device='cuda', dtype=torch.int64)
-    lens_log = []
+    lens_last = None
     for _ in range(args.steps):
         steps, lens = one_update(learner, env, T, phases=True)
         total += steps
-        if timer is not None:
-            lens_log.append(lens.clone())
+        lens_last = lens
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if timer is not None and lens_log:
-        timer.collect(lens_log[-1])   # the event pairs hold the last update's T*L launches
-    lens_last = lens_log[-1].cpu().numpy() if lens_log else None
+    lens_last = lens_last.cpu().numpy() if lens_last is not None else None
     el = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -482,25 +536,23 @@ def main():
     phase_ms = dict(rollout=round(sum(e[0].elapsed_time(e[1]) for e in PHASES) / len(PHASES), 2),
                     learn=round(sum(e[1].elapsed_time(e[2]) for e in PHASES) / len(PHASES), 2))
     roofline = attn_roofline = None
-    if gtimer is not None:
-        gtimer.collect()
-        gtimer.detach()
-        if gtimer.launches:
-            avg_s = gtimer.ms / gtimer.launches / 1e3
-            flops = gtimer.total_flops / gtimer.launches
-            achieved = flops / avg_s / 1e12
-            x6 = os.environ.get('XTRL_GEMM_F32', '0') in ('', '0')
-            peak = X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
-            roofline = dict(kernel='k_gemm_ws<T,T> / k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, '
-                                   '128x128 tiles, split-K over 192 workgroups, on the backward side stream beside '
-                                   'the input-gradient chain; the largest kernel of the update; fp32 products as ' +
-                                   ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
-                                    'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
-                            peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
-                            traffic=prof(pmc_traffic, *WgradGemmTimer.KERNELS),
-                            mfma_busy=prof(pmc_mfma_busy, *WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
-                            avg_launch_us_rocprof=prof(rocprof_avg_us, *WgradGemmTimer.KERNELS),
-                            flops_per_launch=round(flops), launches=gtimer.launches)
+    if gtimer is not None and gtimer.launches:
+        avg_s = gtimer.ms / gtimer.launches / 1e3
+        flops = gtimer.total_flops / gtimer.launches
+        achieved = flops / avg_s / 1e12
+        x6 = os.environ.get('XTRL_GEMM_F32', '0') in ('', '0')
+        peak = X6_PEAK_TFLOPS if x6 else MFMA_F32_PEAK_TFLOPS
+        roofline = dict(kernel='k_gemm_ws<T,T> / k_gemm<2,2,1,2,2,T,T> (learn-step weight-gradient GEMM, '
+                               '128x128 tiles, split-K over 192 workgroups, on the backward side stream beside '
+                               'the input-gradient chain; the largest kernel of the update; fp32 products as ' +
+                               ('six bf16 piece products, peak = bf16 dense peak / 6)' if x6 else
+                                'native f32 MFMA)'), bound='mfma', achieved=round(achieved, 2),
+                        peak=round(peak, 1), unit='TFLOP/s', frac=round(achieved / peak, 4),
+                        traffic=prof(pmc_traffic, *WgradGemmTimer.KERNELS),
+                        mfma_busy=prof(pmc_mfma_busy, *WgradGemmTimer.KERNELS), avg_launch_us=round(avg_s * 1e6, 2),
+                        avg_launch_us_rocprof=prof(rocprof_avg_us, *WgradGemmTimer.KERNELS),
+                        flops_per_launch=round(flops), launches=gtimer.launches,
+                        timed_in='probed pass (events around each launch), not the headline region')
     if timer is not None and timer.launches:
         avg_s = timer.ms / timer.launches / 1e3
         achieved = timer.bytes / timer.launches / avg_s / 1e9
@@ -515,7 +567,6 @@ def main():
         if us:
             attn_roofline.update(avg_launch_us_rocprof=us, frac_rocprof=round(
                 timer.bytes / timer.launches / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4))
-        timer.detach()
 
     total_roof = None
     if lens_last is not None:
@@ -529,7 +580,7 @@ def main():
     # collective the others never enter
     if world == 1:
         try:
-            loss_delta = None if args.no_loss_delta else ppo_loss_delta(learner, env, cfg)
+            loss_delta = None if (args.no_loss_delta or host) else ppo_loss_delta(learner, env, cfg)
         except Exception as e:   # reported, never hidden
             loss_delta = dict(error=repr(e))
         if not args.no_cpu_baseline:
@@ -541,9 +592,11 @@ def main():
                        single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
         line = dict(metric='env-steps/s (rollout+update)', value=round(value, 1), unit='env-steps/s', n_gpus=world,
+                    value_probed=None if value_probed is None else round(value_probed, 1),
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
                     higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
-                    data='synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)',
+                    data=('synthetic (numpy LunarLander-shaped scalar host env, random-init weights)' if host else
+                          'synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)'),
                     config=dict(workload=cfg['workload'],
                                 global_batch=cfg['episodes'] * (cfg.get('genes', 3) if cfg['evo'] else 1) * world,
                                 seq_len=T, parallelism=f'dp{world}', env_steps=env_steps),

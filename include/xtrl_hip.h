@@ -413,7 +413,10 @@ typedef struct XtrlTrainDesc {
    * embeddings / everything), grad_events[2i] on the caller's stream and grad_events[2i + 1] on the
    * weight-gradient stream once every gradient of the bucket is final, so the caller can all-reduce
    * bucket i (a contiguous range of the flat gradient, xtrl_amd.model flat_order) while the backward
-   * continues (DDP's bucketed all-reduce, xtrl.py:885/981) */
+   * continues (DDP's bucketed all-reduce, xtrl.py:885/981).  xtrl_fractal_train_backward: buckets
+   * 0 .. levels + 1 (0: heads + action embedding + final aggregation, 1 + j: level levels - 1 - j,
+   * levels + 1: input embedding / global state / level embeddings / everything else;
+   * xtrl_amd.fractal flat_buckets_names) */
   void** grad_events;
   /* row stride (floats) of the [T][ff] feed-forward buffers hd, u, dff (the fractal body's h, u, dz):
    * >= ff, a multiple of 4; 0 = ff.  A stride off the 4 KiB power of two (e.g. ff + 16) spreads the

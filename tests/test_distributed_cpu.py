@@ -94,3 +94,36 @@ def test_gradient_buckets_cover_the_flat_buffer_in_completion_order():
     g = BucketAllReduce.coalesce(r, 1 << 20)
     assert [x[0] for x in g][0] == 0 and g[-1][1] == r[-1][1] and len(g) == 3
     assert all(a[1] == b[0] for a, b in zip(g, g[1:]))
+
+
+def test_fractal_gradient_buckets_follow_the_fractal_backward():
+    """The fractal body's buckets (FractalPolicyActorCritic.flat_bucket_ranges): contiguous, covering
+    the extended gradient buffer once; heads + final aggregation first, then level L-1 .. 0 (each its
+    block and level projection), then the parameters every level accumulates into (global-state
+    update, level embeddings, a shared block) with the input embedding; GEMM weights 16-byte aligned,
+    each block's q | k | v adjacent.  (The Learner's body has a block per level.)"""
+    from xtrl_amd.fractal import FractalPolicyActorCritic
+    from xtrl_amd.model import ModelConfig
+    from xtrl_amd.params import FlatParams
+    c = ModelConfig(state_dim=8, num_actions=4, dim=64, depth=3, heads=4, dim_head=16, evolutionary=True, dim_gene=8,
+                    reward_range=(-2., 2.))
+    m = FractalPolicyActorCritic(c, 3)
+    flat = FlatParams(m, 'cpu', order=m.flat_order(), extra=9)
+    r = m.flat_bucket_ranges(flat)
+    assert len(r) == 3 + 2 and r[0][0] == 0 and r[-1][1] == flat.grad_ext.numel()
+    assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+    at = lambda n: flat.index[n][0]   # noqa: E731
+    assert r[0][0] <= at('fractal_encoder.final_aggregation.0.weight') < r[0][1]
+    assert r[0][0] <= at('action_head.0.weight') < r[0][1]
+    assert r[1][0] <= at('fractal_encoder.level_projections.2.weight') < r[1][1]
+    assert r[3][0] <= at('fractal_encoder.level_projections.0.weight') < r[3][1]
+    for n in ('fractal_encoder.global_state_update.weight', 'fractal_encoder.level_embedding.level_embeds',
+              'fractal_encoder.input_embed.weight', 'fractal_encoder.global_state_init'):
+        assert r[-1][0] <= at(n) < r[-1][1], n
+    pre = m.block_prefix(1)
+    assert r[2][0] <= at(pre + 'ff.ff.0.0.weight') < r[2][1]
+    flat.span([pre + 'self_attn.to_q.weight', pre + 'self_attn.to_k.weight', pre + 'self_attn.to_v.weight'])
+    for name, (a, b) in flat.index.items():
+        p = dict(m.named_parameters())[name]
+        if p.dim() == 2 and p.shape[1] % 4 == 0:
+            assert a % 4 == 0, name

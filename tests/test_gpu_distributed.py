@@ -62,12 +62,16 @@ def _worker(rank, world, port, out_dir, mode):
     sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
+    if mode == 'c5grad':   # one collective per backward bucket (no coalescing of the small test buckets)
+        os.environ['XTRL_DP_BUCKET_FLOATS'] = '1'
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         gene_mode = mode in ('genes', 'c5')
         if mode == 'c5':     # population 8 over 4 ranks (2 genes each), fractal body
+            learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
+        elif mode == 'c5grad':
             learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
         elif mode == 'c4':   # the C4 partition: one policy, the episodes split 8 ways (torch.chunk)
             learner, env = _make(world, episodes=16, evo=False)
@@ -77,10 +81,13 @@ def _worker(rank, world, port, out_dir, mode):
         traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
         first = dict(actions=traj['actions'].cpu().clone(), lens=lens.cpu().clone(), fit=learner.fitness(cum, genes))
         grads = []
-        if mode in ('grad', 'c4'):
+        from xtrl_amd import distributed as dist_
+        coll0 = dist_.COUNTS['all_reduce']
+        if mode in ('grad', 'c4', 'c5grad'):
             lr = a.opt_cfg['lr']
             a.opt_cfg['lr'] = 0.     # weights fixed: every minibatch gradient at the same point
             a.learn(traj, lens, genes, first['fit'], update=0, probe=_grad_probe(a, grads))
+            first['allreduces'] = dist_.COUNTS['all_reduce'] - coll0
             if mode == 'c4':         # then one full learning update: the ranks must stay in lockstep
                 a.opt_cfg['lr'] = lr
                 learner(env, 1)
@@ -241,3 +248,44 @@ def test_c4_eight_ranks_dp_partition(tmp_path):
         for rank in range(1, world):
             assert torch.equal(r[0][k], r[rank][k]), (k, rank)
     assert torch.isfinite(r[0]['flat']).all() and not torch.equal(r[0]['flat'], flat0.cpu())
+
+
+@pytest.mark.gpu
+def test_c5_fractal_bucketed_allreduce_gradient(tmp_path):
+    """The fractal learn step's data-parallel gradient at world 4 (C5 partition: population 8, two
+    genes per rank): the backward records an event pair per gradient bucket (heads + aggregation, one
+    per level, the rest) and the bucket all-reduces overlap it — one collective per bucket per
+    optimiser step with coalescing off; every rank holds the same gradient, equal to the mean of the
+    four per-rank minibatch gradients a single process computes."""
+    world = 4
+    r = _run(tmp_path, 'c5grad', world=world)
+    steps = len(r[0]['grads'])
+    assert steps > 0
+    levels = 2
+    # per optimiser step: levels + 2 bucket all-reduces (the RSNorm mean rides in the last one)
+    assert r[0]['first']['allreduces'] == steps * (levels + 2), (r[0]['first']['allreduces'], steps)
+    for i in range(1, world):
+        for g0, gi in zip(r[0]['grads'], r[i]['grads']):
+            assert torch.equal(g0, gi)
+    learner, env = _make(1, genes=8, episodes=2, fractal=2)
+    a = learner.agent
+    a.opt_cfg['lr'] = 0.
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    fit = learner.fitness(cum, genes)
+    flat0 = a.flat.flat.clone()
+    rs0 = (a.rs_mean.clone(), a.rs_var.clone(), a.rs_step)
+    per_rank = []
+    for rank in range(world):
+        a.rs_mean, a.rs_var, a.rs_step = rs0[0].clone(), rs0[1].clone(), rs0[2]
+        a.step = 0
+        rows = torch.tensor(r[rank]['slots'], device=lens.device)
+        sub = {k: (v[rows].contiguous() if v is not None else None) for k, v in traj.items()}
+        grads = []
+        a.learn(sub, lens[rows].contiguous(), genes[rows].contiguous(), fit, update=0, probe=_grad_probe(a, grads))
+        assert torch.equal(a.flat.flat, flat0) and len(grads) == steps
+        per_rank.append(grads)
+    for i in range(steps):
+        want = sum(per_rank[k][i] for k in range(world)) / world
+        got = r[0]['grads'][i]
+        scale = float(want.abs().max())
+        assert float((got - want).abs().max()) <= 1e-6 * scale + 1e-9, i

@@ -245,6 +245,55 @@ def test_attention_fwd_bwd(b, H, n, dh):
     tol(vf.grad, vd.grad, 1e-4, 1e-5)
 
 
+def _attn_bwd_lib(q, k, v, lens, do, scale, p, fused, seed=3, offset=1, sub=0):
+    """xtrl_attn_fwd + xtrl_attn_bwd through the C ABI, the backward as the fused one-launch kernel
+    (XTRL_ATTN_FUSED_BWD=1, read per launch) or the dK/dV + dQ kernel pair."""
+    import os
+    from xtrl_amd import _lib as L
+    lib = L.lib()
+    b, H, n, dh = q.shape
+    o, dq, dk, dv = (torch.empty_like(q) for _ in range(4))
+    lse, delta = (torch.empty(b, H, n, device=DEV) for _ in range(2))
+    L.check(lib.xtrl_attn_fwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), b, H, n, dh, scale, p,
+                              seed, offset, sub, L.stream()), 'attn_fwd')
+    old = os.environ.get('XTRL_ATTN_FUSED_BWD')
+    os.environ['XTRL_ATTN_FUSED_BWD'] = '1' if fused else '0'
+    try:
+        L.check(lib.xtrl_attn_bwd(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(o), L.ptr(lse), L.ptr(do), L.ptr(dq),
+                                  L.ptr(dk), L.ptr(dv), L.ptr(delta), b, H, n, dh, scale, p, seed, offset, sub,
+                                  L.stream()), 'attn_bwd')
+    finally:
+        if old is None:
+            del os.environ['XTRL_ATTN_FUSED_BWD']
+        else:
+            os.environ['XTRL_ATTN_FUSED_BWD'] = old
+    torch.cuda.synchronize()
+    return dict(o=o, lse=lse, delta=delta, dq=dq, dk=dk, dv=dv)
+
+
+@pytest.mark.parametrize('b,H,n,p', [(3, 4, 37, 0.), (4, 4, 128, 0.), (4, 4, 128, 0.25), (2, 2, 10, 0.25),
+                                     (3, 2, 100, 0.1), (5, 4, 65, 0.25)])
+def test_attention_fused_backward_matches_two_kernel(b, H, n, p):
+    """The fused short-episode backward (k_attn_bwd_fused: one workgroup per (episode, head), P and dS
+    formed once per (key tile, query tile) pair) against the dK/dV + dQ kernel pair on the same
+    inputs: byte-mode (p = 0.25) and word-mode (p = 0.1) dropout, n not a multiple of 64, ragged
+    lens < n.  dV, dK, dQ and D bit-identical."""
+    g = torch.Generator().manual_seed(n + int(100 * p))
+    q, k, v, do = (torch.randn(b, H, n, 16, generator=g).to(DEV) for _ in range(4))
+    lens = torch.randint(1, n + 1, (b,), generator=g).to(torch.int32)
+    lens[0] = n
+    lens = lens.to(DEV)
+    two = _attn_bwd_lib(q, k, v, lens, do, 0.25, p, False)
+    fus = _attn_bwd_lib(q, k, v, lens, do, 0.25, p, True)
+    report = {}
+    for name in ('o', 'lse', 'delta', 'dv', 'dk', 'dq'):
+        d = (two[name] - fus[name]).abs()
+        report[name] = (float(d.max()), int((d > 0).sum()))
+    print('fused vs two-kernel (max |diff|, #differing):', report)
+    for name in ('o', 'lse', 'delta', 'dv', 'dk', 'dq'):
+        assert torch.equal(two[name], fus[name]), (name, report)
+
+
 def test_attention_dropout_consistent():
     """Same seed -> same mask; the backward differentiates exactly the forward's dropped product."""
     from xtrl_amd import ops

@@ -472,6 +472,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
 #pragma unroll
           for (int c = 0; c < DH; ++c) dsum += dOs[tid][c] * orow[c];
           Dls[tid] = dsum;
+          const int ii = qt * TQ + tid;
+          if (kt == 0 && ii < n) a.Dout[(int64_t)bh * n + ii] = dsum;   // as k_attn_bwd_dkdv's key tile 0
         }
         __syncthreads();
         float dsr[4][4];
@@ -563,12 +565,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
     }
 }
 
-bool attn_fused_bwd_on() {   // XTRL_ATTN_FUSED_BWD=1: the fused backward (opt-in)
-  static const bool on = [] {
-    const char* e = getenv("XTRL_ATTN_FUSED_BWD");
-    return e && atoi(e) == 1;
-  }();
-  return on;
+bool attn_fused_bwd_on() {   // XTRL_ATTN_FUSED_BWD=0: the kernel pair (read per launch: tests flip it)
+  const char* e = getenv("XTRL_ATTN_FUSED_BWD");
+  return !(e && atoi(e) == 0);
 }
 
 int fill_args(AttnArgs& a, const AttnProblem& p) {

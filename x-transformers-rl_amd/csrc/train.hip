@@ -1622,6 +1622,21 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
   }();
   SplitKQueue skq;
   const Ctx cw{D, two ? side.s : s, T, defer ? &skq : nullptr};
+  // data-parallel gradient buckets (FractalPolicyActorCritic.flat_buckets_names): [heads, action
+  // embedding, final aggregation], one per level (last to first), [the rest]; each flushes its
+  // deferred split-K reductions and records an event on both streams once its gradients are final
+  int bucket = 0;
+  auto bucket_done = [&]() -> int {
+    if (!D->grad_events) return XTRL_OK;
+    if (int rc = splitk_flush(skq, cw.s)) return rc;
+    if (hipEventRecord((hipEvent_t)D->grad_events[2 * bucket], s) != hipSuccess ||
+        hipEventRecord((hipEvent_t)D->grad_events[2 * bucket + 1], cw.s) != hipSuccess) {
+      set_error("fractal train: gradient bucket event record failed");
+      return XTRL_E_HIP;
+    }
+    ++bucket;
+    return XTRL_OK;
+  };
   if ((rc = heads_backward(c, cw, Fk))) return rc;
   // d features = frac * dac[:, :d] + dewa[:, :d]  (frac_gradient: the actor / critic share scaled)
   // every backward scratch plane a side-stream weight gradient reads is written once per backward
@@ -1660,6 +1675,7 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
   if ((rc = Fk.fork())) return rc;
   if ((rc = wgrad(cw, F->dhfa, 2 * d, F->cat, ldcat, c.G(F->w_fa0), T, 2 * d, ldcat, c.G(F->b_fa0)))) return rc;
   if ((rc = linear_dgrad(c, F->dhfa, 2 * d, c.P(F->w_fa0), F->dcat, ldcat, T, 2 * d, ldcat, EPI_NONE))) return rc;
+  if ((rc = bucket_done())) return rc;   // bucket 0: heads, action embedding, final aggregation
   // levels, last to first.  dgn: gradient of g_{l+1} (the final g: cat's last d columns); dxn:
   // gradient of x3_l from level l + 1's input (none for the last level).
   // the chained post-norm LayerNorm backward epilogue (XTRL_FUSED_LN=0: separate launches)
@@ -1731,12 +1747,14 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
     dxn = F->dxa;
     dgn = dgc;
     lddgn = d;
+    if ((rc = bucket_done())) return rc;   // bucket Lv - l: level l's block and projection
   }
   // input embedding (x_in,0 = state W_in^T + b_in + le[0]) and global_state_init (g_0 on every row)
   if ((rc = Fk.fork())) return rc;
   if ((rc = wgrad(cw, F->dxa, d, D->swr, S + 1, c.G(D->w_pin), T, d, S, c.G(F->b_in)))) return rc;
   if ((rc = colsum(c, dgn, lddgn, T, d, c.G(F->g_init)))) return rc;
   if ((rc = splitk_flush(skq, cw.s))) return rc;
+  if ((rc = bucket_done())) return rc;   // bucket Lv + 1: embeddings, global state, level embeddings
   if ((rc = Fk.wait(Fk.mark()))) return rc;
   XTRL_REQUIRE(!Fk.failed, "fractal train: side-stream event record failed");
   XTRL_REQUIRE(!Fk.on() || (size_t)Fk.next == fractal_events_needed(Lv), "fractal train: side events %d != %d", Fk.next,

@@ -334,32 +334,63 @@ class FractalPolicyActorCritic(FractalWorldModelActorCritic):
             return 'fractal_encoder.base_block.'
         return f'fractal_encoder.fractal_blocks.{li}.'
 
-    def flat_order(self):
-        """Every parameter once.  Weights used as one GEMM operand by the fused learn step
-        (train.FractalTrainStep) are adjacent: each block's to_q | to_k | to_v, the actor | critic first
-        layers, to_pred.0 | to_pred_done.0 (weights and biases); groups whose size is not a multiple
-        of 4 floats go last, so every GEMM weight starts 16-byte aligned."""
+    def flat_buckets_names(self):
+        """Parameter groups of the flat buffer, bucketed in the order the fused fractal backward
+        completes them (csrc/train.hip fractal_train_backward records an event pair per bucket for the
+        overlapped data-parallel all-reduce): [heads, action embedding, final aggregation], [level L-1's
+        block + level projection], ..., [level 0's], [input embedding, global-state init / update,
+        level embeddings (accumulated over every level) and the parameters no forward reads].  A shared
+        (share_weights / hypernetwork) block accumulates over the levels, so it goes to the last bucket.
+        Weights used as one GEMM operand are adjacent groups: each block's to_q | to_k | to_v, the
+        actor | critic first layers, to_pred.0 | to_pred_done.0 (weights and biases); groups whose size
+        is not a multiple of 4 floats move to the last bucket, so every GEMM weight starts 16-byte
+        aligned.  -> list of buckets, each a list of groups."""
         params = dict(self.named_parameters())
-        taken, groups = set(), []
+        taken = set()
 
         def grp(names):
             taken.update(names)
-            groups.append(list(names))
+            return list(names)
 
-        grp(['action_head.0.weight', 'critic_head.0.weight'])
-        grp(['action_head.0.bias', 'critic_head.0.bias'])
-        grp(['to_pred.0.weight', 'to_pred_done.0.weight'])
-        grp(['to_pred.0.bias', 'to_pred_done.0.bias'])
-        for li in range(self.levels):
-            pre = self.block_prefix(li) + 'self_attn.'
-            if pre + 'to_q.weight' not in taken:
-                grp([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight'])
-        for n in params:
-            if n not in taken:
-                grp([n])
+        def under(*prefixes):
+            return [grp([n]) for n in params if n not in taken and n.startswith(prefixes)]
+
+        enc = self.fractal_encoder
+        heads = [grp(['action_head.0.weight', 'critic_head.0.weight']), grp(['action_head.0.bias', 'critic_head.0.bias']),
+                 grp(['to_pred.0.weight', 'to_pred_done.0.weight']), grp(['to_pred.0.bias', 'to_pred_done.0.bias'])]
+        heads += under('action_head.', 'critic_head.', 'to_pred.', 'to_pred_done.', 'to_state_embed.',
+                       'latent_to_embed.', 'action_embeds.', 'fractal_encoder.final_aggregation.')
+        per_level = not (enc.share_weights or enc.use_hypernetwork)
+        levels = []
+        for li in reversed(range(self.levels)):
+            g = []
+            if per_level:
+                pre = self.block_prefix(li)
+                g.append(grp([pre + 'self_attn.to_q.weight', pre + 'self_attn.to_k.weight', pre + 'self_attn.to_v.weight']))
+                g += under(pre + 'norm3.', pre + 'ff.', pre + 'norm2.', pre + 'norm1.', pre + 'global_attn.to_out.',
+                           pre + 'global_attn.to_v.', pre + 'self_attn.to_out.')
+            g += under(f'fractal_encoder.level_projections.{li}.')
+            levels.append(g)
+        if not per_level:
+            pre = self.block_prefix(0) + 'self_attn.'
+            tail0 = [grp([pre + 'to_q.weight', pre + 'to_k.weight', pre + 'to_v.weight'])]
+        else:
+            tail0 = []
+        tail = tail0 + [grp([n]) for n in params if n not in taken]
+        buckets = [heads] + levels + [tail]
         size = lambda g: sum(params[n].numel() for n in g)
-        groups = [g for g in groups if size(g) % 4 == 0] + [g for g in groups if size(g) % 4]
-        return [n for g in groups for n in g]
+        odd = [g for b in buckets for g in b if size(g) % 4]
+        buckets = [[g for g in b if size(g) % 4 == 0] for b in buckets]
+        buckets[-1] += odd
+        return buckets
+
+    def flat_order(self):
+        """Every parameter once, in bucket order (flat_buckets_names)."""
+        return [n for b in self.flat_buckets_names() for g in b for n in g]
+
+    def flat_bucket_ranges(self, flat):
+        from .model import bucket_ranges
+        return bucket_ranges(self.flat_buckets_names(), flat)
 
     def bind_flat(self, flat, ws):
         self._flat, self._ws = flat, ws

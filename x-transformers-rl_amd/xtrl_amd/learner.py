@@ -284,8 +284,8 @@ class Agent(nn.Module):
         return F.normalize(self.genes_device()[gene_ids], dim=-1)
 
     def genes_device(self):
-        if self._genes_dev is None:
-            self._genes_dev = self.gene_pool.genes.to(self.device)
+        if self._genes_dev is None:   # (after an evolve_: an async copy, no mid-learn host wait)
+            self._genes_dev = _to_device_async(self.gene_pool.genes.detach(), self.device)
         return self._genes_dev
 
     # ---- EMA (ema-pytorch update(), restated) ---------------------------------------------------------
@@ -348,8 +348,10 @@ class Agent(nn.Module):
         gene_ids = gene_ids.to(dev)
         rs_mean, rs_var, rs_step = self.rs_mean.clone(), self.rs_var.clone(), self.rs_step
         model.train()
-        perms = [epoch_permutation(self.seed, update, e, N) for e in range(self.epochs)]
-        perms = torch.stack(perms).to(dev)
+        # the epochs' minibatch orders (host generator: bit parity with torch.randperm), uploaded from
+        # pinned memory without a host wait — the learn's only host round trip is the length max above
+        perms = torch.stack([epoch_permutation(self.seed, update, e, N) for e in range(self.epochs)])
+        perms = _to_device_async(perms, dev)
         sd = self.rs_var.sqrt().clamp(min=1e-5)
         lo, hi = c.reward_range
         fused = self.fused_learn
@@ -514,6 +516,15 @@ class Agent(nn.Module):
         raw = eng.logits[0].clone()
         new_h = dict(t=t + 1, cache=[x.clone() for x in eng.cache_tensors()])
         return raw, new_h
+
+
+def _to_device_async(t, dev):
+    """Host tensor -> device without blocking the host: a pinned staging copy and a non-blocking
+    upload (the caching host allocator keeps the pinned block alive until the copy has run)."""
+    dev = torch.device(dev)
+    if dev.type != 'cuda':
+        return t.to(dev)
+    return t.contiguous().pin_memory().to(dev, non_blocking=True)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -130,6 +130,22 @@ def _rotate_half(x):
     return torch.stack((-x2, x1), dim=-1).reshape(*x.shape[:-2], -1)
 
 
+def bucket_ranges(buckets, flat):
+    """[(start, end)] of each bucket (a list of name groups, in flat order) in ``flat.grad_ext``; the
+    last one runs to its end: the RSNorm-mean tail rides with it."""
+    out = []
+    for b in buckets:
+        names = [n for g in b for n in g]
+        out.append([flat.index[names[0]][0], flat.index[names[-1]][1]] if names else None)
+    for i in range(len(out)):
+        if out[i] is None:
+            out[i] = [out[i - 1][1], out[i - 1][1]] if i else [0, 0]
+    for a, b in zip(out, out[1:]):
+        assert a[1] == b[0], 'flat buckets are not contiguous'
+    out[-1][1] = flat.grad_ext.numel()
+    return [tuple(r) for r in out]
+
+
 class WorldModelActorCritic(nn.Module):
     def __init__(self, c: ModelConfig):
         super().__init__()
@@ -228,19 +244,7 @@ class WorldModelActorCritic(nn.Module):
         return [n for b in self.flat_buckets_names() for g in b for n in g]
 
     def flat_bucket_ranges(self, flat):
-        """[(start, end)] of each bucket in ``flat.grad_ext`` (the last one runs to its end: the
-        RSNorm-mean tail rides with it)."""
-        out = []
-        for b in self.flat_buckets_names():
-            names = [n for g in b for n in g]
-            out.append([flat.index[names[0]][0], flat.index[names[-1]][1]] if names else None)
-        for i in range(len(out)):
-            if out[i] is None:
-                out[i] = [out[i - 1][1], out[i - 1][1]] if i else [0, 0]
-        for a, b in zip(out, out[1:]):
-            assert a[1] == b[0], 'flat buckets are not contiguous'
-        out[-1][1] = flat.grad_ext.numel()
-        return [tuple(r) for r in out]
+        return bucket_ranges(self.flat_buckets_names(), flat)
 
     def bind_flat(self, flat, ws):
         """Record the concatenated weight / gradient views used by forward_train."""

@@ -328,8 +328,9 @@ class FractalTrainStep(FusedTrainStep):
         return self._outputs()
 
     def backward(self, grad_events=None):
-        """(no per-bucket events: the caller all-reduces the whole gradient after the backward)"""
-        assert grad_events is None, 'the fractal learn step has no gradient buckets'
+        """``grad_events``: ctypes array of 2 (levels + 2) HIP event handles recorded per gradient
+        bucket (FractalPolicyActorCritic.flat_buckets_names), or None."""
+        self.D.grad_events = C.cast(grad_events, C.POINTER(C.c_void_p)) if grad_events is not None else None
         L.check(L.lib().xtrl_fractal_train_backward(C.byref(self.D), C.byref(self.Fd), L.stream()),
                 'fractal_train_backward')
 
