@@ -219,6 +219,7 @@ class ModelConfig:
     value_residual: bool = False
     learned_mix: bool = False
     ff_mult: int = 4          # x-transformers FeedForward mult, reached through world_model['ff_mult']
+    ff_no_bias: bool = False  # world_model['ff_no_bias'] (x-transformers FeedForward no_bias)
 
 
 class OracleWMAC(nn.Module):
@@ -234,7 +235,8 @@ class OracleWMAC(nn.Module):
                                    rotary_pos_emb=True, attn_dropout=cfg.dropout, ff_dropout=cfg.dropout,
                                    verbose=False, attn_gate_values=cfg.gate_values,
                                    add_value_residual=cfg.value_residual,
-                                   learned_value_residual_mix=cfg.learned_mix, ff_mult=cfg.ff_mult))
+                                   learned_value_residual_mix=cfg.learned_mix, ff_mult=cfg.ff_mult,
+                                   ff_no_bias=cfg.ff_no_bias))
         self.reward_embed = nn.Parameter(torch.ones(d) * 1e-2)
         if cfg.continuous:
             self.action_embeds = nn.Linear(cfg.num_actions, d)
@@ -494,6 +496,7 @@ class LearnerConfig:
     value_residual: bool = False
     learned_mix: bool = False
     ff_mult: int = 4
+    ff_no_bias: bool = False
     continuous: bool = False
     squash: bool = True
     clamp: tuple | None = None
@@ -547,7 +550,7 @@ class OracleLearner:
                          c.reward_range, 100, c.continuous, c.squash, c.evolutionary,
                          self.gp['dim'] if c.evolutionary else 0, c.frac_head_grad, c.beta_s, c.eps_clip,
                          c.value_clip, c.dropout, c.reward_dropout, True, c.gate_values, c.value_residual,
-                         c.learned_mix, c.ff_mult)
+                         c.learned_mix, c.ff_mult, c.ff_no_bias)
         self.model = model_factory(mc) if model_factory is not None else OracleWMAC(mc)
         if init_state_dict is not None:
             self.model.load_state_dict(init_state_dict)

@@ -259,11 +259,13 @@ class Attention(nn.Module):
 
 
 class FeedForward(nn.Module):
-    def __init__(self, dim, mult=4, dropout=0.):
+    """x-transformers FeedForward (GELU, no GLU); ``no_bias``: both Linears without bias (ff_no_bias)."""
+
+    def __init__(self, dim, mult=4, dropout=0., no_bias=False):
         super().__init__()
         inner = dim * mult
-        self.ff = nn.Sequential(nn.Sequential(nn.Linear(dim, inner), nn.GELU()), nn.Dropout(dropout),
-                                nn.Linear(inner, dim))
+        self.ff = nn.Sequential(nn.Sequential(nn.Linear(dim, inner, bias=not no_bias), nn.GELU()), nn.Dropout(dropout),
+                                nn.Linear(inner, dim, bias=not no_bias))
 
     def forward(self, x):
         return self.ff(x)
@@ -325,7 +327,7 @@ class LayerIntermediates:
 class Decoder(nn.Module):
     def __init__(self, dim, depth, heads=8, attn_dim_head=64, rotary_pos_emb=False, attn_dropout=0.,
                  ff_dropout=0., verbose=True, attn_gate_values=False, add_value_residual=False,
-                 learned_value_residual_mix=False, ff_mult=4, **unsupported):
+                 learned_value_residual_mix=False, ff_mult=4, ff_no_bias=False, **unsupported):
         super().__init__()
         if unsupported:
             raise NotImplementedError(f'restated Decoder does not model {sorted(unsupported)}')
@@ -337,7 +339,7 @@ class Decoder(nn.Module):
                              learned_value_residual_mix=learned_value_residual_mix and add_value_residual and ind > 0)
             self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]), attn, _Residual()]))
             self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]),
-                                              FeedForward(dim, ff_mult, ff_dropout), _Residual()]))
+                                              FeedForward(dim, ff_mult, ff_dropout, ff_no_bias), _Residual()]))
         self.rotary_pos_emb = RotaryEmbedding(attn_dim_head // 2) if rotary_pos_emb else None
         self.final_norm = LayerNorm(dim)
 

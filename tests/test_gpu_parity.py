@@ -390,7 +390,7 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
                  hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None,
-                 ff_mult=4, genes=3, shard_by_gene=False):
+                 ff_mult=4, genes=3, shard_by_gene=False, ff_no_bias=False):
     """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides.
     ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult)."""
     from xtrl_amd import Learner, SynthVecSim
@@ -403,6 +403,8 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
     wm = dict(attn_dim_head=16, heads=4, depth=depth)
     if ff_mult != 4:
         wm['ff_mult'] = ff_mult
+    if ff_no_bias:
+        wm['ff_no_bias'] = True
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     gp = dict(dim=gene_dim, num_genes_per_island=genes, num_selected=2, tournament_size=2)
@@ -424,7 +426,7 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
                         learned_mix=gates, continuous=cont, clamp=(-1., 1.) if cont else None, evolutionary=evo,
                         evolve_every=1, evolve_after_step=0, gene_pool=gp, max_timesteps=T, batch_size=batch,
                         num_episodes_per_update=episodes, sim_mode=mode, hazard_log2=hazard, seed=seed,
-                        reward_dropout=reward_dropout, ff_mult=ff_mult)
+                        reward_dropout=reward_dropout, ff_mult=ff_mult, ff_no_bias=ff_no_bias)
     sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
     genes = learner.agent.gene_pool.genes.clone() if evo else None
     oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes, model_factory=factory)
@@ -1030,6 +1032,23 @@ def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, drop
         agent.learn(traj, lens, genes, fit, update=0, probe=probe)
     print('minibatches (n, loss, worst grad err / scale, episodes):', seen)
     return seen
+
+
+@pytest.mark.parametrize('dim,gates', [(48, True), (256, False)])
+def test_ff_no_bias_rollout_and_learn_match_oracle(dim, gates):
+    """world_model['ff_no_bias'] (x-transformers FeedForward without biases): the rollout (the decode
+    feed-forward kernel on zero packed biases) and the fused learn step (bias pointers absent: no bias
+    epilogue, no bias gradient) against the oracle's bias-free FeedForward."""
+    learner, env, oracle = make_learner(depth=2, gates=gates, T=24, episodes=6, batch=3, seed=6, hazard=3, dim=dim,
+                                        ff_no_bias=True)
+    names = [n for n, _ in learner.agent.model.named_parameters()]
+    assert not any(n.endswith(('ff.0.0.bias', 'ff.2.bias')) for n in names)
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 24)
+    torch.cuda.synchronize()
+    episodes_o, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2)
+    assert len(seen) == 2
 
 
 def test_c3_shape_rollout_and_learn_match_oracle():

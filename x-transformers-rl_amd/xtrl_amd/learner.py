@@ -49,6 +49,21 @@ EMA_DEFAULTS = dict(update_after_step=100, update_every=10, inv_gamma=1., power=
                     update_model_with_ema_every=None, update_model_with_ema_beta=0.)
 
 
+# x-transformers Decoder / Attention / FeedForward options (>= 2.3, the reference's pin, pyproject.toml:35)
+# at their default values: passing one of them explicitly builds the network the MI355X decoder runs
+XT_DEFAULTS = dict(
+    causal=True, cross_attend=False, only_cross=False, use_scalenorm=False, use_rmsnorm=False, use_simple_rmsnorm=False,
+    alibi_pos_bias=False, rel_pos_bias=False, dynamic_pos_bias=False, rotary_xpos=False, residual_attn=False,
+    cross_residual_attn=False, macaron=False, pre_norm=True, gate_residual=False, scale_residual=False,
+    shift_tokens=0, sandwich_norm=False, resi_dual=False, zero_init_branch_output=False, layer_dropout=0.,
+    use_layerscale=False, unet_skips=False, reinject_input=False, weight_tie_layers=False,
+    ff_glu=False, ff_swish=False, ff_relu_squared=False, ff_post_act_ln=False, ff_no_bias=False,
+    attn_talking_heads=False, attn_head_scale=False, attn_sparse_topk=None, attn_num_mem_kv=0, attn_on_attn=False,
+    attn_gate_value_heads=False, attn_swiglu_values=False, attn_qk_norm=False, attn_one_kv_head=False,
+    attn_kv_heads=None, attn_shared_kv=False, attn_value_dim_head=None, attn_add_zero_kv=False,
+    attn_rotary_embed_values=False, attn_max_attend_past=None)
+
+
 def epoch_permutation(seed, update, epoch, n):
     g = torch.Generator().manual_seed((int(seed) * 1000003 + int(update)) * 1000003 + int(epoch) & (2 ** 62 - 1))
     return torch.randperm(n, generator=g)
@@ -98,14 +113,21 @@ class Agent(nn.Module):
         wm = dict(world_model)
         # x-transformers switches that select an implementation, not the math: accepted and ignored
         # (attn_flash: fused scaled-dot-product attention instead of the explicit softmax — the same
-        # function; the learn step's attention here is always the fused HIP kernel)
-        for k in ('attn_flash',):
+        # function; attn_onnxable: an export-friendly softmax; the learn step's attention here is always
+        # the fused HIP kernel).  Options given at their x-transformers default build the same network:
+        # accepted too.
+        for k in ('attn_flash', 'attn_onnxable'):
             wm.pop(k, None)
+        for k, default in XT_DEFAULTS.items():
+            if k in wm and wm[k] == default:
+                wm.pop(k)
         known = {'attn_dim_head', 'heads', 'depth', 'attn_gate_values', 'add_value_residual',
-                 'learned_value_residual_mix', 'ff_mult'}
+                 'learned_value_residual_mix', 'ff_mult', 'ff_no_bias'}
         unknown = set(wm) - known
         if unknown:
-            raise NotImplementedError(f'world_model options {sorted(unknown)} are not supported by the MI355X decoder')
+            raise NotImplementedError(f'world_model options {sorted(unknown)} are not supported by the MI355X decoder '
+                                      f'(supported: {sorted(known)}, implementation switches attn_flash / '
+                                      f'attn_onnxable, and any option at its x-transformers default)')
         self.seed = int(seed)
         self.evolutionary = evolutionary
         self.evolve_every, self.evolve_after_step = evolve_every, evolve_after_step
@@ -118,15 +140,16 @@ class Agent(nn.Module):
                         value_clip=value_clip, dropout=dropout, reward_dropout=reward_dropout,
                         gate_values=wm.get('attn_gate_values', False), value_residual=wm.get('add_value_residual', False),
                         learned_mix=wm.get('learned_value_residual_mix', False), ff_mult=int(wm.get('ff_mult', 4)),
+                        ff_no_bias=bool(wm.get('ff_no_bias', False)),
                         rotary_abs_rollout=rotary_abs_rollout,
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
         # policy body: the x-transformers Decoder (x_transformers_rl.py) or the per-timestep causal
         # fractal encoder (fractal_rl.py:349-619 made causal, fractal.FractalPolicyActorCritic)
         if policy_body == 'fractal':
-            if c.gate_values or c.value_residual:
-                raise NotImplementedError('the fractal policy body has no gated values / value residual: '
-                                          'set attn_gate_values / add_value_residual to False')
+            if c.gate_values or c.value_residual or c.ff_no_bias:
+                raise NotImplementedError('the fractal policy body has no gated values / value residual / bias-free '
+                                          'feed-forward: set attn_gate_values / add_value_residual / ff_no_bias to False')
             levels = int(fractal_levels or c.depth)
             self.model = FractalPolicyActorCritic(c, levels).to(dev)
         elif policy_body == 'decoder':

@@ -45,6 +45,7 @@ class ModelConfig:
     value_residual: bool = False
     learned_mix: bool = False
     ff_mult: int = 4
+    ff_no_bias: bool = False             # x-transformers FeedForward no_bias (world_model['ff_no_bias'])
     rotary_abs_rollout: bool = False     # decision log: reference semantics = rotary position 0 in rollout
     hl_reduction_mean: bool = True       # decision log: hl-gauss-pytorch default reduction
     hl_sigma_ratio: float = 2.0
@@ -91,9 +92,9 @@ class XAttention(nn.Module):
 class XFeedForward(nn.Module):
     def __init__(self, c: ModelConfig):
         super().__init__()
-        inner = c.dim * c.ff_mult
-        self.ff = nn.Sequential(nn.Sequential(nn.Linear(c.dim, inner), nn.GELU()), nn.Dropout(c.dropout),
-                                nn.Linear(inner, c.dim))
+        inner, bias = c.dim * c.ff_mult, not c.ff_no_bias
+        self.ff = nn.Sequential(nn.Sequential(nn.Linear(c.dim, inner, bias=bias), nn.GELU()), nn.Dropout(c.dropout),
+                                nn.Linear(inner, c.dim, bias=bias))
 
 
 class _Residual(nn.Module):
@@ -318,7 +319,8 @@ class WorldModelActorCritic(nn.Module):
             x = self._lin(o, blk.to_out) + x
             (ln_f, _, _), ffb, _ = ff_l
             f0 = ffb.ff[0][0]   # Linear + GELU + Dropout in one GEMM epilogue (the fused step's mask stream)
-            h = ops.linear_gelu_drop(ln_f(x), f0.weight, f0.bias, f0.weight.grad, f0.bias.grad, self._ws, p_drop,
+            h = ops.linear_gelu_drop(ln_f(x), f0.weight, f0.bias, f0.weight.grad,
+                                     f0.bias.grad if f0.bias is not None else None, self._ws, p_drop,
                                      attn_seed, ff_offset, li)
             x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)

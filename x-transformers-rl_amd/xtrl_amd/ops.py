@@ -122,7 +122,7 @@ class LinearGeluDropFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         M = x2.shape[0]
-        assert w.is_contiguous() and b.is_contiguous()
+        assert w.is_contiguous() and (b is None or b.is_contiguous())
         y = torch.empty(M, N, device=x.device, dtype=torch.float32)
         deriv = torch.empty(M, N, device=x.device, dtype=torch.float32)
         L.check(L.lib().xtrl_linear_gelu_drop(L.ptr(x2), K, L.ptr(w), L.ptr(b), L.ptr(y), N, L.ptr(deriv), N, M, N, K,

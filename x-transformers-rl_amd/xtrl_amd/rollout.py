@@ -173,9 +173,10 @@ class RolloutEngine:
             wl['w_out_t'].copy_(blk.to_out.weight.t())
             wl['ln_ff'].copy_(ln_f.gamma)
             wl['w_ff1'].copy_(ffb.ff[0][0].weight)
-            wl['b_ff1'].copy_(ffb.ff[0][0].bias)
             wl['w_ff2'].copy_(ffb.ff[2].weight)
-            wl['b_ff2'].copy_(ffb.ff[2].bias)
+            if ffb.ff[0][0].bias is not None:   # (ff_no_bias: the packed biases stay zero)
+                wl['b_ff1'].copy_(ffb.ff[0][0].bias)
+                wl['b_ff2'].copy_(ffb.ff[2].bias)
         self._pack_gemm_weights()
 
     def _pack_common(self, model, rs_mean, rs_var):
