@@ -166,13 +166,16 @@ class DecodeAttnTimer:
         torch.cuda.synchronize()
         lens = lens.cpu().numpy()
         # the steps with a live episode (the rollout stops launching sub-graphs once none is live,
-        # so the event pairs of later steps may not belong to this update)
-        T_eff = int(lens.max())
+        # so the event pairs of later steps may not belong to this update), and decoded by the
+        # multi-kernel step (the row-resident step of a long tail has no separate attention launch)
+        T_eff = min(int(lens.max()), getattr(self.eng, 'rows_from_step', self.T))
         for i in range(T_eff * self.L):
             self.ms += self.events[2 * i].elapsed_time(self.events[2 * i + 1])
         self.launches += T_eff * self.L
         c = self.eng.c
         H, dh = c.heads, c.dim_head
+        if T_eff == 0:
+            return
         t = np.arange(T_eff)
         alive = (lens[None, :] > t[:, None]).sum(1)                  # live episodes at step t
         # per live (env, head): read K,V rows 0..t-1 (2 t dh f32) + its q|k|v(|gate|mix) row

@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 13
+#define XTRL_ABI_VERSION 14
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -101,6 +101,11 @@ typedef struct XtrlDecodeLayer {
   const uint16_t* w_ff2x; /* [d][ff] FF2 weights, or NULL: when both are set (with xn, mlp_part and
                              mlp_cnt) FF1 + GELU + FF2 + residual + the next pre-norm run as one launch
                              on the bf16 matrix cores (fp32 products as six piece products) */
+  /* k-major (transposed, plain fp32) copies for the row-resident step (xtrl_decode_step_rows), or NULL:
+   * w_qkv_t [d][round4(n_qkv)] (padding columns zero), w_ff1_t [d][ff], w_ff2_t [ff][d] */
+  const float* w_qkv_t;
+  const float* w_ff1_t;
+  const float* w_ff2_t;
 } XtrlDecodeLayer;
 
 typedef struct XtrlRngState {   /* device memory; read by the sampling / sim kernels */
@@ -181,6 +186,10 @@ typedef struct XtrlDecodeDesc {
   /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
    * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
   void** prof_events;
+  /* k-major heads for the row-resident step, or NULL: w_h1_t [in_dim][4d] (w_h1 transposed),
+   * w_h2_t [4d][round4(n_act + B)] (the block-diagonal w_h2 transposed, padding columns zero) */
+  const float* w_h1_t;
+  const float* w_h2_t;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
@@ -189,6 +198,13 @@ int xtrl_rollout_begin(const XtrlDecodeDesc* desc, void* stream);
 /* one timestep t for all E episodes; with sim_mode == -1 the env step happens on the host and
  * xtrl_rollout_env_feedback() writes its results back. */
 int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream);
+/* The same step, row-resident (replaces xtrl_decode_step for few live rows / small models; same
+ * outputs to fp32 rounding): one workgroup carries a live row through compaction, embeddings, every
+ * layer, the heads and the sampling + Sim step in ONE launch, min(max_rows, E) workgroups taking
+ * live rows b, b + grid, ...  Needs the k-major weights (w_qkv_t / w_ff1_t / w_ff2_t, w_out_t,
+ * w_h1_t / w_h2_t), d <= 256, E <= 8192, L <= 8, n_act <= 64 (the reference loop it replaces:
+ * x_transformers_rl.py:1250-1341). */
+int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void* stream);
 /* Host env results of step t (xtrl.py:1297-1336) for the live rows: next_state [E][S], reward [E],
  * terminated [E] (stored as is_boundary), truncated [E] or NULL.  An episode ends when terminated,
  * truncated or t + 1 == t_limit (max_timesteps); with `bootstrap` a truncated, not terminated

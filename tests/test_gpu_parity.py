@@ -467,9 +467,18 @@ def compare_rollout(traj, lens, episodes, cont=False, rows=None, prefix=None):
         assert float(traj['values'][i, n:].abs().sum()) == 0.
 
 
+@pytest.fixture(params=['rows', 'multi'])
+def decode_path(request, monkeypatch):
+    """The decode step the rollout takes at these sizes (d <= 128, few rows): the row-resident step
+    (xtrl_decode_step_rows, one workgroup per live row) or the multi-kernel step (XTRL_DECODE_ROWS=0)."""
+    monkeypatch.setenv('XTRL_DECODE_ROWS', '1' if request.param == 'rows' else '0')
+    return request.param
+
+
 @pytest.mark.parametrize('depth,gates,evo', [(1, False, False), (2, True, False), (2, True, True), (3, True, True)])
-def test_rollout_matches_oracle(depth, gates, evo):
+def test_rollout_matches_oracle(depth, gates, evo, decode_path):
     learner, env, oracle = make_learner(depth=depth, gates=gates, evo=evo)
+    assert (learner._engine_for(env, 12).rows_max > 0) == (decode_path == 'rows')
     traj, lens, _, cum = learner.rollout_device(env, 0, 12)
     torch.cuda.synchronize()
     episodes, fitness = oracle.rollout(0)
@@ -490,7 +499,7 @@ def test_rollout_d256_matches_oracle(ff):
     compare_rollout(traj, lens, episodes)
 
 
-def test_rollout_continuous_matches_oracle():
+def test_rollout_continuous_matches_oracle(decode_path):
     learner, env, oracle = make_learner(cont=True, gates=True)
     traj, lens, _, _ = learner.rollout_device(env, 0, 12)
     torch.cuda.synchronize()
@@ -499,8 +508,9 @@ def test_rollout_continuous_matches_oracle():
 
 
 @pytest.mark.parametrize('dim', [48, 256])
-def test_rollout_graph_replay_equals_eager(dim):
-    """dim 256: the one-launch feed-forward kernel (its per-panel arrival counters reset in-graph)."""
+def test_rollout_graph_replay_equals_eager(dim, decode_path):
+    """dim 256: the one-launch feed-forward kernel (its per-panel arrival counters reset in-graph).
+    dim 48 (rows): the row-resident step's graphs."""
     learner, env, _ = make_learner(depth=2, T=16, episodes=40, dim=dim)
     traj, lens, _, _ = learner.rollout_device(env, 0, 16)
     eager = {k: v.clone() for k, v in traj.items() if v is not None}
@@ -1092,6 +1102,30 @@ def _full_width_rollout(cfg):
     return learner, traj, lens, genes, cum
 
 
+def test_c2_full_width_rollout_matches_oracle():
+    """The C2 bench rollout at full width: 768 (episode, gene) pairs (256 episodes x 3 genes, 32-dim
+    genes), T = 500, depth 2, d 128, through the captured graphs — the multi-kernel step while more
+    than rows_max rows are live, then the row-resident step for the long tail (chunks after the live
+    count fell to rows_max) — against the oracle's batch-1 loop: every pair's first 4 steps, and 16
+    whole episodes (the longest ones, which run deep into the row-resident tail, and a spread)."""
+    learner, env, oracle = _bench_learner('c2')
+    learner.use_graph = True
+    learner._engine = None
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 500)
+    torch.cuda.synchronize()
+    eng = learner._engine[1]
+    assert len(learner.episode_genes) == 768 and eng.rows_max > 0 and eng.chunks_rows > 2
+    episodes, fitness = oracle.rollout(0, max_timesteps=4)
+    compare_rollout(traj, lens, episodes, prefix=4)
+    lens_c = lens.cpu()
+    longest = torch.argsort(lens_c, descending=True, stable=True)[:8].tolist()
+    spread = [int(x) for x in torch.linspace(3, 764, 8).round().long().tolist()]
+    rows = sorted(set(longest + spread))
+    episodes, _ = oracle.rollout(0, slots=rows)
+    compare_rollout(traj, lens, episodes, rows=rows)
+    assert int(lens_c.max()) > 300
+
+
 def test_c5_full_width_fractal_rollout_matches_oracle():
     """The C5 bench rollout at full width: 1024 (episode, gene) pairs of EPO population 8, the
     fractal policy body (4 levels, d 256) — 37 launches per step through the captured hipGraph,
@@ -1309,7 +1343,7 @@ def _compare_host(learner, oracle, env_gpu, env_cpu, T, seeds=None):
 
 
 @pytest.mark.parametrize('ret,limit', [(3, None), (4, 5), (5, 5), (5, None), (5, 9), (4, 9)])
-def test_host_env_scalar_contract_matches_oracle(ret, limit):
+def test_host_env_scalar_contract_matches_oracle(ret, limit, decode_path):
     """The reference's scalar env (batch 1, pairs one by one) through the device decode: states,
     actions, log-probs, rewards, is_boundary = terminated, critic logits and lengths as the
     oracle's reference loop; truncated episodes carry the next state's value (bootstrap) — limit 9 =
@@ -1322,7 +1356,7 @@ def test_host_env_scalar_contract_matches_oracle(ret, limit):
 
 
 @pytest.mark.parametrize('frac,dim', [(None, 48), (2, 48), (None, 256)])
-def test_host_env_vectorised_waves_match_oracle(frac, dim):
+def test_host_env_vectorised_waves_match_oracle(frac, dim, decode_path):
     """A vectorised env of 4 sub-envs over 2 genes x 5 episodes (10 pairs: waves of 4, 4, 2 — the
     last one partial), evolutionary with per-episode reset seeds, truncation at 6 steps (the
     truncation bootstrap step included); decoder and fractal policy bodies (dim 256: the decoder's

@@ -1319,6 +1319,296 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
   return XTRL_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-resident decode step (few live rows, small models): ONE workgroup carries a live row through
+// the whole step — compaction, RSNorm + embeddings, every layer (LayerNorm, q|k|v|gate|mix, value
+// residual, rotary, KV append, attention over 0..t, gate, out-projection + residual, LayerNorm,
+// FF1 + GELU, FF2 + residual), the final norm, the heads and the sampling + Sim step — with the
+// activations in LDS.  Same semantics as the multi-launch step (k_embed / dgemm / k_attn_decode /
+// k_mlp / k_heads_sample); the products are plain fp32 FMAs (different summation order, fp32
+// rounding level).  The multi-launch step pays ~15 dependent launches whatever the live count
+// (C2's long tail: one or two live episodes for hundreds of steps; a scalar host env: one row per
+// step); here a step is one launch whose time is the row's weight stream (k-major copies, float4
+// per lane, L2-resident for d <= 128) plus its dependent latency chain.
+// 256 threads = 4 waves; workgroup b takes live rows b, b + gridDim.x, ...
+// ---------------------------------------------------------------------------------------------
+constexpr int ROW_T = 256;
+
+// out[n] = act(sum_k x[k] WT[k ldw + n] + bias[n]) (+ res[n]) for n < N (N % 4 == 0, k-major WT, 16-byte
+// aligned rows): wave w sums k in its quarter of [0, K) sequentially, lanes take float4 column
+// groups; the four quarter sums meet in LDS (fixed order).  ACT: 0 none, 1 GELU, 2 SiLU.
+template <int ACT>
+__device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT, int ldw, const float* bias, int N,
+                                         float* out, float* part, const float* res = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int Kq = (K + 3) >> 2, k0 = w * Kq, k1 = min(K, k0 + Kq);
+  for (int n4 = 4 * lane; n4 < N; n4 += 256) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* wp = WT + n4;
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) {
+      const float xv = x[k];
+      const float4 wv = *reinterpret_cast<const float4*>(wp + (int64_t)k * ldw);
+      acc.x = fmaf(xv, wv.x, acc.x);
+      acc.y = fmaf(xv, wv.y, acc.y);
+      acc.z = fmaf(xv, wv.z, acc.z);
+      acc.w = fmaf(xv, wv.w, acc.w);
+    }
+    *reinterpret_cast<float4*>(part + w * N + n4) = acc;
+  }
+  __syncthreads();
+  for (int n = tid; n < N; n += ROW_T) {
+    float v = ((part[n] + part[N + n]) + (part[2 * N + n] + part[3 * N + n])) + (bias ? bias[n] : 0.f);
+    if constexpr (ACT == 1) v = geluf_(v);
+    if constexpr (ACT == 2) v = siluf_(v);
+    if (res) v += res[n];
+    out[n] = v;
+  }
+  __syncthreads();
+}
+
+// out[c] = LayerNorm(x)[c] * g[c] (x-transformers: no affine, eps 1e-5, two-pass) by wave 0; d <= 256
+__device__ __forceinline__ void row_layernorm(const float* x, const float* g, int d, float* out) {
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    float v[4], sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = tid + 64 * k;
+      v[k] = c < d ? x[c] : 0.f;
+      sm += v[k];
+    }
+    const float mean = wave_sum_dpp(sm) / (float)d;
+    float qq = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float dl = v[k] - mean;
+      qq += tid + 64 * k < d ? dl * dl : 0.f;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = tid + 64 * k;
+      if (c < d) out[c] = ((v[k] - mean) * rstd) * g[c];
+    }
+  }
+  __syncthreads();
+}
+
+struct RowLds {   // floats, carved from the dynamic LDS
+  int x, xn, qkv, att, v1, h, ac, part, sc, lg, tot;
+};
+__host__ __device__ inline int round4i(int x) { return (x + 3) & ~3; }
+__host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
+  RowLds o;
+  const int I = D.H * D.dh, nq = round4i(D.n_qkv), hw = D.ff > 4 * D.d ? D.ff : 4 * D.d;
+  const int n2 = round4i((D.continuous ? 2 * D.A : D.A) + D.B);
+  int maxn = nq > hw ? nq : hw;
+  maxn = maxn > n2 ? maxn : n2;
+  maxn = maxn > D.d ? maxn : D.d;
+  int at = 0;
+  o.x = at; at += round4i(D.d);
+  o.xn = at; at += round4i(D.d);
+  o.qkv = at; at += nq;
+  o.att = at; at += round4i(I);
+  o.v1 = at; at += round4i(I);
+  o.h = at; at += round4i(hw);
+  o.ac = at; at += round4i(D.in_dim);
+  o.part = at; at += 5 * maxn;   // quarter sums [4][N] (+ the heads' output row behind them)
+  o.sc = at; at += 4 * round4i(D.Tmax);
+  o.lg = at; at += 64;
+  o.tot = at;
+  return o;
+}
+
+constexpr int ROW_MAX_L = 8;
+struct RowLayers {   // the layer descriptors by value (XtrlDecodeDesc.layers is a host array)
+  XtrlDecodeLayer l[ROW_MAX_L];
+};
+
+template <int DH>
+__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, const RowLayers RL, int t) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  __shared__ int rows_sh[EMB_MAX_E];
+  __shared__ int wsum[ROW_T / 64];
+  const RowLds Lo = row_lds(D);
+  float *xs = lds + Lo.x, *xn = lds + Lo.xn, *qkv = lds + Lo.qkv, *att = lds + Lo.att, *v1s = lds + Lo.v1;
+  float *hs = lds + Lo.h, *ac = lds + Lo.ac, *part = lds + Lo.part, *lg = lds + Lo.lg;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int S = D.S, d = D.d, H = D.H, I = H * DH, L = D.L;
+  // ---- compaction (as k_embed<CMP>): every workgroup ranks the live slots itself
+  int n_live = 0;
+  for (int c0 = 0; c0 < D.E; c0 += ROW_T) {
+    const int e = c0 + tid;
+    const bool al = e < D.E && D.alive[e] != 0;
+    const uint64_t bal = __ballot(al);
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = n_live, tot = 0;
+    for (int i = 0; i < ROW_T / 64; ++i) {
+      off += i < w ? wsum[i] : 0;
+      tot += wsum[i];
+    }
+    if (al) rows_sh[off + __popcll(bal & ((1ull << lane) - 1ull))] = e;
+    n_live += tot;
+    __syncthreads();
+  }
+  if (blockIdx.x == 0 && tid == 0) D.live_count[t & 1] = n_live;
+  const int n_act = D.continuous ? 2 * D.A : D.A;
+  const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
+  const float scale = 1.0f / sqrtf((float)DH);
+  for (int r = blockIdx.x; r < n_live; r += gridDim.x) {
+    const int e = rows_sh[r];
+    if (tid == 0) D.live_rows[(t & 1) * D.E + r] = e;
+    // ---- RSNorm of [state, prev reward], embeddings (k_embed's arithmetic and order)
+    if (tid <= S) {
+      const float xv = tid < S ? D.state[(int64_t)e * S + tid] : D.prev_reward[e];
+      part[tid] = (xv - D.rs_mean[tid]) / fmaxf(sqrtf(D.rs_var[tid]), D.rs_eps);
+      if (tid < S) D.traj_states[((int64_t)e * D.Tmax + t) * S + tid] = xv;
+    }
+    __syncthreads();
+    if (tid < d) {
+      const int c = tid;
+      float p = 0.f, se = 0.f;
+      for (int sidx = 0; sidx < S; ++sidx) {
+        p += part[sidx] * D.w_pin[c * S + sidx];
+        se += part[sidx] * D.w_se[c * S + sidx];
+      }
+      p += D.b_pin ? D.b_pin[c] : 0.f;
+      float ak;
+      if (D.continuous) {
+        float acc = 0.f;
+        for (int i = 0; i < D.A; ++i) acc += D.prev_action_f[e * D.A + i] * D.act_emb[c * D.A + i];
+        ak = acc + D.act_emb_b[c];
+      } else {
+        const int a = D.prev_action[e];
+        ak = a >= 0 ? D.act_emb[a * d + c] : 0.f;   // SafeEmbedding: -1 -> 0
+      }
+      if (D.state_only) ak = 0.f;
+      const float rew = (D.no_reward_cond || D.state_only) ? 0.f : part[S] * D.reward_embed[c];
+      xs[c] = p + (ak + rew);
+      ac[d + c] = se + D.b_se[c];
+      if (D.evolutionary && D.lat_embed) ac[2 * d + c] = D.lat_embed[(int64_t)e * d + c];
+    }
+    __syncthreads();
+    // ---- decoder layers
+    for (int l = 0; l < L; ++l) {
+      const XtrlDecodeLayer& Ly = RL.l[l];
+      row_layernorm(xs, Ly.ln_attn, d, xn);
+      row_gemv<0>(xn, d, Ly.w_qkv_t, nq4, Ly.b_qkv, nq4, qkv, part);
+      // attention: head h on wave h % 4; lane = g * DH + c (channel c, key group g of KG)
+      constexpr int KG = 64 / DH;
+      const int c = lane % DH, g = lane / DH;
+      const int64_t cbase0 = (int64_t)e * H;
+      float* sc = lds + Lo.sc + w * round4i(D.Tmax);
+      for (int h = w; h < H; h += ROW_T / 64) {
+        float q = qkv[h * DH + c], k = qkv[I + h * DH + c], v = qkv[2 * I + h * DH + c];
+        if (D.value_residual) {
+          if (l == 0) {
+            if (g == 0) {
+              v1s[h * DH + c] = v;
+              D.v1[(int64_t)r * I + h * DH + c] = v;
+            }
+          } else if (D.learned_mix) {
+            v = lerpf_(v, v1s[h * DH + c], sigmoidf_(qkv[3 * I + (D.gate_values ? I : 0) + h]));
+          }
+        }
+        if (D.rotary_abs && c < D.rot_dim) {
+          const float f = (float)t * D.inv_freq[c >> 1];
+          const float cs = cosf(f), sn = sinf(f);
+          const float qp = __shfl_xor(q, 1, 64), kp = __shfl_xor(k, 1, 64);
+          const float sgn = (c & 1) ? 1.f : -1.f;
+          q = q * cs + (sgn * qp) * sn;
+          k = k * cs + (sgn * kp) * sn;
+        }
+        const int64_t cb = (cbase0 + h) * D.Tmax * DH;
+        if (g == 0) {
+          Ly.k_cache[cb + (int64_t)t * DH + c] = k;
+          Ly.v_cache[cb + (int64_t)t * DH + c] = v;
+        }
+        float qreg[DH], kreg[DH];
+#pragma unroll
+        for (int i = 0; i < DH; ++i) {
+          qreg[i] = __shfl(q, i, 64);
+          kreg[i] = __shfl(k, i, 64);
+        }
+        // scores (one key per lane; the new key from registers), k_attn_decode's order
+        float mx = -INFINITY;
+        for (int j = lane; j <= t; j += 64) {
+          float s = 0.f;
+          if (j < t) {
+            const float4* kr = reinterpret_cast<const float4*>(Ly.k_cache + cb + (int64_t)j * DH);
+#pragma unroll
+            for (int i = 0; i < DH / 4; ++i) {
+              const float4 kv = kr[i];
+              s += qreg[4 * i] * kv.x;
+              s += qreg[4 * i + 1] * kv.y;
+              s += qreg[4 * i + 2] * kv.z;
+              s += qreg[4 * i + 3] * kv.w;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < DH; ++i) s += qreg[i] * kreg[i];
+          }
+          s *= scale;
+          sc[j] = s;
+          mx = fmaxf(mx, s);
+        }
+        mx = wave_max_dpp(mx);
+        float sum = 0.f;
+        for (int j = lane; j <= t; j += 64) {
+          const float p = expf(sc[j] - mx);
+          sc[j] = p;
+          sum += p;
+        }
+        sum = wave_sum_dpp(sum);
+        wave_sync();
+        // P.V: lane (g, c) sums keys j = g, g + KG, ... of channel c; the KG groups then meet
+        float acc = 0.f;
+        for (int j = g; j <= t; j += KG) acc += sc[j] * (j < t ? Ly.v_cache[cb + (int64_t)j * DH + c] : v);
+#pragma unroll
+        for (int o = DH; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
+        float o = acc / sum;
+        if (D.gate_values) o *= sigmoidf_(qkv[3 * I + h * DH + c]);
+        if (g == 0) att[h * DH + c] = o;
+        wave_sync();
+      }
+      __syncthreads();
+      // out-projection + residual (W_out^T is k-major), then FF: LN, FF1 + GELU, FF2 + residual
+      row_gemv<0>(att, I, Ly.w_out_t, d, nullptr, d, xs, part, xs);
+      row_layernorm(xs, Ly.ln_ff, d, xn);
+      row_gemv<1>(xn, d, Ly.w_ff1_t, ff, Ly.b_ff1, ff, hs, part);
+      row_gemv<0>(hs, ff, Ly.w_ff2_t, d, Ly.b_ff2, d, xs, part, xs);
+    }
+    // ---- heads: [final LN(x) | state embed | latent] -> SiLU hidden -> block-diagonal last layer
+    row_layernorm(xs, D.ln_final, d, ac);
+    row_gemv<2>(ac, D.in_dim, D.w_h1_t, 4 * d, D.b_h1, 4 * d, hs, part);
+    row_gemv<0>(hs, 4 * d, D.w_h2_t, n2, D.b_h2, n2, part + 4 * n2, part);   // (after the quarter sums)
+    const float* out2 = part + 4 * n2;
+    for (int n = tid; n < n_act + D.B; n += ROW_T) {
+      if (n < n_act) {
+        lg[n] = out2[n];
+        D.logits[(int64_t)r * n_act + n] = out2[n];
+      } else D.traj_values[((int64_t)e * D.Tmax + t) * D.B + (n - n_act)] = out2[n];
+    }
+    __syncthreads();
+    if (tid < SAMPLE_L) {
+      const SampleIn in = sample_load(D, e);
+      sample_row(D, t, e, tid, lg, in);
+    }
+    __syncthreads();
+  }
+}
+
+bool row_ok(const XtrlDecodeDesc* D) {
+  if (!D->w_h1_t || !D->w_h2_t || D->d > 256 || D->E > EMB_MAX_E || (D->continuous ? 2 * D->A : D->A) > 64 ||
+      D->L > ROW_MAX_L)
+    return false;
+  for (int l = 0; l < D->L; ++l)
+    if (!D->layers[l].w_qkv_t || !D->layers[l].w_ff1_t || !D->layers[l].w_ff2_t || !D->layers[l].w_out_t) return false;
+  return D->ff % 4 == 0 && (size_t)row_lds(*D).tot * sizeof(float) <= 96 * 1024;
+}
+
 }  // namespace
 
 int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
@@ -1357,6 +1647,25 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
       return rc;
   }
   return decode_heads(D, t, !mlp_fused(D, D->L - 1), s);
+}
+
+
+// the row-resident step over the live rows (workgroup b: rows b, b + grid, ...)
+int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s) {
+  if (int rc = check_desc(D)) return rc;
+  XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode rows: t=%d outside [0, %d)", t, D->Tmax);
+  XTRL_REQUIRE(row_ok(D), "decode rows: the row-resident step needs the k-major weights (w_*_t), d <= 256, "
+                          "E <= %d, at most %d layers and its LDS within 96 KiB", EMB_MAX_E, ROW_MAX_L);
+  XTRL_REQUIRE(max_rows > 0, "decode rows: max_rows %d", max_rows);
+  const dim3 grid(std::min(max_rows, D->E));
+  const size_t lds = (size_t)row_lds(*D).tot * sizeof(float);
+  RowLayers RL{};
+  for (int l = 0; l < D->L; ++l) RL.l[l] = D->layers[l];
+  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, RL, t);
+  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, RL, t);
+  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, RL, t);
+  XTRL_LAUNCHED("decode_row");
+  return XTRL_OK;
 }
 
 int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t, hipStream_t s) {
@@ -1461,6 +1770,9 @@ int sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const 
 
 }  // namespace xtrl
 
+extern "C" int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void* stream) {
+  return xtrl::decode_step_rows(desc, t, max_rows, xtrl::as_stream(stream));
+}
 extern "C" int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream) {
   return xtrl::decode_step(desc, t, xtrl::as_stream(stream));
 }

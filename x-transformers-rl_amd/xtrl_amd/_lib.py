@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -28,7 +28,7 @@ LOSS_TOK, LOSS_STATS = 30, 32
 
 class DecodeLayer(C.Structure):
     _fields_ = [(n, P) for n in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2',
-                                 'k_cache', 'v_cache', 'w_out_t', 'w_ff1x', 'w_ff2x')]
+                                 'k_cache', 'v_cache', 'w_out_t', 'w_ff1x', 'w_ff2x', 'w_qkv_t', 'w_ff1_t', 'w_ff2_t')]
 
 
 class RngState(C.Structure):
@@ -49,7 +49,8 @@ class DecodeDesc(C.Structure):
                                     'traj_actions', 'traj_actions_f', 'traj_logp', 'traj_rewards', 'traj_bounds',
                                     'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count',
                                     'mlp_part', 'mlp_cnt', 'lat_embed')]
-                + [('prof_events', C.POINTER(C.c_void_p))])
+                + [('prof_events', C.POINTER(C.c_void_p))]
+                + [(n, P) for n in ('w_h1_t', 'w_h2_t')])
 
 
 class FractalLevel(C.Structure):
@@ -134,6 +135,7 @@ SIGNATURES = {
     'xtrl_layernorm_f32': (I32, [P, I32, P, P, I32, I32, I32, P]),
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
+    'xtrl_decode_step_rows': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
     'xtrl_dgemm': (I32, [P, I32, P, P, P, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, P]),
     'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),

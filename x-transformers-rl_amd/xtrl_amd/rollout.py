@@ -30,6 +30,10 @@ from .model import WorldModelActorCritic
 SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
 
 
+def _r4(n):
+    return (n + 3) & ~3
+
+
 class RolloutEngine:
     def __init__(self, model: WorldModelActorCritic, E: int, Tmax: int, *, sim_mode=SIM_LANDER, hazard_log2=6,
                  clamp=None, use_graph=False, cfg=None):
@@ -70,8 +74,13 @@ class RolloutEngine:
         # decode weights (nn.Linear layouts; the GEMM operands are packed from them, self.wpk)
         self.w = dict(w_pin=z(d, S), act_emb=z(A, d) if not c.continuous else z(d, A),
                       act_emb_b=z(d) if c.continuous else None, reward_embed=z(d), w_se=z(d, S), b_se=z(d),
-                      ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_h2=z(nA + B, 4 * d), b_h2=z(nA + B),
-                      inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
+                      ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_h2=z(nA + B, 4 * d),
+                      b_h2=z(_r4(nA + B)), inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
+        self.nA = nA
+        # the row-resident step (xtrl_decode_step_rows): k-major heads (padding columns zero)
+        self.rows_max = self._rows_max(c)
+        if self.rows_max:
+            self.w.update(w_h1_t=z(c.in_dim, 4 * d), w_h2_t=z(4 * d, _r4(nA + B)))
         self.w_lat = None
         self._pk_src = [(self.w, 'w_h1'), (self.w, 'w_h2')]
         self._alloc_body(z)
@@ -86,8 +95,11 @@ class RolloutEngine:
         c = self.c
         d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
         # w_out_t: to_out transposed for the attention kernel's fused out-projection
-        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(self.n_qkv), w_out=z(d, I), w_out_t=z(I, d),
+        self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(_r4(self.n_qkv)), w_out=z(d, I), w_out_t=z(I, d),
                         ln_ff=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+        if self.rows_max:   # k-major copies for the row-resident step
+            for wl in self.wl:
+                wl.update(w_qkv_t=z(d, _r4(self.n_qkv)), w_ff1_t=z(d, ff), w_ff2_t=z(ff, d))
         # w_ff1x / w_ff2x: split-bf16 images of FF1 / FF2 for the one-launch feed-forward kernel
         if ff % 128 == 0 and d % 64 == 0 and d <= 256:
             n1, n2 = (int(L.lib().xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
@@ -108,7 +120,8 @@ class RolloutEngine:
         for i, (w, (kc, vc)) in enumerate(zip(self.wl, self.kv)):
             layers[i] = L.DecodeLayer(*(self._wv(w, k) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
                                                                  'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc),
-                                      self._wv(w, 'w_out_t'), self._wv(w, 'w_ff1x'), self._wv(w, 'w_ff2x'))
+                                      self._wv(w, 'w_out_t'), self._wv(w, 'w_ff1x'), self._wv(w, 'w_ff2x'),
+                                      *(self._wv(w, k) for k in ('w_qkv_t', 'w_ff1_t', 'w_ff2_t')))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -121,7 +134,7 @@ class RolloutEngine:
             D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
         w = self.w
         for k in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1',
-                  'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var'):
+                  'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var', 'w_h1_t', 'w_h2_t'):
             setattr(D, k, self._wv(w, k))
         D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
         for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
@@ -168,7 +181,7 @@ class RolloutEngine:
                     rows.append(torch.zeros(c.heads, c.dim, device=self.dev))
                     bias.append(torch.zeros(c.heads, device=self.dev))
             torch.cat(rows, out=wl['w_qkv'])
-            torch.cat(bias, out=wl['b_qkv'])
+            torch.cat(bias, out=wl['b_qkv'][:self.n_qkv])
             wl['w_out'].copy_(blk.to_out.weight)
             wl['w_out_t'].copy_(blk.to_out.weight.t())
             wl['ln_ff'].copy_(ln_f.gamma)
@@ -194,17 +207,25 @@ class RolloutEngine:
         torch.cat((model.action_head[0].weight, model.critic_head[0].weight), out=w['w_h1'])
         torch.cat((model.action_head[0].bias, model.critic_head[0].bias), out=w['b_h1'])
         # heads' last Linear as one block-diagonal weight over the [actor | critic] hidden row
-        nA, d2 = w['b_h2'].numel() - c.num_bins, 2 * c.dim
+        nA, d2 = self.nA, 2 * c.dim
         w['w_h2'].zero_()
         w['w_h2'][:nA, :d2].copy_(model.action_head[2].weight)
         w['w_h2'][nA:, d2:].copy_(model.critic_head[2].weight)
-        torch.cat((model.action_head[2].bias, model.critic_head[2].bias), out=w['b_h2'])
+        torch.cat((model.action_head[2].bias, model.critic_head[2].bias), out=w['b_h2'][:nA + c.num_bins])
         w['rs_mean'].copy_(rs_mean)
         w['rs_var'].copy_(rs_var)
         if c.evolutionary:
             self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
 
     def _pack_gemm_weights(self):
+        if self.rows_max:   # k-major copies of the row-resident step
+            w = self.w
+            w['w_h1_t'].copy_(w['w_h1'].t())
+            w['w_h2_t'][:, :w['w_h2'].shape[0]].copy_(w['w_h2'].t())
+            for wl in self.wl:
+                wl['w_qkv_t'][:, :self.n_qkv].copy_(wl['w_qkv'].t())
+                wl['w_ff1_t'].copy_(wl['w_ff1'].t())
+                wl['w_ff2_t'].copy_(wl['w_ff2'].t())
         lib = L.lib()
         for src, k in self._pk_src:
             t = src[k]
@@ -234,12 +255,32 @@ class RolloutEngine:
             self.lat_embed.copy_(F.linear(latent, *self.w_lat))
         L.check(L.lib().xtrl_rollout_begin(C.byref(self.desc), L.stream()), 'rollout_begin')
 
-    def step(self, t):
+    # the row-resident decode step (xtrl_decode_step_rows) takes over once at most this many rows are
+    # live: for d <= 128 a row's weights (<= ~2 MB) stream from the XCD's L2 and one launch per step
+    # beats the ~15 dependent launches of the multi-kernel step up to one workgroup per CU; wider
+    # models keep the multi-kernel step (their weights outgrow the L2).  XTRL_DECODE_ROWS=0: off.
+    ROWS = True
+
+    def _rows_max(self, c):
+        if not self.ROWS or os.environ.get('XTRL_DECODE_ROWS', '1') == '0':
+            return 0
+        nA = 2 * c.num_actions if c.continuous else c.num_actions
+        if c.dim > 128 or c.depth > 8 or nA > 64 or self.E > 8192 or (c.dim * c.ff_mult) % 4:
+            return 0
+        return 256
+
+    def step(self, t, rows=False):
+        """Decode step t: the multi-kernel step, or (``rows``) the row-resident one."""
+        if rows:
+            L.check(L.lib().xtrl_decode_step_rows(C.byref(self.desc), int(t), self.rows_max, L.stream()),
+                    f'decode_step_rows(t={t})')
+            return
         L.check(L.lib().xtrl_decode_step(C.byref(self.desc), int(t), L.stream()), f'decode_step(t={t})')
 
     def _steps(self):
+        rows = 0 < self.E <= self.rows_max
         for t in range(self.T):
-            self.step(t)
+            self.step(t, rows)
 
     def cache_tensors(self):
         """The per-episode decode state carried between deploy calls (Agent.forward hiddens)."""
@@ -263,31 +304,47 @@ class RolloutEngine:
             return self.traj
         if self.graph is None:
             self._steps()   # warm-up launch outside capture (code objects loaded)
+            if self.rows_max and self.E > self.rows_max:
+                self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
+                for t in range(self.T):
+                    self.step(t, True)   # (the row-resident kernel's code object too)
             self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
             CH = max(1, self.CHUNK)
             self._chunks = [(t0, min(t0 + CH, self.T)) for t0 in range(0, self.T, CH)]
             self._live_host = torch.zeros(len(self._chunks), dtype=torch.int32, pin_memory=True)
             self._live_dev = torch.zeros(len(self._chunks), dtype=torch.int32, device=self.dev)
-            graphs = []
-            for i, (t0, t1) in enumerate(self._chunks):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for t in range(t0, t1):
-                        self.step(t)
-                    # live rows at the chunk's last step (the embed kernel of step t1 - 1 counted them)
-                    self._live_dev[i:i + 1].copy_(self.live_count[(t1 - 1) & 1:((t1 - 1) & 1) + 1])
-                graphs.append(g)
+            # two graph sets: the multi-kernel step, and (rows_max) the row-resident step for the chunks
+            # after the live count has dropped to rows_max (it never rises within a rollout)
+            graphs = {}
+            for rows in [False] + ([True] if self.rows_max else []):
+                graphs[rows] = []
+                for i, (t0, t1) in enumerate(self._chunks):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        for t in range(t0, t1):
+                            self.step(t, rows)
+                        # live rows at the chunk's last step (its compaction counted them)
+                        self._live_dev[i:i + 1].copy_(self.live_count[(t1 - 1) & 1:((t1 - 1) & 1) + 1])
+                    graphs[rows].append(g)
             self.graph = graphs
             self._chunk_ev = [torch.cuda.Event() for _ in self._chunks]
         stream = torch.cuda.current_stream()
-        for i, g in enumerate(self.graph):
-            g.replay()
+        rows = 0 < self.E <= self.rows_max
+        self.chunks_rows = 0
+        self.rows_from_step = 0 if rows else self.T   # first step decoded by the row-resident step
+        for i in range(len(self._chunks)):
+            if rows and self.rows_from_step == self.T:
+                self.rows_from_step = self._chunks[i][0]
+            self.graph[rows][i].replay()
+            self.chunks_rows += int(rows)
             self._live_host[i:i + 1].copy_(self._live_dev[i:i + 1], non_blocking=True)
             self._chunk_ev[i].record(stream)
             if i >= 1:
                 self._chunk_ev[i - 1].synchronize()
-                if int(self._live_host[i - 1]) == 0:
+                live = int(self._live_host[i - 1])
+                if live == 0:
                     break
+                rows = rows or live <= self.rows_max
         return self.traj
 
     @torch.no_grad()
@@ -331,7 +388,7 @@ class RolloutEngine:
         for t in range(T + 1):
             if not live.any() and not pending.any():
                 break
-            self.step(t)
+            self.step(t, 0 < E <= self.rows_max)
             pending[:] = False
             if not live.any():
                 break
@@ -369,6 +426,8 @@ class FractalRolloutEngine(RolloutEngine):
     running sum of the level's outputs over the episode so far (the causal mean pools of the
     global-state update and the level projection); the step's global state starts at
     global_state_init and is updated level by level (fractal_rl.py:318-340, causal)."""
+
+    ROWS = False   # (no row-resident form of the fractal step)
 
     def __init__(self, model, E: int, Tmax: int, **kw):
         c = dataclasses.replace(model.cfg, depth=model.levels, gate_values=False, value_residual=False,
@@ -455,7 +514,7 @@ class FractalRolloutEngine(RolloutEngine):
         ops.gemm(w['g_init'][None, :d], self.wl[0]['w_c'], out=w['c0'][None])
         self._pack_gemm_weights()
 
-    def step(self, t):
+    def step(self, t, rows=False):
         L.check(L.lib().xtrl_fractal_decode_step(C.byref(self.desc), C.byref(self.fdesc), int(t), L.stream()),
                 f'fractal_decode_step(t={t})')
 
