@@ -190,6 +190,7 @@ typedef struct XtrlDecodeDesc {
    * w_h2_t [4d][round4(n_act + B)] (the block-diagonal w_h2 transposed, padding columns zero) */
   const float* w_h1_t;
   const float* w_h2_t;
+  const XtrlDecodeLayer* layers_dev;   /* DEVICE copy of the L layer descriptors (the row-resident step) */
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
@@ -213,6 +214,16 @@ int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void*
 int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state, const float* reward,
                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap,
                               void* stream);
+/* Host-env loop helpers (the reference's `env.step(action.tolist())` loop, xtrl.py:1284-1341), one call
+ * per half of a step.  The exception to the no-synchronisation rule above: xtrl_host_decode runs
+ * decode step t (rows_max > 0: xtrl_decode_step_rows), copies the rows' actions (prev_action [E]
+ * int32, continuous prev_action_f [E][A]) to act_host (pinned host memory) and synchronises the
+ * stream — the one host wait of a step.  xtrl_host_feedback copies the pinned stage (next_state
+ * [E][S] fp32 | reward [E] fp32 | terminated [E] u8 | truncated [E] u8) to dev_stage (device, same
+ * layout) and runs xtrl_rollout_env_feedback on it. */
+int xtrl_host_decode(const XtrlDecodeDesc* desc, int t, int rows_max, void* act_host, void* stream);
+int xtrl_host_feedback(const XtrlDecodeDesc* desc, int t, const void* host_stage, void* dev_stage, int t_limit,
+                       int bootstrap, void* stream);
 
 /* Decode-step projection (the rollout's GEMM):
  *   C[dst(m), n] = act( LN?(A)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])   for m < (m_dev ? *m_dev : M)

@@ -1330,19 +1330,24 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
 // (C2's long tail: one or two live episodes for hundreds of steps; a scalar host env: one row per
 // step); here a step is one launch whose time is the row's weight stream (k-major copies, float4
 // per lane, L2-resident for d <= 128) plus its dependent latency chain.
-// 256 threads = 4 waves; workgroup b takes live rows b, b + gridDim.x, ...
+// ROW_T threads; workgroup b takes live rows b, b + gridDim.x, ...
 // ---------------------------------------------------------------------------------------------
-constexpr int ROW_T = 256;
+constexpr int ROW_T = 512;      // 8 waves (2 per SIMD, up to 256 VGPRs: no spills), 8 float4 loads in flight per lane
+constexpr int ROW_PART = 4096;  // GEMV partial sums: k-groups x N <= 8 x ROW_T floats
 
 // out[n] = act(sum_k x[k] WT[k ldw + n] + bias[n]) (+ res[n]) for n < N (N % 4 == 0, k-major WT, 16-byte
-// aligned rows): wave w sums k in its quarter of [0, K) sequentially, lanes take float4 column
-// groups; the four quarter sums meet in LDS (fixed order).  ACT: 0 none, 1 GELU, 2 SiLU.
+// aligned rows).  The ROW_T threads form KG = ROW_T / (N / 4) k-groups (at most 32) x N / 4 float4
+// columns: thread (g, c4) sums its k-group's k sequentially (8 loads in flight), the KG partial rows
+// meet in LDS in group order.  ACT: 0 none, 1 GELU, 2 SiLU.  Called by every thread of the workgroup.
 template <int ACT>
 __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT, int ldw, const float* bias, int N,
                                          float* out, float* part, const float* res = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int Kq = (K + 3) >> 2, k0 = w * Kq, k1 = min(K, k0 + Kq);
-  for (int n4 = 4 * lane; n4 < N; n4 += 256) {
+  const int tid = threadIdx.x, NC4 = N >> 2;
+  const int KG = NC4 >= ROW_T ? 1 : min(32, ROW_T / NC4);
+  const int Kc = (K + KG - 1) / KG;
+  for (int item = tid; item < KG * NC4; item += ROW_T) {
+    const int g = item / NC4, n4 = 4 * (item - g * NC4);
+    const int k0 = g * Kc, k1 = min(K, k0 + Kc);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const float* wp = WT + n4;
 #pragma unroll 8
@@ -1354,11 +1359,13 @@ __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT,
       acc.z = fmaf(xv, wv.z, acc.z);
       acc.w = fmaf(xv, wv.w, acc.w);
     }
-    *reinterpret_cast<float4*>(part + w * N + n4) = acc;
+    *reinterpret_cast<float4*>(part + g * N + n4) = acc;
   }
   __syncthreads();
   for (int n = tid; n < N; n += ROW_T) {
-    float v = ((part[n] + part[N + n]) + (part[2 * N + n] + part[3 * N + n])) + (bias ? bias[n] : 0.f);
+    float v = part[n];
+    for (int g = 1; g < KG; ++g) v += part[g * N + n];
+    v += bias ? bias[n] : 0.f;
     if constexpr (ACT == 1) v = geluf_(v);
     if constexpr (ACT == 2) v = siluf_(v);
     if (res) v += res[n];
@@ -1403,9 +1410,6 @@ __host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
   RowLds o;
   const int I = D.H * D.dh, nq = round4i(D.n_qkv), hw = D.ff > 4 * D.d ? D.ff : 4 * D.d;
   const int n2 = round4i((D.continuous ? 2 * D.A : D.A) + D.B);
-  int maxn = nq > hw ? nq : hw;
-  maxn = maxn > n2 ? maxn : n2;
-  maxn = maxn > D.d ? maxn : D.d;
   int at = 0;
   o.x = at; at += round4i(D.d);
   o.xn = at; at += round4i(D.d);
@@ -1414,20 +1418,17 @@ __host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
   o.v1 = at; at += round4i(I);
   o.h = at; at += round4i(hw);
   o.ac = at; at += round4i(D.in_dim);
-  o.part = at; at += 5 * maxn;   // quarter sums [4][N] (+ the heads' output row behind them)
-  o.sc = at; at += 4 * round4i(D.Tmax);
+  o.part = at; at += ROW_PART + n2;   // partial rows (+ the heads' output row behind them)
+  o.sc = at; at += D.H * (round4i(D.Tmax) + 64);   // per head: the scores, then the new value row
   o.lg = at; at += 64;
   o.tot = at;
   return o;
 }
 
-constexpr int ROW_MAX_L = 8;
-struct RowLayers {   // the layer descriptors by value (XtrlDecodeDesc.layers is a host array)
-  XtrlDecodeLayer l[ROW_MAX_L];
-};
+constexpr int ROW_MAX_L = 64;
 
 template <int DH>
-__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, const RowLayers RL, int t) {
+__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_sh[EMB_MAX_E];
   __shared__ int wsum[ROW_T / 64];
@@ -1457,6 +1458,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, co
   const int n_act = D.continuous ? 2 * D.A : D.A;
   const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
   const float scale = 1.0f / sqrtf((float)DH);
+  constexpr int F4 = DH / 4, LPK = DH / 4, KPI = 64 / LPK;   // P.V: lanes per key row, key rows per wave pass
   for (int r = blockIdx.x; r < n_live; r += gridDim.x) {
     const int e = rows_sh[r];
     if (tid == 0) D.live_rows[(t & 1) * D.E + r] = e;
@@ -1493,15 +1495,13 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, co
     __syncthreads();
     // ---- decoder layers
     for (int l = 0; l < L; ++l) {
-      const XtrlDecodeLayer& Ly = RL.l[l];
+      const XtrlDecodeLayer& Ly = D.layers_dev[l];   // (device copy: scalar loads, no kernel-argument array)
       row_layernorm(xs, Ly.ln_attn, d, xn);
       row_gemv<0>(xn, d, Ly.w_qkv_t, nq4, Ly.b_qkv, nq4, qkv, part);
-      // attention: head h on wave h % 4; lane = g * DH + c (channel c, key group g of KG)
-      constexpr int KG = 64 / DH;
-      const int c = lane % DH, g = lane / DH;
-      const int64_t cbase0 = (int64_t)e * H;
-      float* sc = lds + Lo.sc + w * round4i(D.Tmax);
+      // attention: head h on wave h (waves past H idle); k_attn_decode's arithmetic and lane roles
       for (int h = w; h < H; h += ROW_T / 64) {
+        const int c = lane % DH, g = lane / DH;
+        float* sc = lds + Lo.sc + h * (round4i(D.Tmax) + 64);
         float q = qkv[h * DH + c], k = qkv[I + h * DH + c], v = qkv[2 * I + h * DH + c];
         if (D.value_residual) {
           if (l == 0) {
@@ -1521,57 +1521,93 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, co
           q = q * cs + (sgn * qp) * sn;
           k = k * cs + (sgn * kp) * sn;
         }
-        const int64_t cb = (cbase0 + h) * D.Tmax * DH;
+        const int64_t cb = ((int64_t)e * H + h) * D.Tmax * DH;
         if (g == 0) {
           Ly.k_cache[cb + (int64_t)t * DH + c] = k;
           Ly.v_cache[cb + (int64_t)t * DH + c] = v;
+          sc[round4i(D.Tmax) + c] = v;   // (the new value row, read by the P.V lanes below; q is broadcast
+          att[h * DH + c] = q;           //  from LDS, its head's att slot is written only after the scores)
         }
-        float qreg[DH], kreg[DH];
+        float kn = 0.f;
 #pragma unroll
-        for (int i = 0; i < DH; ++i) {
-          qreg[i] = __shfl(q, i, 64);
-          kreg[i] = __shfl(k, i, 64);
-        }
-        // scores (one key per lane; the new key from registers), k_attn_decode's order
-        float mx = -INFINITY;
-        for (int j = lane; j <= t; j += 64) {
-          float s = 0.f;
-          if (j < t) {
-            const float4* kr = reinterpret_cast<const float4*>(Ly.k_cache + cb + (int64_t)j * DH);
+        for (int i = 0; i < DH; ++i) kn += __shfl(q, i, 64) * __shfl(k, i, 64);
+        kn *= scale;   // the new key's score, k_attn_decode's channel order
+        wave_sync();
+        const float4* q4 = reinterpret_cast<const float4*>(att + h * DH);
+        // scores of the cached keys, one key per lane, NP 64-key passes in flight
+        constexpr int NP = DH == 16 ? 2 : 1;
+        float mx = kn;
+        for (int j0 = 0; j0 < t; j0 += 64 * NP) {
+          float4 kr[NP][F4];
 #pragma unroll
-            for (int i = 0; i < DH / 4; ++i) {
-              const float4 kv = kr[i];
-              s += qreg[4 * i] * kv.x;
-              s += qreg[4 * i + 1] * kv.y;
-              s += qreg[4 * i + 2] * kv.z;
-              s += qreg[4 * i + 3] * kv.w;
-            }
-          } else {
+          for (int u = 0; u < NP; ++u) {
+            const int j = min(j0 + lane + 64 * u, t - 1);
 #pragma unroll
-            for (int i = 0; i < DH; ++i) s += qreg[i] * kreg[i];
+            for (int i = 0; i < F4; ++i) kr[u][i] = reinterpret_cast<const float4*>(Ly.k_cache + cb + (int64_t)j * DH)[i];
           }
-          s *= scale;
-          sc[j] = s;
-          mx = fmaxf(mx, s);
+#pragma unroll
+          for (int u = 0; u < NP; ++u) {
+            const int j = j0 + lane + 64 * u;
+            float s_ = 0.f;
+#pragma unroll
+            for (int i = 0; i < F4; ++i) {
+              const float4 qv = q4[i];
+              s_ += qv.x * kr[u][i].x;
+              s_ += qv.y * kr[u][i].y;
+              s_ += qv.z * kr[u][i].z;
+              s_ += qv.w * kr[u][i].w;
+            }
+            s_ *= scale;
+            if (j < t) {
+              sc[j] = s_;
+              mx = fmaxf(mx, s_);
+            }
+          }
         }
         mx = wave_max_dpp(mx);
         float sum = 0.f;
-        for (int j = lane; j <= t; j += 64) {
+        for (int j = lane; j < t; j += 64) {
           const float p = expf(sc[j] - mx);
           sc[j] = p;
           sum += p;
         }
-        sum = wave_sum_dpp(sum);
+        const float pn = expf(kn - mx);
+        sum = wave_sum_dpp(sum) + pn;
         wave_sync();
-        // P.V: lane (g, c) sums keys j = g, g + KG, ... of channel c; the KG groups then meet
-        float acc = 0.f;
-        for (int j = g; j <= t; j += KG) acc += sc[j] * (j < t ? Ly.v_cache[cb + (int64_t)j * DH + c] : v);
+        // P.V: lane (kk = key in a pass, cq = channel quad), float4 value rows, 8 passes in flight
+        const int kk = lane % KPI, cq = lane / KPI;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j0 = 0; j0 < t; j0 += 8 * KPI) {
+          float4 vr[8];
 #pragma unroll
-        for (int o = DH; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);
-        float o = acc / sum;
-        if (D.gate_values) o *= sigmoidf_(qkv[3 * I + h * DH + c]);
-        if (g == 0) att[h * DH + c] = o;
-        wave_sync();
+          for (int u = 0; u < 8; ++u) {
+            const int j = min(j0 + kk + KPI * u, t - 1);
+            vr[u] = *reinterpret_cast<const float4*>(Ly.v_cache + cb + (int64_t)j * DH + 4 * cq);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int j = j0 + kk + KPI * u;
+            const float p = j < t ? sc[j] : 0.f;
+            acc.x += p * vr[u].x;
+            acc.y += p * vr[u].y;
+            acc.z += p * vr[u].z;
+            acc.w += p * vr[u].w;
+          }
+        }
+        acc.x = kpi_sum<KPI>(acc.x);
+        acc.y = kpi_sum<KPI>(acc.y);
+        acc.z = kpi_sum<KPI>(acc.z);
+        acc.w = kpi_sum<KPI>(acc.w);
+        if (kk == 0) {   // + the new key's term, normalise, gate
+          const float* vn = sc + round4i(D.Tmax) + 4 * cq;
+          float o4[4] = {(acc.x + pn * vn[0]) / sum, (acc.y + pn * vn[1]) / sum, (acc.z + pn * vn[2]) / sum,
+                         (acc.w + pn * vn[3]) / sum};
+          if (D.gate_values) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o4[i] *= sigmoidf_(qkv[3 * I + h * DH + 4 * cq + i]);
+          }
+          *reinterpret_cast<float4*>(att + h * DH + 4 * cq) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+        }
       }
       __syncthreads();
       // out-projection + residual (W_out^T is k-major), then FF: LN, FF1 + GELU, FF2 + residual
@@ -1583,13 +1619,15 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, co
     // ---- heads: [final LN(x) | state embed | latent] -> SiLU hidden -> block-diagonal last layer
     row_layernorm(xs, D.ln_final, d, ac);
     row_gemv<2>(ac, D.in_dim, D.w_h1_t, 4 * d, D.b_h1, 4 * d, hs, part);
-    row_gemv<0>(hs, 4 * d, D.w_h2_t, n2, D.b_h2, n2, part + 4 * n2, part);   // (after the quarter sums)
-    const float* out2 = part + 4 * n2;
+    float* out2 = part + ROW_PART;
+    row_gemv<0>(hs, 4 * d, D.w_h2_t, n2, D.b_h2, n2, out2, part);
     for (int n = tid; n < n_act + D.B; n += ROW_T) {
       if (n < n_act) {
         lg[n] = out2[n];
         D.logits[(int64_t)r * n_act + n] = out2[n];
-      } else D.traj_values[((int64_t)e * D.Tmax + t) * D.B + (n - n_act)] = out2[n];
+      } else {
+        D.traj_values[((int64_t)e * D.Tmax + t) * D.B + (n - n_act)] = out2[n];
+      }
     }
     __syncthreads();
     if (tid < SAMPLE_L) {
@@ -1601,7 +1639,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, co
 }
 
 bool row_ok(const XtrlDecodeDesc* D) {
-  if (!D->w_h1_t || !D->w_h2_t || D->d > 256 || D->E > EMB_MAX_E || (D->continuous ? 2 * D->A : D->A) > 64 ||
+  if (!D->layers_dev || !D->w_h1_t || !D->w_h2_t || D->d > 256 || D->E > EMB_MAX_E || (D->continuous ? 2 * D->A : D->A) > 64 ||
       D->L > ROW_MAX_L)
     return false;
   for (int l = 0; l < D->L; ++l)
@@ -1655,15 +1693,13 @@ int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode rows: t=%d outside [0, %d)", t, D->Tmax);
   XTRL_REQUIRE(row_ok(D), "decode rows: the row-resident step needs the k-major weights (w_*_t), d <= 256, "
-                          "E <= %d, at most %d layers and its LDS within 96 KiB", EMB_MAX_E, ROW_MAX_L);
+                          "E <= %d, at most %d layers, layers_dev and its LDS within 96 KiB", EMB_MAX_E, ROW_MAX_L);
   XTRL_REQUIRE(max_rows > 0, "decode rows: max_rows %d", max_rows);
   const dim3 grid(std::min(max_rows, D->E));
   const size_t lds = (size_t)row_lds(*D).tot * sizeof(float);
-  RowLayers RL{};
-  for (int l = 0; l < D->L; ++l) RL.l[l] = D->layers[l];
-  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, RL, t);
-  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, RL, t);
-  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, RL, t);
+  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, t);
+  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, t);
+  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, t);
   XTRL_LAUNCHED("decode_row");
   return XTRL_OK;
 }
@@ -1761,6 +1797,37 @@ int env_feedback(const XtrlDecodeDesc* D, int t, const float* next_state, const 
   return XTRL_OK;
 }
 
+// host-env loop (Learner.rollout_host), the device half of a step: decode step t (rows_max > 0: the
+// row-resident step), the rows' actions to pinned host memory, one stream synchronisation
+int host_decode(const XtrlDecodeDesc* D, int t, int rows_max, void* act_host, hipStream_t s) {
+  XTRL_REQUIRE(act_host, "host_decode: null action buffer");
+  if (int rc = rows_max > 0 ? decode_step_rows(D, t, rows_max, s) : decode_step(D, t, s)) return rc;
+  const size_t bytes = (size_t)D->E * (D->continuous ? D->A : 1) * 4;
+  const void* src = D->continuous ? (const void*)D->prev_action_f : (const void*)D->prev_action;
+  if (hipMemcpyAsync(act_host, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    set_error("host_decode: action copy / synchronisation failed");
+    return XTRL_E_HIP;
+  }
+  return XTRL_OK;
+}
+
+// ... and the env's results back: the pinned stage [E][S] next state | [E] reward | [E] terminated
+// (u8) | [E] truncated (u8) to the device stage (same layout), then the feedback kernel on it
+int host_feedback(const XtrlDecodeDesc* D, int t, const void* host_stage, void* dev_stage, int t_limit, int bootstrap,
+                  hipStream_t s) {
+  XTRL_REQUIRE(host_stage && dev_stage, "host_feedback: null stage");
+  const int E = D->E, S = D->S;
+  if (hipMemcpyAsync(dev_stage, host_stage, (size_t)4 * E * (S + 1) + 2 * (size_t)E, hipMemcpyHostToDevice, s) !=
+      hipSuccess) {
+    set_error("host_feedback: stage copy failed");
+    return XTRL_E_HIP;
+  }
+  float* f = static_cast<float*>(dev_stage);
+  const uint8_t* flags = reinterpret_cast<const uint8_t*>(f + (int64_t)E * (S + 1));
+  return env_feedback(D, t, f, f + (int64_t)E * S, flags, flags + E, t_limit, bootstrap, s);
+}
+
 int sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const int32_t* ep, hipStream_t s) {
   XTRL_REQUIRE(state && ep && E > 0 && S > 0, "sim_reset: bad arguments");
   hipLaunchKernelGGL(k_sim_reset, dim3((E + 255) / 256), dim3(256), 0, s, state, E, S, seed, update, ep);
@@ -1784,6 +1851,13 @@ extern "C" int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, cons
                                          int t_limit, int bootstrap, void* stream) {
   return xtrl::env_feedback(desc, t, next_state, reward, terminated, truncated, t_limit, bootstrap,
                             xtrl::as_stream(stream));
+}
+extern "C" int xtrl_host_decode(const XtrlDecodeDesc* desc, int t, int rows_max, void* act_host, void* stream) {
+  return xtrl::host_decode(desc, t, rows_max, act_host, xtrl::as_stream(stream));
+}
+extern "C" int xtrl_host_feedback(const XtrlDecodeDesc* desc, int t, const void* host_stage, void* dev_stage,
+                                  int t_limit, int bootstrap, void* stream) {
+  return xtrl::host_feedback(desc, t, host_stage, dev_stage, t_limit, bootstrap, xtrl::as_stream(stream));
 }
 extern "C" int xtrl_sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update,
                               const int32_t* episode_of_slot, void* stream) {

@@ -50,7 +50,8 @@ class DecodeDesc(C.Structure):
                                     'traj_values', 'x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count',
                                     'mlp_part', 'mlp_cnt', 'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))]
-                + [(n, P) for n in ('w_h1_t', 'w_h2_t')])
+                + [(n, P) for n in ('w_h1_t', 'w_h2_t')]
+                + [('layers_dev', C.POINTER(DecodeLayer))])
 
 
 class FractalLevel(C.Structure):
@@ -136,6 +137,8 @@ SIGNATURES = {
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
     'xtrl_decode_step_rows': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
+    'xtrl_host_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P, P]),
+    'xtrl_host_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, I32, I32, P]),
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
     'xtrl_dgemm': (I32, [P, I32, P, P, P, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, P]),
     'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),

@@ -137,6 +137,10 @@ class RolloutEngine:
                   'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var', 'w_h1_t', 'w_h2_t'):
             setattr(D, k, self._wv(w, k))
         D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
+        if self.rows_max:   # the row-resident step reads the layer descriptors from device memory
+            raw = bytes(memoryview(layers).cast('B'))
+            self._layers_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.dev)
+            D.layers_dev = C.cast(C.c_void_p(self._layers_dev.data_ptr()), C.POINTER(L.DecodeLayer))
         for k in ('state', 'prev_action', 'prev_action_f', 'prev_reward', 'alive', 'lens', 'cum_reward',
                   'episode_of_slot'):
             setattr(D, k, rows(getattr(self, k)))
@@ -267,7 +271,11 @@ class RolloutEngine:
         nA = 2 * c.num_actions if c.continuous else c.num_actions
         if c.dim > 128 or c.depth > 8 or nA > 64 or self.E > 8192 or (c.dim * c.ff_mult) % 4:
             return 0
-        return 256
+        r4 = lambda x: (x + 3) & ~3
+        d, I, ff = c.dim, c.heads * c.dim_head, c.dim * c.ff_mult   # decode.hip row_lds (in_dim <= 3 d)
+        lds = (2 * r4(d) + r4(self.n_qkv) + 2 * r4(I) + r4(max(ff, 4 * d)) + 3 * d + 4096 + r4(nA + c.num_bins)
+               + c.heads * (r4(self.T) + 64) + 64)
+        return 256 if 4 * lds <= 96 * 1024 else 0
 
     def step(self, t, rows=False):
         """Decode step t: the multi-kernel step, or (``rows``) the row-resident one."""
@@ -347,6 +355,10 @@ class RolloutEngine:
                 rows = rows or live <= self.rows_max
         return self.traj
 
+    def _host_decode(self, t, rows_max, desc, act_p, stream):
+        """Decode step t of a host-env wave, its actions to the pinned buffer, one host wait."""
+        L.check(L.lib().xtrl_host_decode(desc, t, rows_max, act_p, stream), f'host_decode(t={t})')
+
     @torch.no_grad()
     def run_host_wave(self, env_reset, env_step, seed, update, rows, latent=None, slots=None, max_steps=None,
                       bootstrap=True):
@@ -379,22 +391,25 @@ class RolloutEngine:
         lens = np.zeros(E, dtype=np.int64)
         totals = np.zeros(E, dtype=np.float64)
         lib = L.lib()
-        src = self.prev_action_f if self.c.continuous else self.prev_action
         st_state = st[:E * S].view(E, S).numpy()
         st_rew, st_flags = st[E * S:E * (S + 1)].numpy(), st[E * (S + 1):].view(torch.uint8)
-        ns_d, rw_d = dst[:E * S], dst[E * S:E * (S + 1)]
-        fl_d = dst[E * (S + 1):].view(torch.uint8)
+        flags = st_flags.numpy()
+        act_np = self._host_act.numpy().reshape(E, A) if self.c.continuous else self._host_act.numpy()
+        # one library call per half step: decode + action copy + the step's one host wait, then the
+        # env's results staged back + the feedback kernel (xtrl_host_decode / xtrl_host_feedback)
+        desc, stream = C.byref(self.desc), L.stream()
+        act_p, st_p, dst_p = self._host_act.data_ptr(), st.data_ptr(), dst.data_ptr()
+        rows_max = self.rows_max if 0 < E <= self.rows_max else 0
         pending = np.zeros(E, dtype=bool)    # rows taking their bootstrap decode step
         for t in range(T + 1):
             if not live.any() and not pending.any():
                 break
-            self.step(t, 0 < E <= self.rows_max)
-            pending[:] = False
-            if not live.any():
+            if not live.any():   # only bootstrap rows: their decode step, no env step
+                self.step(t, rows_max > 0)
                 break
-            self._host_act.copy_(src.reshape(-1), non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            act = self._host_act.numpy().reshape(E, A) if self.c.continuous else self._host_act.numpy()
+            self._host_decode(t, rows_max, desc, act_p, stream)
+            pending[:] = False
+            act = act_np
             ns, r, term, trunc = env_step(act, live.copy())
             ns = np.asarray(ns, dtype=np.float32).reshape(E, S)
             r = np.asarray(r, dtype=np.float64).reshape(E)
@@ -403,14 +418,10 @@ class RolloutEngine:
             totals[live] += r[live]
             lens[live] = t + 1
             st_state[:] = ns
-            st_rew[:] = r.astype(np.float32)
-            flags = st_flags.numpy()
+            st_rew[:] = r
             flags[:E] = term
             flags[E:2 * E] = trunc
-            dst.copy_(st, non_blocking=True)
-            L.check(lib.xtrl_rollout_env_feedback(C.byref(self.desc), t, L.ptr(ns_d), L.ptr(rw_d), L.ptr(fl_d[:E]),
-                                                  L.ptr(fl_d[E:2 * E]), T, int(bootstrap), L.stream()),
-                    'env_feedback')
+            L.check(lib.xtrl_host_feedback(desc, t, st_p, dst_p, T, int(bootstrap), stream), 'host_feedback')
             ended = live & (term | trunc | (t + 1 >= T))
             boot_now = live & trunc & ~term & bool(bootstrap)     # the last step (t + 1 == T) included
             boot_rows |= boot_now
@@ -428,6 +439,12 @@ class FractalRolloutEngine(RolloutEngine):
     global_state_init and is updated level by level (fractal_rl.py:318-340, causal)."""
 
     ROWS = False   # (no row-resident form of the fractal step)
+
+    def _host_decode(self, t, rows_max, desc, act_p, stream):
+        self.step(t)
+        src = self.prev_action_f if self.c.continuous else self.prev_action
+        self._host_act.copy_(src.reshape(-1), non_blocking=True)
+        torch.cuda.current_stream().synchronize()
 
     def __init__(self, model, E: int, Tmax: int, **kw):
         c = dataclasses.replace(model.cfg, depth=model.levels, gate_values=False, value_residual=False,
