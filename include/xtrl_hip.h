@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 14
+#define XTRL_ABI_VERSION 15
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -186,11 +186,19 @@ typedef struct XtrlDecodeDesc {
   /* optional profiling: 2 * Tmax * L hipEvent_t recorded around each attention-decode launch
    * (events[2 (t L + l)] before, [2 (t L + l) + 1] after); NULL = off */
   void** prof_events;
-  /* k-major heads for the row-resident step, or NULL: w_h1_t [in_dim][4d] (w_h1 transposed),
-   * w_h2_t [4d][round4(n_act + B)] (the block-diagonal w_h2 transposed, padding columns zero) */
+  /* k-major heads, or NULL: w_h1_t [in_dim][4d] (w_h1 transposed; the row-resident step),
+   * w_h2_t [4d][round4(n_act + B)] (the block-diagonal w_h2 transposed, padding columns zero; the
+   * row-resident step and the one-launch heads) */
   const float* w_h1_t;
   const float* w_h2_t;
   const XtrlDecodeLayer* layers_dev;   /* DEVICE copy of the L layer descriptors (the row-resident step) */
+  /* the one-launch heads (hidden layer + SiLU + last projection + sampling), or NULL: w_h1x = the
+   * split-bf16 image of w_h1 (xtrl_dgemm_pack_x6 with N = 4d, K = in_dim), heads_part = partial
+   * outputs [ceil(E / 16)][4d / 64][16][round4(n_act + B)], heads_cnt = one arrival counter per
+   * 16-row panel [ceil(E / 16)] (zero-initialised; every launch leaves them zero) */
+  const uint16_t* w_h1x;
+  float* heads_part;
+  uint32_t* heads_cnt;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and

@@ -983,7 +983,7 @@ struct FrMlp {
 };
 
 template <int NT2, int MT>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
-__global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
+__global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
                                              const float* res, float* C, int ldc, const float* g_next, float* Y,
                                              int ldy, const FrMlp fm) {
   constexpr int d = 64 * NT2, NT1 = MLP_HW / 64, BM = 16 * MT;
@@ -1104,20 +1104,41 @@ __global__ __launch_bounds__(256) void k_mlp(const XtrlDecodeDesc D, const XtrlD
   if (!last_sh) return;   // (workgroup-uniform)
   // ---- the last chunk workgroup of the panel: residual + b2 + the partials in chunk order (every
   //      load issued before the first store: C may be the residual row itself)
+  //      The partials are loaded HB chunks at a time, all HB x EPT loads of a batch in flight together
+  //      (a loop of one chunk per round trip measured ~8 memory round trips in this tail), clamped
+  //      past the last chunk and added in chunk order
   constexpr int EPT = BM * d / 256;   // elements per thread
+  constexpr int HB = EPT <= 16 ? 8 : 4;
   const float* part0 = D.mlp_part + (int64_t)p * HC * BM * d;
-  float v[EPT];
+  float v[EPT], rv[EPT], bv[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
     const int e = tid + 256 * k, r = e / d, col = e - r * d;
-    v[k] = res[(int64_t)min(m0 + r, M - 1) * d + col] + Ly.b_ff2[col];
+    rv[k] = res[(int64_t)min(m0 + r, M - 1) * d + col];
+    bv[k] = Ly.b_ff2[col];
   }
-  for (int cc = 0; cc < HC; ++cc)
+  for (int c0 = 0; c0 < HC; c0 += HB) {
+    float pv[HB][EPT];
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-      const int e = tid + 256 * k, r = e / d, col = e - r * d;
-      v[k] += __hip_atomic_load(part0 + ((int64_t)cc * BM + r) * d + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int u = 0; u < HB; ++u) {
+      const int cc = min(c0 + u, HC - 1);
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int e = tid + 256 * k, r = e / d, col = e - r * d;
+        pv[u][k] = __hip_atomic_load(part0 + ((int64_t)cc * BM + r) * d + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    if (c0 == 0) {
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) v[k] = rv[k] + bv[k];
+    }
+#pragma unroll
+    for (int u = 0; u < HB; ++u)
+      if (c0 + u < HC) {   // (uniform; no load under it)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) v[k] += pv[u][k];
+      }
+  }
   if (tid == 0) __hip_atomic_store(D.mlp_cnt + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
@@ -1286,13 +1307,219 @@ int dproj(const XtrlDecodeDesc* D, int t, const float* A, int lda, const float* 
 // [Wa1; Wc1]^T + b); the last Linear layers as one block-diagonal projection (actor logits to the
 // logits rows, critic bins straight into the trajectory row t of each live episode: Memory.value,
 // xtrl.py:1315); then sampling and the Sim step
+// ---------------------------------------------------------------------------------------------
+// the actor-critic heads in ONE launch (replaces the hidden-layer projection and the last
+// projection + sampling pair): workgroup (hidden chunk c of 64 units, 16-row panel p), 8 waves —
+// wave w multiplies the panel's [final-normed x | state embed | latent] rows (ac_in, staged in LDS)
+// by hidden tile w & 3 of the chunk over k half w >> 2 (split-bf16 products on the bf16 matrix
+// cores, the weight pre-split by xtrl_dgemm_pack_x6), the two k halves meet in LDS in order, + b1,
+// SiLU; then the chunk's partial of the block-diagonal last Linear (actor chunks c < HC / 2 feed the
+// n_act actor outputs, critic chunks the B value logits; fp32 FMAs over the chunk's 64 hidden units,
+// W2 rows staged in LDS) goes out with sc1 stores and the panel's arrival counter (k_mlp's hand-off)
+// elects the last chunk workgroup, which sums the partials in chunk order + b2, stores the logits /
+// value logits and runs the sampling + Sim step of its rows (SAMPLE_L lanes per row, the rows'
+// sampling inputs loaded while the matrix cores run).
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ inline int round4i(int x) { return (x + 3) & ~3; }
+constexpr int HD_HW = 64;   // hidden units per workgroup
+constexpr int HD_T = 512;   // threads
+struct HeadsLds {   // floats, carved from the dynamic LDS
+  int a, hp, hs, w2, lg, tot;
+};
+__host__ __device__ inline HeadsLds heads_lds(int in_dim, int np) {
+  HeadsLds o;
+  int at = 0;
+  o.a = at; at += 16 * (in_dim + 4);
+  o.hp = at; at += 2 * 16 * (HD_HW + 4);
+  o.hs = at; at += 16 * (HD_HW + 4);
+  o.w2 = at; at += HD_HW * np;
+  o.lg = at; at += 16 * 64;
+  o.tot = at;
+  return o;
+}
+
+template <int JH>   // k steps (32 deep) per wave: in_dim = 64 JH
+__global__ __launch_bounds__(HD_T) void k_heads_mlp(const XtrlDecodeDesc D, int t) {
+  extern __shared__ __attribute__((aligned(16))) float hl[];
+  __shared__ int e_sh[16];
+  __shared__ int last_sh;
+  constexpr int in_dim = 64 * JH, LDA = in_dim + 4, LDH = HD_HW + 4;
+  constexpr int AV = (16 * in_dim / 4 + HD_T - 1) / HD_T;   // A panel float4 per thread
+  constexpr int W2V = 8;                                    // W2 chunk float4 per thread (np <= 128)
+  constexpr int CHM = 8;                                    // chunks per head half at most (d <= 256)
+  const int n_act = D.continuous ? 2 * D.A : D.A, na2 = n_act + D.B, np = round4i(na2);
+  const int HC = 4 * D.d / HD_HW, HCh = HC / 2;
+  const int c = blockIdx.x, p = blockIdx.y, m0 = 16 * p;
+  const int M = D.live_count[t & 1];
+  if (m0 >= M) return;   // (workgroup-uniform)
+  const HeadsLds Lo = heads_lds(in_dim, np);
+  float *As = hl + Lo.a, *Hp = hl + Lo.hp, *Hs = hl + Lo.hs, *W2s = hl + Lo.w2, *lg = hl + Lo.lg;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, q = lane >> 4;
+  const int tile = w & 3, kh = w >> 2;
+  const bool actor = c < HCh;
+  const int n0 = actor ? 0 : n_act, nn = actor ? n_act : D.B;
+  // ---- one batch: the panel's rows, this wave's W1 fragments, b1, the chunk's W2 rows, b2, slots
+  float4 av[AV];
+#pragma unroll
+  for (int u = 0; u < AV; ++u) {
+    const int f = min(tid + HD_T * u, 16 * (in_dim / 4) - 1), r = f / (in_dim / 4), k4 = f - r * (in_dim / 4);
+    av[u] = reinterpret_cast<const float4*>(D.ac_in + (int64_t)min(m0 + r, M - 1) * D.in_dim)[k4];
+  }
+  const uint4* w1 = reinterpret_cast<const uint4*>(D.w_h1x);
+  const int JS = in_dim / 32;
+  const int64_t P1 = (int64_t)(4 * D.d / 16) * JS * 64;   // slots per piece plane
+  const int t16 = c * (HD_HW / 16) + tile;
+  uint4 bw[JH][3];
+  {
+    const uint4* wp = w1 + ((int64_t)t16 * JS + kh * JH) * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < JH; ++s)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) bw[s][pc] = wp[pc * P1 + 64 * s];
+  }
+  float b1v[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b1v[j] = D.b_h1[c * HD_HW + ((tid + HD_T * j) & (HD_HW - 1))];
+  const int w2n = HD_HW * np / 4;
+  float4 w2v[W2V];
+#pragma unroll
+  for (int u = 0; u < W2V; ++u)
+    w2v[u] = reinterpret_cast<const float4*>(D.w_h2_t + (int64_t)c * HD_HW * np)[min(tid + HD_T * u, w2n - 1)];
+  float b2v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b2v[j] = D.b_h2[min((tid + HD_T * j) % na2, np - 1)];
+  const int srow = tid / SAMPLE_L, sub = tid % SAMPLE_L;
+  int e = 0;
+  if (srow < 16) e = rows_of(D, t)[min(m0 + srow, M - 1)];
+  // ---- to LDS
+#pragma unroll
+  for (int u = 0; u < AV; ++u) {
+    const int f = tid + HD_T * u;
+    if (f < 16 * (in_dim / 4)) {
+      const int r = f / (in_dim / 4), k4 = f - r * (in_dim / 4);
+      *reinterpret_cast<float4*>(As + r * LDA + 4 * k4) = av[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < W2V; ++u)
+    if (tid + HD_T * u < w2n) reinterpret_cast<float4*>(W2s)[tid + HD_T * u] = w2v[u];
+  if (srow < 16 && sub == 0) e_sh[srow] = e;
+  SampleIn in{};
+  if (srow < 16) in = sample_load(D, e);   // (in flight during the products)
+  __syncthreads();
+  // ---- hidden tile over this wave's k half -> Hp[kh]
+  {
+    f32x4v acc[2] = {f32x4v{0.f, 0.f, 0.f, 0.f}, f32x4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < JH; ++s) {
+      const float* ap = As + lr * LDA + 32 * (kh * JH + s) + 8 * q;
+      bf16x8 a[3];
+      split3x8(*reinterpret_cast<const f32x4v*>(ap), *reinterpret_cast<const f32x4v*>(ap + 4), a[0], a[1], a[2]);
+      acc[s & 1] = mfma_x6(a, bw[s], acc[s & 1]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Hp[(kh * 16 + 4 * q + i) * LDH + 16 * tile + lr] = acc[0][i] + acc[1][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {   // 16 x 64 hidden values, two per thread
+    const int i = tid + HD_T * j, r = i / HD_HW, col = i & (HD_HW - 1);
+    Hs[r * LDH + col] = siluf_((Hp[r * LDH + col] + Hp[(16 + r) * LDH + col]) + b1v[j]);
+  }
+  __syncthreads();
+  // ---- the chunk's partial of its head's outputs (16 rows x nn over the chunk's 64 hidden units on
+  //      v_mfma_f32_16x16x4_f32, wave w: output columns n0 + 16 w ...) -> sc1 stores
+  float* part = D.heads_part + ((int64_t)p * HC + c) * 16 * np;
+  if (w < (nn + 15) / 16) {   // (wave-uniform)
+    const int n = n0 + 16 * w + lr;
+    const bool nv = n < n0 + nn;
+    const int nc = nv ? n : n0;
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < HD_HW / 4; ++s) {
+      const float b = W2s[(4 * s + q) * np + nc];
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Hs[lr * LDH + 4 * s + q], nv ? b : 0.f, acc, 0, 0, 0);
+    }
+    if (nv) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(part + (4 * q + i) * np + n, acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // the hand-off of k_mlp (MI355X_MICROARCH.md visibility, "Valid forms": sc1 stores, per-wave
+  // vmcnt(0), a workgroup barrier, one agent-scope counter add; the last arriver reads with sc1 loads)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last_sh = __hip_atomic_fetch_add(D.heads_cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(HC - 1);
+  __syncthreads();
+  if (!last_sh) return;   // (workgroup-uniform)
+  // ---- the last arriver: outputs = the partials of the head's chunks in chunk order + b2, every
+  //      partial load of a thread in flight together
+  const float* part0 = D.heads_part + (int64_t)p * HC * 16 * np;
+  float pv[4][CHM];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int it = min(tid + HD_T * j, 16 * na2 - 1), r = it / na2, n = it - r * na2, cb = n < n_act ? 0 : HCh;
+#pragma unroll
+    for (int u = 0; u < CHM; ++u)
+      pv[j][u] = __hip_atomic_load(part0 + ((int64_t)(cb + min(u, HCh - 1)) * 16 + r) * np + n, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) __hip_atomic_store(D.heads_cnt + p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int it = tid + HD_T * j;
+    if (it < 16 * na2) {
+      const int r = it / na2, n = it - r * na2, m = m0 + r;
+      float v = 0.f;
+#pragma unroll
+      for (int u = 0; u < CHM; ++u)
+        if (u < HCh) v += pv[j][u];
+      v += b2v[j];
+      if (m < M) {
+        if (n < n_act) {
+          lg[r * 64 + n] = v;
+          D.logits[(int64_t)m * n_act + n] = v;
+        } else {
+          D.traj_values[((int64_t)e_sh[r] * D.Tmax + t) * D.B + (n - n_act)] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (srow < 16 && m0 + srow < M) sample_row(D, t, e, sub, lg + srow * 64, in);
+}
+
+bool heads_fused(const XtrlDecodeDesc* D, bool final_norm) {
+  const int n_act = D->continuous ? 2 * D->A : D->A, np = round4i(n_act + D->B);
+  const int jh = D->in_dim / 64;
+  return !final_norm && D->w_h1x && D->w_h2_t && D->heads_part && D->heads_cnt && D->in_dim % 64 == 0 &&
+         (jh == 2 || jh == 3 || jh == 4 || jh == 6 || jh == 8 || jh == 12) && D->d % 32 == 0 && D->d <= 256 &&
+         n_act <= 64 && np <= 128 && (size_t)heads_lds(D->in_dim, np).tot * sizeof(float) <= 160 * 1024;
+}
+
 int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s) {
   const int E = D->E, d = D->d;
   int rc;
+  const int n_act = D->continuous ? 2 * D->A : D->A;
+  if (heads_fused(D, final_norm)) {   // hidden layer + SiLU + last projection + sampling: one launch
+    const dim3 grid(4 * d / HD_HW, (E + 15) / 16);
+    const size_t lds = (size_t)heads_lds(D->in_dim, round4i(n_act + D->B)).tot * sizeof(float);
+    switch (D->in_dim / 64) {
+      case 2: hipLaunchKernelGGL(k_heads_mlp<2>, grid, dim3(HD_T), lds, s, *D, t); break;
+      case 3: hipLaunchKernelGGL(k_heads_mlp<3>, grid, dim3(HD_T), lds, s, *D, t); break;
+      case 4: hipLaunchKernelGGL(k_heads_mlp<4>, grid, dim3(HD_T), lds, s, *D, t); break;
+      case 6: hipLaunchKernelGGL(k_heads_mlp<6>, grid, dim3(HD_T), lds, s, *D, t); break;
+      case 8: hipLaunchKernelGGL(k_heads_mlp<8>, grid, dim3(HD_T), lds, s, *D, t); break;
+      default: hipLaunchKernelGGL(k_heads_mlp<12>, grid, dim3(HD_T), lds, s, *D, t); break;
+    }
+    XTRL_LAUNCHED("heads_mlp");
+    return XTRL_OK;
+  }
   if ((rc = dproj(D, t, D->ac_in, D->in_dim, D->w_h1, D->in_dim, D->b_h1, final_norm ? D->ln_final : nullptr,
                   final_norm ? d : 0, nullptr, 0, D->hff, 4 * d, 4 * d, EPI_SILU, s)))
     return rc;
-  const int n_act = D->continuous ? 2 * D->A : D->A;
   const int ks = dg_ks(n_act + D->B, 4 * d);
   if (n_act <= 64 / ks) {   // block-diagonal projection + sampling in one launch (actor columns in block 0)
     DGemmArgs g;
@@ -1405,7 +1632,6 @@ __device__ __forceinline__ void row_layernorm(const float* x, const float* g, in
 struct RowLds {   // floats, carved from the dynamic LDS
   int x, xn, qkv, att, v1, h, ac, part, sc, lg, tot;
 };
-__host__ __device__ inline int round4i(int x) { return (x + 3) & ~3; }
 __host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
   RowLds o;
   const int I = D.H * D.dh, nq = round4i(D.n_qkv), hw = D.ff > 4 * D.d ? D.ff : 4 * D.d;

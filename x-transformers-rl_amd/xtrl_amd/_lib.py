@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -51,7 +51,8 @@ class DecodeDesc(C.Structure):
                                     'mlp_part', 'mlp_cnt', 'lat_embed')]
                 + [('prof_events', C.POINTER(C.c_void_p))]
                 + [(n, P) for n in ('w_h1_t', 'w_h2_t')]
-                + [('layers_dev', C.POINTER(DecodeLayer))])
+                + [('layers_dev', C.POINTER(DecodeLayer))]
+                + [(n, P) for n in ('w_h1x', 'heads_part', 'heads_cnt')])
 
 
 class FractalLevel(C.Structure):

@@ -77,10 +77,20 @@ class RolloutEngine:
                       ln_final=z(d), w_h1=z(4 * d, c.in_dim), b_h1=z(4 * d), w_h2=z(nA + B, 4 * d),
                       b_h2=z(_r4(nA + B)), inv_freq=z(max(dh // 4, 1)), rs_mean=z(S + 1), rs_var=z(S + 1))
         self.nA = nA
-        # the row-resident step (xtrl_decode_step_rows): k-major heads (padding columns zero)
+        # k-major block-diagonal last head Linear (padding columns zero): the one-launch heads and the
+        # row-resident step (xtrl_decode_step_rows, which also reads the k-major hidden layer)
+        self.w['w_h2_t'] = z(4 * d, _r4(nA + B))
         self.rows_max = self._rows_max(c)
         if self.rows_max:
-            self.w.update(w_h1_t=z(c.in_dim, 4 * d), w_h2_t=z(4 * d, _r4(nA + B)))
+            self.w['w_h1_t'] = z(c.in_dim, 4 * d)
+        # the one-launch heads (k_heads_mlp): split-bf16 image of the hidden layer, per 16-row panel one
+        # partial output row block per 64-wide hidden chunk and an arrival counter
+        if c.in_dim % 64 == 0 and d % 32 == 0:
+            self.w['w_h1x'] = z(int(L.lib().xtrl_dgemm_packed_x6_elems(4 * d, c.in_dim)), dt=torch.int16)
+            self.heads_part = z((E + 15) // 16 * (4 * d // 64) * 16 * _r4(nA + B))
+            self.heads_cnt = z((E + 15) // 16, dt=i32)
+        else:
+            self.heads_part = self.heads_cnt = None
         self.w_lat = None
         self._pk_src = [(self.w, 'w_h1'), (self.w, 'w_h2')]
         self._alloc_body(z)
@@ -134,7 +144,7 @@ class RolloutEngine:
             D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
         w = self.w
         for k in ('w_pin', 'b_pin', 'act_emb', 'act_emb_b', 'reward_embed', 'w_se', 'b_se', 'ln_final', 'w_h1', 'b_h1',
-                  'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var', 'w_h1_t', 'w_h2_t'):
+                  'w_h2', 'b_h2', 'inv_freq', 'rs_mean', 'rs_var', 'w_h1_t', 'w_h2_t', 'w_h1x'):
             setattr(D, k, self._wv(w, k))
         D.layers = C.cast(layers, C.POINTER(L.DecodeLayer))
         if self.rows_max:   # the row-resident step reads the layer descriptors from device memory
@@ -149,10 +159,12 @@ class RolloutEngine:
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
         for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count', 'lat_embed',
-                  'mlp_part', 'mlp_cnt'):
+                  'mlp_part', 'mlp_cnt', 'heads_part', 'heads_cnt'):
             setattr(D, k, rows(getattr(self, k)))
         if os.environ.get('XTRL_DECODE_MLP', '1') == '0':   # A/B switch: the two-GEMM feed-forward
             D.mlp_part = None
+        if os.environ.get('XTRL_DECODE_HEADS', '0') == '0':   # A/B switch: the one-launch heads (opt-in)
+            D.heads_part = None
         self.desc, self._layers = D, layers
 
     # ------------------------------------------------------------------------------------------
@@ -222,15 +234,19 @@ class RolloutEngine:
             self.w_lat = (model.latent_to_embed.weight.detach().clone(), model.latent_to_embed.bias.detach().clone())
 
     def _pack_gemm_weights(self):
+        w = self.w
+        w['w_h2_t'][:, :w['w_h2'].shape[0]].copy_(w['w_h2'].t())
         if self.rows_max:   # k-major copies of the row-resident step
-            w = self.w
             w['w_h1_t'].copy_(w['w_h1'].t())
-            w['w_h2_t'][:, :w['w_h2'].shape[0]].copy_(w['w_h2'].t())
             for wl in self.wl:
                 wl['w_qkv_t'][:, :self.n_qkv].copy_(wl['w_qkv'].t())
                 wl['w_ff1_t'].copy_(wl['w_ff1'].t())
                 wl['w_ff2_t'].copy_(wl['w_ff2'].t())
         lib = L.lib()
+        if 'w_h1x' in w:
+            t = w['w_h1']
+            L.check(lib.xtrl_dgemm_pack_x6(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(w['w_h1x']), L.stream()),
+                    'dgemm_pack_x6(w_h1)')
         for src, k in self._pk_src:
             t = src[k]
             L.check(lib.xtrl_dgemm_pack(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(self.wpk[(id(src), k)]),
