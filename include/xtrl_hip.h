@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 15
+#define XTRL_ABI_VERSION 16
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -106,6 +106,11 @@ typedef struct XtrlDecodeLayer {
   const float* w_qkv_t;
   const float* w_ff1_t;
   const float* w_ff2_t;
+  /* fp32 fragment images (xtrl_dgemm_pack_f8) of FF1 [ff][d] and FF2 [d][ff], or NULL: when both are
+   * set the one-launch feed-forward reads these (4 bytes a weight instead of the split images' 6)
+   * and splits the weight fragments into their bf16 pieces itself — the same pieces, bit-identical */
+  const float* w_ff1f;
+  const float* w_ff2f;
 } XtrlDecodeLayer;
 
 typedef struct XtrlRngState {   /* device memory; read by the sampling / sim kernels */
@@ -166,7 +171,7 @@ typedef struct XtrlDecodeDesc {
   float* x;      /* [E][d] residual stream */
   float* qkv;    /* [E][n_qkv] */
   float* att;    /* [E][I] */
-  float* hff;    /* [E][max(ff, 4d)] */
+  float* hff;    /* [E][max(ff or 2 ff with ff_glu, 4d)] */
   float* ac_in;  /* [E][in_dim]  (final-normed embed | state embed | latent embed) */
   float* logits; /* [E][A or 2A] */
   float* v1;     /* [E][I] first layer's values (value residual) */
@@ -199,6 +204,16 @@ typedef struct XtrlDecodeDesc {
   const uint16_t* w_h1x;
   float* heads_part;
   uint32_t* heads_cnt;
+  /* the row-resident step's split heads (up to 4 workgroups per row), or NULL (one workgroup per
+   * row): row_part = partial outputs [E][4][round4(n_act + B)], row_cnt = one arrival counter per
+   * row [E] (zero-initialised; every launch leaves them zero) */
+  float* row_part;
+  uint32_t* row_cnt;
+  /* world_model['ff_glu']: FF1 (w_ff1 / b_ff1) is the GLU projection [2 ff][d]; the step forms
+   * hglu [E][ff] = value * gelu(gate) from it (the one-launch feed-forward and the row-resident step
+   * are not used) */
+  int ff_glu;
+  float* hglu;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
@@ -218,7 +233,8 @@ int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void*
  * terminated [E] (stored as is_boundary), truncated [E] or NULL.  An episode ends when terminated,
  * truncated or t + 1 == t_limit (max_timesteps); with `bootstrap` a truncated, not terminated
  * episode takes one more decode step that only writes its critic logits (the next state's value,
- * xtrl.py:1323-1336) into the padding slot traj_values[e][t + 1] (needs t + 1 < Tmax). */
+ * xtrl.py:1323-1336) into the padding slot traj_values[e][t + 1] (needs t + 1 < Tmax); a row still
+ * flagged for that step (alive 2: the row-resident step leaves the flag) is cleared here. */
 int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* next_state, const float* reward,
                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap,
                               void* stream);
@@ -255,6 +271,11 @@ int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, void* stre
  * of a plane holding W[16 (n / 16) + lane % 16][32 s + 8 (lane / 16) .. + 7], zero past N. */
 int64_t xtrl_dgemm_packed_x6_elems(int N, int K);
 int xtrl_dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, void* stream);
+/* The same fragment order in fp32 (K a multiple of 32): two planes of xtrl_dgemm_packed_f8_floats(N, K)
+ * / 2 floats, float4 slot (n / 16 * K / 32 + s) * 64 + lane of plane h holding
+ * W[16 (n / 16) + lane % 16][32 s + 8 (lane / 16) + 4 h .. + 3], zero past N. */
+int64_t xtrl_dgemm_packed_f8_floats(int N, int K);
+int xtrl_dgemm_pack_f8(const float* W, int ldw, int N, int K, float* Wp, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fractal policy body, one decode step (fractal_rl.py:37-346, 510-619 restated per timestep and
@@ -462,6 +483,13 @@ typedef struct XtrlTrainDesc {
    * — written once per backward, so the caller's stream never waits for the weight-gradient stream
    * before the final join; 0: one plane each, reused layer by layer behind events */
   int scratch_per_layer;
+  /* world_model['ff_glu'] (x-transformers FeedForward glu = True): w_ff1 / b_ff1 are the GLU
+   * projection [2 ff][d] / [2 ff] (value rows, then gate rows); per layer u holds its output
+   * [T][ld_u2] (ld_u2 >= 2 ff, a multiple of 4) for the backward, dff is the projection's gradient
+   * ([L][T][ld_u2] planes), glu_dh [T][ld_ff] the gradient w.r.t. the GLU + dropout output.  0: GELU */
+  int ff_glu;
+  int ld_u2;
+  float* glu_dh;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
@@ -536,6 +564,13 @@ int xtrl_linear_gelu_drop(const float* X, int ldx, const float* W, const float* 
 /* the feed-forward dropout keep mask of layer `layer` as uint8 [M][N] (tests / reference mode) */
 int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset, uint32_t layer,
                          void* stream);
+/* x-transformers FeedForward with glu = True (world_model['ff_glu']): u [M][2 ff] = the GLU projection's
+ * output [value | gate], h[m][j] = drop(u[m][j] * gelu(u[m][ff + j])) (erf GELU, the dropout keep bits
+ * of xtrl_ff_dropout_mask(seed, offset, layer) over [M][ff]); the backward writes du [M][2 ff] from dh */
+int xtrl_glu_drop_fwd(const float* u, int ldu, float* h, int ldh, int M, int ff, float p, uint64_t seed,
+                      uint32_t offset, uint32_t layer, void* stream);
+int xtrl_glu_drop_bwd(const float* dh, int lddh, const float* u, int ldu, float* du, int lddu, int M, int ff, float p,
+                      uint64_t seed, uint32_t offset, uint32_t layer, void* stream);
 /* floats of XtrlTrainDesc.part (the partial-sum workspace) a learn step of T = b * n tokens needs;
  * host-only, no device call */
 int64_t xtrl_train_part_floats(int T, int b, int d, int A);

@@ -220,6 +220,7 @@ class ModelConfig:
     learned_mix: bool = False
     ff_mult: int = 4          # x-transformers FeedForward mult, reached through world_model['ff_mult']
     ff_no_bias: bool = False  # world_model['ff_no_bias'] (x-transformers FeedForward no_bias)
+    ff_glu: bool = False      # world_model['ff_glu'] (x-transformers FeedForward glu: GELU-gated project-in)
 
 
 class OracleWMAC(nn.Module):
@@ -236,7 +237,7 @@ class OracleWMAC(nn.Module):
                                    verbose=False, attn_gate_values=cfg.gate_values,
                                    add_value_residual=cfg.value_residual,
                                    learned_value_residual_mix=cfg.learned_mix, ff_mult=cfg.ff_mult,
-                                   ff_no_bias=cfg.ff_no_bias))
+                                   ff_no_bias=cfg.ff_no_bias, ff_glu=cfg.ff_glu))
         self.reward_embed = nn.Parameter(torch.ones(d) * 1e-2)
         if cfg.continuous:
             self.action_embeds = nn.Linear(cfg.num_actions, d)
@@ -497,6 +498,7 @@ class LearnerConfig:
     learned_mix: bool = False
     ff_mult: int = 4
     ff_no_bias: bool = False
+    ff_glu: bool = False
     continuous: bool = False
     squash: bool = True
     clamp: tuple | None = None
@@ -550,7 +552,7 @@ class OracleLearner:
                          c.reward_range, 100, c.continuous, c.squash, c.evolutionary,
                          self.gp['dim'] if c.evolutionary else 0, c.frac_head_grad, c.beta_s, c.eps_clip,
                          c.value_clip, c.dropout, c.reward_dropout, True, c.gate_values, c.value_residual,
-                         c.learned_mix, c.ff_mult, c.ff_no_bias)
+                         c.learned_mix, c.ff_mult, c.ff_no_bias, c.ff_glu)
         self.model = model_factory(mc) if model_factory is not None else OracleWMAC(mc)
         if init_state_dict is not None:
             self.model.load_state_dict(init_state_dict)

@@ -258,14 +258,30 @@ class Attention(nn.Module):
         return self.to_out(out), (k, v), orig_v
 
 
-class FeedForward(nn.Module):
-    """x-transformers FeedForward (GELU, no GLU); ``no_bias``: both Linears without bias (ff_no_bias)."""
+class GLU(nn.Module):
+    """x-transformers GLU (the ``ff_glu`` project-in): ``proj`` = Linear(dim, 2 inner) (always with a
+    bias), ``x, gate = proj(x).chunk(2, -1)``, out = x * act(gate) (no mult_bias)."""
 
-    def __init__(self, dim, mult=4, dropout=0., no_bias=False):
+    def __init__(self, dim_in, dim_out, activation):
+        super().__init__()
+        self.act = activation
+        self.proj = nn.Linear(dim_in, dim_out * 2)
+
+    def forward(self, x):
+        x, gate = self.proj(x).chunk(2, dim=-1)
+        return x * self.act(gate)
+
+
+class FeedForward(nn.Module):
+    """x-transformers FeedForward (GELU); ``no_bias``: the Linears without bias (ff_no_bias; the GLU
+    projection keeps its bias); ``glu``: the GLU project-in (ff_glu)."""
+
+    def __init__(self, dim, mult=4, dropout=0., no_bias=False, glu=False):
         super().__init__()
         inner = dim * mult
-        self.ff = nn.Sequential(nn.Sequential(nn.Linear(dim, inner, bias=not no_bias), nn.GELU()), nn.Dropout(dropout),
-                                nn.Linear(inner, dim, bias=not no_bias))
+        project_in = (GLU(dim, inner, nn.GELU()) if glu else
+                      nn.Sequential(nn.Linear(dim, inner, bias=not no_bias), nn.GELU()))
+        self.ff = nn.Sequential(project_in, nn.Dropout(dropout), nn.Linear(inner, dim, bias=not no_bias))
 
     def forward(self, x):
         return self.ff(x)
@@ -327,7 +343,7 @@ class LayerIntermediates:
 class Decoder(nn.Module):
     def __init__(self, dim, depth, heads=8, attn_dim_head=64, rotary_pos_emb=False, attn_dropout=0.,
                  ff_dropout=0., verbose=True, attn_gate_values=False, add_value_residual=False,
-                 learned_value_residual_mix=False, ff_mult=4, ff_no_bias=False, **unsupported):
+                 learned_value_residual_mix=False, ff_mult=4, ff_no_bias=False, ff_glu=False, **unsupported):
         super().__init__()
         if unsupported:
             raise NotImplementedError(f'restated Decoder does not model {sorted(unsupported)}')
@@ -339,7 +355,7 @@ class Decoder(nn.Module):
                              learned_value_residual_mix=learned_value_residual_mix and add_value_residual and ind > 0)
             self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]), attn, _Residual()]))
             self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]),
-                                              FeedForward(dim, ff_mult, ff_dropout, ff_no_bias), _Residual()]))
+                                              FeedForward(dim, ff_mult, ff_dropout, ff_no_bias, ff_glu), _Residual()]))
         self.rotary_pos_emb = RotaryEmbedding(attn_dim_head // 2) if rotary_pos_emb else None
         self.final_norm = LayerNorm(dim)
 

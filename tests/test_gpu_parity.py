@@ -390,7 +390,7 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
                  hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None,
-                 ff_mult=4, genes=3, shard_by_gene=False, ff_no_bias=False):
+                 ff_mult=4, genes=3, shard_by_gene=False, ff_no_bias=False, ff_glu=False):
     """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides.
     ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult)."""
     from xtrl_amd import Learner, SynthVecSim
@@ -405,6 +405,8 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
         wm['ff_mult'] = ff_mult
     if ff_no_bias:
         wm['ff_no_bias'] = True
+    if ff_glu:
+        wm['ff_glu'] = True
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     gp = dict(dim=gene_dim, num_genes_per_island=genes, num_selected=2, tournament_size=2)
@@ -426,7 +428,7 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
                         learned_mix=gates, continuous=cont, clamp=(-1., 1.) if cont else None, evolutionary=evo,
                         evolve_every=1, evolve_after_step=0, gene_pool=gp, max_timesteps=T, batch_size=batch,
                         num_episodes_per_update=episodes, sim_mode=mode, hazard_log2=hazard, seed=seed,
-                        reward_dropout=reward_dropout, ff_mult=ff_mult, ff_no_bias=ff_no_bias)
+                        reward_dropout=reward_dropout, ff_mult=ff_mult, ff_no_bias=ff_no_bias, ff_glu=ff_glu)
     sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
     genes = learner.agent.gene_pool.genes.clone() if evo else None
     oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes, model_factory=factory)
@@ -1058,6 +1060,26 @@ def test_ff_no_bias_rollout_and_learn_match_oracle(dim, gates):
     episodes_o, _ = oracle.rollout(0)
     compare_rollout(traj, lens, episodes_o)
     seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2)
+    assert len(seen) == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dim,gates,no_bias,dropout', [(64, True, False, 0.25), (128, False, True, 0.)])
+def test_ff_glu_rollout_and_learn_match_oracle(dim, gates, no_bias, dropout):
+    """world_model['ff_glu'] (x-transformers FeedForward glu: the GLU projection [2 ff][d], value *
+    gelu(gate), then the dropout): the rollout (GLU projection GEMM + k_glu_rows, the multi-kernel decode
+    step) and the fused learn step (GLU projection GEMM, k_glu_fwd / k_glu_bwd with the feed-forward
+    dropout stream, gradients of the [2 ff] projection) against the oracle's GLU FeedForward; with
+    ff_no_bias the GLU projection keeps its bias (x-transformers GLU), the last Linear has none."""
+    learner, env, oracle = make_learner(depth=2, gates=gates, T=24, episodes=6, batch=3, seed=8, hazard=3, dim=dim,
+                                        ff_glu=True, ff_no_bias=no_bias)
+    names = [n for n, _ in learner.agent.model.named_parameters()]
+    assert any(n.endswith('ff.0.proj.weight') for n in names) and any(n.endswith('ff.0.proj.bias') for n in names)
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 24)
+    torch.cuda.synchronize()
+    episodes_o, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2, dropout=dropout)
     assert len(seen) == 2
 
 

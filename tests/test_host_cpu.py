@@ -253,13 +253,14 @@ def test_world_model_option_validation():
     a = Learner(5, 2, (-1., 1.), world_model=dict(attn_dim_head=16, heads=4, depth=1, attn_flash=True), **kw).agent
     assert a.cfg.depth == 1 and a.cfg.heads == 4
     with pytest.raises(NotImplementedError):
-        Learner(5, 2, (-1., 1.), world_model=dict(attn_dim_head=16, heads=4, depth=1, ff_glu=True), **kw)
+        Learner(5, 2, (-1., 1.), world_model=dict(attn_dim_head=16, heads=4, depth=1, ff_swish=True), **kw)
 
 
 def test_world_model_options_defaults_accepted_others_named():
     """world_model options at their x-transformers default build the same network (accepted); the
     implementation switches attn_flash / attn_onnxable are accepted; ff_no_bias builds bias-free
-    feed-forward Linears; an option the MI355X decoder does not implement raises, naming it."""
+    feed-forward Linears, ff_glu the GLU project-in (x-transformers GLU: ff.0.proj [2 ff][d] with a
+    bias); an option the MI355X decoder does not implement raises, naming it."""
     from xtrl_amd import Learner
     kw = dict(num_episodes_per_update=2, batch_size=2, accelerate_kwargs=dict(device='cpu'),
               agent_kwargs=dict(hidden_dim=16), use_graph=False)
@@ -272,6 +273,11 @@ def test_world_model_options_defaults_accepted_others_named():
     names = list(c.agent.model.state_dict())
     assert not any(n.endswith(('ff.0.0.bias', 'ff.2.bias')) for n in names)
     assert len(names) == len(list(b.agent.model.state_dict())) - 2
-    for opt in (dict(ff_glu=True), dict(attn_qk_norm=True), dict(use_rmsnorm=True), dict(attn_kv_heads=2)):
+    g = Learner(5, 2, (-1., 1.), world_model=dict(base, ff_glu=True), **kw).agent.model.state_dict()
+    proj = [k for k in g if k.endswith('ff.0.proj.weight')]
+    assert len(proj) == 1 and tuple(g[proj[0]].shape) == (2 * 4 * 16, 16)
+    assert tuple(g[proj[0].replace('weight', 'bias')].shape) == (2 * 4 * 16,)
+    assert not any(k.endswith('ff.0.0.weight') for k in g)
+    for opt in (dict(ff_swish=True), dict(attn_qk_norm=True), dict(use_rmsnorm=True), dict(attn_kv_heads=2)):
         with pytest.raises(NotImplementedError, match=next(iter(opt))):
             Learner(5, 2, (-1., 1.), world_model=dict(base, **opt), **kw)

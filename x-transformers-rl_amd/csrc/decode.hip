@@ -609,9 +609,11 @@ __device__ __forceinline__ SampleIn sample_load(const XtrlDecodeDesc& D, int e) 
 }
 
 // the sample and the Sim step of one live row (slot e) by its SAMPLE_L lanes (sub = lane of the
-// row's aligned group, every lane of the group active); lg = the row's actor outputs in LDS
+// row's aligned group, every lane of the group active); lg = the row's actor outputs in LDS.
+// keep_boot: a truncation-bootstrap row (alive 2) keeps alive = 2 (the next k_env_feedback clears it)
+// — the row-resident step, whose workgroups rank the live rows while others already sample
 __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e, int sub, const float* lg,
-                                           const SampleIn& in) {
+                                           const SampleIn& in, bool keep_boot = false) {
   const XtrlRngState& R = in.R;
   const int al = in.al;
   const uint32_t ep = in.ep;
@@ -634,7 +636,7 @@ __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e
   tw = __shfl(tw, base + 2, 64);
   if (sub != 0) return;
   if (al == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
-    D.alive[e] = 0;
+    if (!keep_boot) D.alive[e] = 0;
     return;
   }
   int a = 0;
@@ -754,7 +756,13 @@ __global__ __launch_bounds__(256) void k_heads_sample(const DGemmArgs a, const X
 __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
                                const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D.E || D.alive[e] != 1) return;
+  if (e >= D.E) return;
+  const uint8_t al = D.alive[e];
+  if (al == 2) {   // its bootstrap step ran (the row-resident step leaves the flag to this kernel)
+    D.alive[e] = 0;
+    return;
+  }
+  if (al != 1) return;
   const bool term = terminated[e] != 0, trunc = truncated && truncated[e] != 0;
   D.traj_rewards[(int64_t)e * D.Tmax + t] = reward[e];
   D.traj_bounds[(int64_t)e * D.Tmax + t] = term ? 1 : 0;
@@ -894,6 +902,7 @@ int check_desc(const XtrlDecodeDesc* D) {
   const int I = D->H * D->dh;
   XTRL_REQUIRE(D->n_qkv == 3 * I + (D->gate_values ? I : 0) + ((D->value_residual && D->learned_mix) ? D->H : 0),
                "decode: n_qkv mismatch");
+  XTRL_REQUIRE(!D->ff_glu || (D->hglu && D->hff), "decode: ff_glu needs hglu");
   return XTRL_OK;
 }
 
@@ -982,8 +991,31 @@ struct FrMlp {
   float eps = 1e-5f;
 };
 
-template <int NT2, int MT>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
-__global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
+// a weight fragment as its three bf16 piece fragments: WR = 3 (the split image, as loaded) or WR = 2
+// (the fp32 image: 8 consecutive k of the lane's column, split here exactly as xtrl_dgemm_pack_x6 does)
+template <int WR>
+__device__ __forceinline__ void frag_pieces(const uint4 (&w)[WR], uint4 (&b)[3]) {
+  if constexpr (WR == 3) {
+    b[0] = w[0]; b[1] = w[1]; b[2] = w[2];
+  } else {
+    const float4 u = __builtin_bit_cast(float4, w[0]), v = __builtin_bit_cast(float4, w[1]);
+    uint32_t h[4], m[4], l[4];
+    split3_pair(u.x, u.y, h[0], m[0], l[0]);
+    split3_pair(u.z, u.w, h[1], m[1], l[1]);
+    split3_pair(v.x, v.y, h[2], m[2], l[2]);
+    split3_pair(v.z, v.w, h[3], m[3], l[3]);
+    b[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    b[1] = make_uint4(m[0], m[1], m[2], m[3]);
+    b[2] = make_uint4(l[0], l[1], l[2], l[3]);
+  }
+}
+
+// FI: the weights come from the fp32 fragment images (Ly.w_ff1f / w_ff2f: 2/3 of the split images'
+// bytes, the split done per fragment before its MFMAs) instead of the split images.  EW (FI only):
+// the W2 fragments are loaded in the same batch as W1 (one weight round trip instead of two; 256
+// registers of weights: one workgroup per SIMD set)
+template <int NT2, int MT, bool FI, bool EW = false>   // d = 64 NT2 (d <= 256): output columns per wave 16 NT2; panel rows 16 MT
+__global__ __launch_bounds__(256, EW ? 1 : 2) void k_mlp(const XtrlDecodeDesc D, const XtrlDecodeLayer Ly, int t, const float* xin,
                                              const float* res, float* C, int ldc, const float* g_next, float* Y,
                                              int ldy, const FrMlp fm) {
   constexpr int d = 64 * NT2, NT1 = MLP_HW / 64, BM = 16 * MT;
@@ -1004,9 +1036,10 @@ __global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const Xt
     for (int r = w; r < BM; r += 4)
       __builtin_amdgcn_global_load_lds((const void*)(xin + (int64_t)min(m0 + r, M - 1) * d + 4 * lane),
                                        (lds_void*)(A1 + r * LDA), 16, 0, 0);
-  const uint4* w1 = reinterpret_cast<const uint4*>(Ly.w_ff1x);
+  constexpr int WR = FI ? 2 : 3;   // 16-byte registers per weight fragment
+  const uint4* w1 = reinterpret_cast<const uint4*>(FI ? (const void*)Ly.w_ff1f : (const void*)Ly.w_ff1x);
   const int64_t P1 = (int64_t)D.ff / 16 * JS1 * 64;   // slots per piece plane
-  uint4 bw[NT1][JS1][3];
+  uint4 bw[NT1][JS1][WR];
   float b1v[NT1];
 #pragma unroll
   for (int nt = 0; nt < NT1; ++nt) {
@@ -1015,9 +1048,25 @@ __global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const Xt
 #pragma unroll
     for (int s = 0; s < JS1; ++s)
 #pragma unroll
-      for (int pc = 0; pc < 3; ++pc) bw[nt][s][pc] = wp[pc * P1 + 64 * s];
+      for (int pc = 0; pc < WR; ++pc) bw[nt][s][pc] = wp[pc * P1 + 64 * s];
     b1v[nt] = Ly.b_ff1[t16 * 16 + lr];
   }
+  // this wave's W2 fragments: tiles w NT2 + nt, k steps of chunk c (EW: in this batch; else issued
+  // after FF1: with the first batch they would double the registers)
+  const uint4* w2 = reinterpret_cast<const uint4*>(FI ? (const void*)Ly.w_ff2f : (const void*)Ly.w_ff2x);
+  const int64_t P2 = (int64_t)(d / 16) * JS2 * 64;
+  uint4 b2w[NT2][JSC][WR];
+  auto load_w2 = [&]() {
+#pragma unroll
+    for (int nt = 0; nt < NT2; ++nt) {
+      const uint4* wp = w2 + ((int64_t)(w * NT2 + nt) * JS2 + c * JSC) * 64 + lane;
+#pragma unroll
+      for (int s = 0; s < JSC; ++s)
+#pragma unroll
+        for (int pc = 0; pc < WR; ++pc) b2w[nt][s][pc] = wp[pc * P2 + 64 * s];
+    }
+  };
+  if constexpr (EW) load_w2();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // ---- FF1 chunk + GELU -> Hs
@@ -1035,7 +1084,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const Xt
         bf16x8 a[3];
         split3x8(*reinterpret_cast<const f32x4v*>(ap), *reinterpret_cast<const f32x4v*>(ap + 4), a[0], a[1], a[2]);
 #pragma unroll
-        for (int nt = 0; nt < NT1; ++nt) acc[mt][nt][s & 1] = mfma_x6(a, bw[nt][s], acc[mt][nt][s & 1]);
+        for (int nt = 0; nt < NT1; ++nt) {
+          uint4 b[3];
+          frag_pieces<WR>(bw[nt][s], b);
+          acc[mt][nt][s & 1] = mfma_x6(a, b, acc[mt][nt][s & 1]);
+        }
       }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -1046,19 +1099,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const Xt
           Hs[(16 * mt + 4 * q + i) * LDH + w * 16 * NT1 + 16 * nt + lr] =
               geluf_((acc[mt][nt][0][i] + acc[mt][nt][1][i]) + b1v[nt]);
   }
-  // ---- this wave's W2 piece fragments: tiles w NT2 + nt, k steps of chunk c (issued after FF1:
-  //      with the first batch they would double the registers)
-  const uint4* w2 = reinterpret_cast<const uint4*>(Ly.w_ff2x);
-  const int64_t P2 = (int64_t)(d / 16) * JS2 * 64;
-  uint4 b2w[NT2][JSC][3];
-#pragma unroll
-  for (int nt = 0; nt < NT2; ++nt) {
-    const uint4* wp = w2 + ((int64_t)(w * NT2 + nt) * JS2 + c * JSC) * 64 + lane;
-#pragma unroll
-    for (int s = 0; s < JSC; ++s)
-#pragma unroll
-      for (int pc = 0; pc < 3; ++pc) b2w[nt][s][pc] = wp[pc * P2 + 64 * s];
-  }
+  if constexpr (!EW) load_w2();
   __syncthreads();   // (Hs complete)
   // ---- FF2 partial of the chunk -> sc1 stores
   {
@@ -1075,7 +1116,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp(const XtrlDecodeDesc D, const Xt
         bf16x8 a[3];
         split3x8(*reinterpret_cast<const f32x4v*>(ap), *reinterpret_cast<const f32x4v*>(ap + 4), a[0], a[1], a[2]);
 #pragma unroll
-        for (int nt = 0; nt < NT2; ++nt) acc[mt][nt][s & 1] = mfma_x6(a, b2w[nt][s], acc[mt][nt][s & 1]);
+        for (int nt = 0; nt < NT2; ++nt) {
+          uint4 b[3];
+          frag_pieces<WR>(b2w[nt][s], b);
+          acc[mt][nt][s & 1] = mfma_x6(a, b, acc[mt][nt][s & 1]);
+        }
       }
     float* part = D.mlp_part + ((int64_t)p * HC + c) * BM * d;
 #pragma unroll
@@ -1227,8 +1272,20 @@ int mlp_rows() {
   return r;
 }
 
+// XTRL_MLP_EW=1: the fp32-image feed-forward loads W1 and W2 in one batch (one workgroup per SIMD set)
+bool mlp_ew() {
+  static const bool on = [] {
+    const char* e = getenv("XTRL_MLP_EW");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
+
+// the one-launch feed-forward's weights: the fp32 fragment images (preferred) or the split images
+bool mlp_weights(const XtrlDecodeLayer& Ly) { return (Ly.w_ff1f && Ly.w_ff2f) || (Ly.w_ff1x && Ly.w_ff2x); }
+
 bool mlp_fused(const XtrlDecodeDesc* D, int l) {
-  return D->xn && D->mlp_part && D->mlp_cnt && D->layers[l].w_ff1x && D->layers[l].w_ff2x && attn_fused(D, l) &&
+  return !D->ff_glu && D->xn && D->mlp_part && D->mlp_cnt && mlp_weights(D->layers[l]) && attn_fused(D, l) &&
          D->d % 64 == 0 &&
          D->d <= 256 && D->ff % MLP_HW == 0;
 }
@@ -1242,11 +1299,16 @@ int launch_mlp_rows(const XtrlDecodeDesc* D, int l, int t, const float* xin, con
   const int bm = mlp_rows();
   const dim3 grid(D->ff / MLP_HW, (D->E + bm - 1) / bm);
   const XtrlDecodeLayer& Ly = D->layers[l];
+  const bool fi = Ly.w_ff1f && Ly.w_ff2f;
 #define XTRL_MLP(NT2)                                                                              \
   do {                                                                                             \
-    if (bm == 32)                                                                                  \
-      hipLaunchKernelGGL((k_mlp<NT2, 2>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
-    else hipLaunchKernelGGL((k_mlp<NT2, 1>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    if (bm == 32 && fi)                                                                            \
+      hipLaunchKernelGGL((k_mlp<NT2, 2, true>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    else if (bm == 32)                                                                             \
+      hipLaunchKernelGGL((k_mlp<NT2, 2, false>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    else if (fi && mlp_ew()) hipLaunchKernelGGL((k_mlp<NT2, 1, true, true>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    else if (fi) hipLaunchKernelGGL((k_mlp<NT2, 1, true>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
+    else hipLaunchKernelGGL((k_mlp<NT2, 1, false>), grid, dim3(256), 0, s, *D, Ly, t, xin, res, C, ldc, g, Y, ldy, fm); \
   } while (0)
   switch (D->d / 64) {
     case 1: XTRL_MLP(1); break;
@@ -1290,6 +1352,17 @@ int launch_attn_decode(const XtrlDecodeDesc* D, int l, int t, hipStream_t s, con
 }
 
 // one decode projection over the live rows of step t
+// ff_glu: hglu[r][j] = hff[r][j] * gelu(hff[r][ff + j]) over the step's live rows (x-transformers GLU;
+// the rollout runs the model in eval: no dropout)
+__global__ void k_glu_rows(const XtrlDecodeDesc D, int t) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ff = D.ff, M = D.live_count[t & 1];
+  if (i >= (int64_t)M * ff) return;
+  const int r = (int)(i / ff), j = (int)(i - (int64_t)r * ff);
+  const float* u = D.hff + (int64_t)r * 2 * ff;
+  D.hglu[(int64_t)r * ff + j] = u[j] * geluf_(u[ff + j]);
+}
+
 int dproj(const XtrlDecodeDesc* D, int t, const float* A, int lda, const float* W, int K, const float* bias,
           const float* gamma, int ln_k, const float* R, int ldr, float* C, int ldc, int N, int epi, hipStream_t s,
           const int32_t* row_map = nullptr, int n_split = 1 << 30, float* C2 = nullptr, int ldc2 = 0,
@@ -1652,9 +1725,16 @@ __host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
 }
 
 constexpr int ROW_MAX_L = 64;
+constexpr int ROW_G = 4;      // workgroups per row at most (the heads split across them)
+constexpr int ROW_CUS = 256;  // (rows x workgroups per row kept within one workgroup per CU)
 
+// G > 1: with few live rows, Ge = min(G, 256 / live) workgroups carry each row — every one runs the
+// row's embedding and layers (identical arithmetic; only the first stores the shared state), then
+// takes 4 d / Ge of the heads' hidden units and its partial of the last Linear; the partials meet
+// through k_mlp's hand-off (sc1 stores, one counter per row) and the last arriver sums them in
+// workgroup order, adds b2 and samples.  The heads are ~40 % of a row's weight bytes (C2).
 template <int DH>
-__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t) {
+__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t, int G) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_sh[EMB_MAX_E];
   __shared__ int wsum[ROW_T / 64];
@@ -1663,11 +1743,16 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   float *hs = lds + Lo.h, *ac = lds + Lo.ac, *part = lds + Lo.part, *lg = lds + Lo.lg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int S = D.S, d = D.d, H = D.H, I = H * DH, L = D.L;
-  // ---- compaction (as k_embed<CMP>): every workgroup ranks the live slots itself
+  // ---- compaction (as k_embed<CMP>): every workgroup ranks the live slots itself.  Workgroups that
+  //      start late (the grid need not be resident at once) may find rows that others have already
+  //      stepped: a Sim row ended at this step has alive 0 and lens t + 1 and still counts; a bootstrap
+  //      row keeps alive 2 through the launch (sample_row keep_boot) — so every workgroup ranks the
+  //      rows live at the step's start
   int n_live = 0;
   for (int c0 = 0; c0 < D.E; c0 += ROW_T) {
     const int e = c0 + tid;
-    const bool al = e < D.E && D.alive[e] != 0;
+    const int ec = min(e, D.E - 1);
+    const bool al = e < D.E && (D.alive[ec] != 0 || (D.sim_mode >= 0 && D.lens[ec] == t + 1));
     const uint64_t bal = __ballot(al);
     if (lane == 0) wsum[w] = __popcll(bal);
     __syncthreads();
@@ -1685,14 +1770,18 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
   const float scale = 1.0f / sqrtf((float)DH);
   constexpr int F4 = DH / 4, LPK = DH / 4, KPI = 64 / LPK;   // P.V: lanes per key row, key rows per wave pass
-  for (int r = blockIdx.x; r < n_live; r += gridDim.x) {
+  const int Ge = max(1, min(G, ROW_CUS / max(n_live, 1)));   // workgroups per row (uniform)
+  const int gs = blockIdx.x % Ge, nrw = (int)gridDim.x / Ge;
+  const bool lead = gs == 0;   // stores the row's shared state
+  __shared__ int last_sh;
+  for (int r = (int)blockIdx.x / Ge; r < n_live && (int)blockIdx.x < nrw * Ge; r += nrw) {
     const int e = rows_sh[r];
-    if (tid == 0) D.live_rows[(t & 1) * D.E + r] = e;
+    if (lead && tid == 0) D.live_rows[(t & 1) * D.E + r] = e;
     // ---- RSNorm of [state, prev reward], embeddings (k_embed's arithmetic and order)
     if (tid <= S) {
       const float xv = tid < S ? D.state[(int64_t)e * S + tid] : D.prev_reward[e];
       part[tid] = (xv - D.rs_mean[tid]) / fmaxf(sqrtf(D.rs_var[tid]), D.rs_eps);
-      if (tid < S) D.traj_states[((int64_t)e * D.Tmax + t) * S + tid] = xv;
+      if (lead && tid < S) D.traj_states[((int64_t)e * D.Tmax + t) * S + tid] = xv;
     }
     __syncthreads();
     if (tid < d) {
@@ -1733,7 +1822,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
           if (l == 0) {
             if (g == 0) {
               v1s[h * DH + c] = v;
-              D.v1[(int64_t)r * I + h * DH + c] = v;
+              if (lead) D.v1[(int64_t)r * I + h * DH + c] = v;
             }
           } else if (D.learned_mix) {
             v = lerpf_(v, v1s[h * DH + c], sigmoidf_(qkv[3 * I + (D.gate_values ? I : 0) + h]));
@@ -1749,8 +1838,10 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
         }
         const int64_t cb = ((int64_t)e * H + h) * D.Tmax * DH;
         if (g == 0) {
-          Ly.k_cache[cb + (int64_t)t * DH + c] = k;
-          Ly.v_cache[cb + (int64_t)t * DH + c] = v;
+          if (lead) {
+            Ly.k_cache[cb + (int64_t)t * DH + c] = k;
+            Ly.v_cache[cb + (int64_t)t * DH + c] = v;
+          }
           sc[round4i(D.Tmax) + c] = v;   // (the new value row, read by the P.V lanes below; q is broadcast
           att[h * DH + c] = q;           //  from LDS, its head's att slot is written only after the scores)
         }
@@ -1844,9 +1935,34 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
     }
     // ---- heads: [final LN(x) | state embed | latent] -> SiLU hidden -> block-diagonal last layer
     row_layernorm(xs, D.ln_final, d, ac);
-    row_gemv<2>(ac, D.in_dim, D.w_h1_t, 4 * d, D.b_h1, 4 * d, hs, part);
+    const int hw = 4 * d / Ge, hc0 = gs * hw;   // this workgroup's hidden units
+    row_gemv<2>(ac, D.in_dim, D.w_h1_t + hc0, 4 * d, D.b_h1 + hc0, hw, hs, part);
     float* out2 = part + ROW_PART;
-    row_gemv<0>(hs, 4 * d, D.w_h2_t, n2, D.b_h2, n2, out2, part);
+    row_gemv<0>(hs, hw, D.w_h2_t + (int64_t)hc0 * n2, n2, Ge == 1 ? D.b_h2 : nullptr, n2, out2, part);
+    if (Ge > 1) {   // the partials meet (k_mlp's hand-off); the last arriver sums them in order + b2
+      float* rp = D.row_part + (int64_t)r * ROW_G * n2;
+      for (int n = tid; n < n2; n += ROW_T)
+        __hip_atomic_store(rp + gs * n2 + n, out2[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        last_sh = __hip_atomic_fetch_add(D.row_cnt + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(Ge - 1);
+      __syncthreads();
+      if (!last_sh) continue;   // (workgroup-uniform)
+      for (int n = tid; n < n2; n += ROW_T) {
+        float pv[ROW_G];
+#pragma unroll
+        for (int g2 = 0; g2 < ROW_G; ++g2)
+          pv[g2] = __hip_atomic_load(rp + min(g2, Ge - 1) * n2 + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float v = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < ROW_G; ++g2)
+          if (g2 < Ge) v += pv[g2];
+        out2[n] = v + D.b_h2[n];
+      }
+      if (tid == 0) __hip_atomic_store(D.row_cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
     for (int n = tid; n < n_act + D.B; n += ROW_T) {
       if (n < n_act) {
         lg[n] = out2[n];
@@ -1858,14 +1974,14 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
     __syncthreads();
     if (tid < SAMPLE_L) {
       const SampleIn in = sample_load(D, e);
-      sample_row(D, t, e, tid, lg, in);
+      sample_row(D, t, e, tid, lg, in, true);
     }
     __syncthreads();
   }
 }
 
 bool row_ok(const XtrlDecodeDesc* D) {
-  if (!D->layers_dev || !D->w_h1_t || !D->w_h2_t || D->d > 256 || D->E > EMB_MAX_E || (D->continuous ? 2 * D->A : D->A) > 64 ||
+  if (D->ff_glu || !D->layers_dev || !D->w_h1_t || !D->w_h2_t || D->d > 256 || D->E > EMB_MAX_E || (D->continuous ? 2 * D->A : D->A) > 64 ||
       D->L > ROW_MAX_L)
     return false;
   for (int l = 0; l < D->L; ++l)
@@ -1903,10 +2019,18 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
       if ((rc = launch_mlp(D, l, t, s))) return rc;
       continue;
     }
-    if ((rc = dproj(D, t, xn_ff ? D->xn : D->x, d, Ly.w_ff1, d, Ly.b_ff1, xn_ff ? nullptr : Ly.ln_ff, xn_ff ? 0 : d,
-                    nullptr, 0, D->hff, ff, ff, EPI_GELU, s)))
+    if (D->ff_glu) {   // the GLU projection [2 ff], then value * gelu(gate)
+      if ((rc = dproj(D, t, xn_ff ? D->xn : D->x, d, Ly.w_ff1, d, Ly.b_ff1, xn_ff ? nullptr : Ly.ln_ff,
+                      xn_ff ? 0 : d, nullptr, 0, D->hff, 2 * ff, 2 * ff, EPI_NONE, s)))
+        return rc;
+      hipLaunchKernelGGL(k_glu_rows, dim3((unsigned)(((int64_t)D->E * ff + 255) / 256)), dim3(256), 0, s, *D, t);
+      XTRL_LAUNCHED("glu_rows");
+    } else if ((rc = dproj(D, t, xn_ff ? D->xn : D->x, d, Ly.w_ff1, d, Ly.b_ff1, xn_ff ? nullptr : Ly.ln_ff,
+                           xn_ff ? 0 : d, nullptr, 0, D->hff, ff, ff, EPI_GELU, s))) {
       return rc;
-    if ((rc = dproj(D, t, D->hff, ff, Ly.w_ff2, ff, Ly.b_ff2, nullptr, 0, D->x, d, last ? D->ac_in : D->x,
+    }
+    const float* h = D->ff_glu ? D->hglu : D->hff;
+    if ((rc = dproj(D, t, h, ff, Ly.w_ff2, ff, Ly.b_ff2, nullptr, 0, D->x, d, last ? D->ac_in : D->x,
                     last ? D->in_dim : d, d, EPI_NONE, s)))
       return rc;
   }
@@ -1921,11 +2045,17 @@ int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s
   XTRL_REQUIRE(row_ok(D), "decode rows: the row-resident step needs the k-major weights (w_*_t), d <= 256, "
                           "E <= %d, at most %d layers, layers_dev and its LDS within 96 KiB", EMB_MAX_E, ROW_MAX_L);
   XTRL_REQUIRE(max_rows > 0, "decode rows: max_rows %d", max_rows);
-  const dim3 grid(std::min(max_rows, D->E));
+  static const int g_env = [] {   // XTRL_ROW_G: workgroups per row at most (1, 2 or 4; default 4)
+    const char* e = getenv("XTRL_ROW_G");
+    const int v = e ? atoi(e) : ROW_G;
+    return (v == 1 || v == 2 || v == 4) ? v : ROW_G;
+  }();
+  const int G = (D->row_part && D->row_cnt && D->d % 4 == 0) ? g_env : 1;
+  const dim3 grid(std::min(max_rows, D->E) * G);
   const size_t lds = (size_t)row_lds(*D).tot * sizeof(float);
-  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, t);
-  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, t);
-  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, t);
+  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, t, G);
+  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, t, G);
+  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, t, G);
   XTRL_LAUNCHED("decode_row");
   return XTRL_OK;
 }
@@ -1969,7 +2099,7 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
     }
     // s3 = x2 + FF(x2): one launch (k_mlp, split-bf16 weight images) or the two projections
     const XtrlDecodeLayer& Ly = D->layers[l];
-    const bool mlp = D->mlp_part && D->mlp_cnt && Ly.w_ff1x && Ly.w_ff2x && d % 64 == 0 && d <= 256 &&
+    const bool mlp = D->mlp_part && D->mlp_cnt && mlp_weights(Ly) && d % 64 == 0 && d <= 256 &&
                      ff % MLP_HW == 0;
     // x3 = LN3(s3), its running mean, the next level's input: in the k_mlp tail, or a row kernel
     const float* le_next = l + 1 < Lv ? F->level[l + 1].level_emb : nullptr;

@@ -81,6 +81,23 @@ __global__ void k_dg_pack_x6(const float* W, int ldw, int N, int K, uint4* Wp) {
   Wp[2 * slots + s] = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// the same fragment order in fp32: plane h of slot s holds the lane's k0 + 4 h .. + 3
+__global__ void k_dg_pack_f8(const float* W, int ldw, int N, int K, float4* Wp) {
+  const int JS = K >> 5;
+  const int64_t slots = (int64_t)((N + 15) >> 4) * JS * 64;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= slots) return;
+  const int lane = (int)(s & 63);
+  const int64_t rest = s >> 6;
+  const int sk = (int)(rest % JS), t16 = (int)(rest / JS);
+  const int n = 16 * t16 + (lane & 15), k0 = 32 * sk + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = n < N ? W[(int64_t)n * ldw + k0 + i] : 0.f;
+  Wp[s] = make_float4(v[0], v[1], v[2], v[3]);
+  Wp[slots + s] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 template <int MT, int NT, int KS, int EPI, bool LN, bool RES>
 void launch_dg(const DGemmArgs& a, int rows, hipStream_t s) {
   constexpr int BM = 16 * MT, BN = 64 * NT / KS;
@@ -128,6 +145,18 @@ int dgemm_pack(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s) 
 }
 
 int64_t dgemm_packed_x6_elems(int N, int K) { return (int64_t)3 * ((N + 15) / 16) * 16 * K; }
+
+int64_t dgemm_packed_f8_floats(int N, int K) { return (int64_t)((N + 15) / 16) * 16 * K; }
+
+int dgemm_pack_f8(const float* W, int ldw, int N, int K, float* Wp, hipStream_t s) {
+  XTRL_REQUIRE(W && Wp && N > 0 && K > 0 && K % 32 == 0 && ldw >= K && ((uintptr_t)Wp & 15u) == 0,
+               "dgemm_pack_f8: bad arguments (K a multiple of 32, Wp 16-byte aligned)");
+  const int64_t slots = dgemm_packed_f8_floats(N, K) / 8;
+  hipLaunchKernelGGL(k_dg_pack_f8, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, s, W, ldw, N, K,
+                     reinterpret_cast<float4*>(Wp));
+  XTRL_LAUNCHED("dgemm_pack_f8");
+  return XTRL_OK;
+}
 
 int dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, hipStream_t s) {
   XTRL_REQUIRE(W && Wp && N > 0 && K > 0 && K % 32 == 0 && ldw >= K && ((uintptr_t)Wp & 15u) == 0,
@@ -177,6 +206,10 @@ extern "C" int xtrl_dgemm_pack(const float* W, int ldw, int N, int K, float* Wp,
   return xtrl::dgemm_pack(W, ldw, N, K, Wp, xtrl::as_stream(stream));
 }
 extern "C" int64_t xtrl_dgemm_packed_x6_elems(int N, int K) { return xtrl::dgemm_packed_x6_elems(N, K); }
+extern "C" int64_t xtrl_dgemm_packed_f8_floats(int N, int K) { return xtrl::dgemm_packed_f8_floats(N, K); }
+extern "C" int xtrl_dgemm_pack_f8(const float* W, int ldw, int N, int K, float* Wp, void* stream) {
+  return xtrl::dgemm_pack_f8(W, ldw, N, K, Wp, xtrl::as_stream(stream));
+}
 extern "C" int xtrl_dgemm_pack_x6(const float* W, int ldw, int N, int K, uint16_t* Wp, void* stream) {
   return xtrl::dgemm_pack_x6(W, ldw, N, K, Wp, xtrl::as_stream(stream));
 }

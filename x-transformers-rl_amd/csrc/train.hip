@@ -652,23 +652,77 @@ __global__ void k_copy_col(const float* src, int ld, float* dst, int lddst, int 
 
 // the FF dropout keep mask of the GELU_DROP epilogue (gemm.hip): word mode (one Philox block per
 // 4 rows of a column) or byte mode (thresh8 != 0: one block per 16 rows, see ff_block8)
-__global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint32_t thresh8, uint64_t seed,
-                          uint32_t off, uint32_t layer) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)M * N) return;
-  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+// the feed-forward dropout's keep bit of element (m, n) of the [T][ff] hidden (the FF1 epilogue's stream)
+__device__ __forceinline__ bool ff_keep(int m, int n, uint32_t thresh, uint32_t thresh8, uint64_t seed, uint32_t off,
+                                        uint32_t layer) {
   if (thresh8) {
     const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(((m >> 5) << 1) | ((m >> 2) & 1)), off,
                                     rng_c3(FIELD_FF_DROPOUT, 2 * layer + 1), seed);
     const int g = (m >> 3) & 3;
     const uint32_t w = g == 0 ? r.x : (g == 1 ? r.y : (g == 2 ? r.z : r.w));
-    mask[i] = (uint8_t)(((w >> (8 * (m & 3))) & 0xFFu) >= thresh8);
-    return;
+    return ((w >> (8 * (m & 3))) & 0xFFu) >= thresh8;
   }
+  if (thresh == 0) return true;
   const u32x4_t r = philox4x32_10((uint32_t)n, (uint32_t)(m >> 2), off, rng_c3(FIELD_FF_DROPOUT, 2 * layer), seed);
   const int q = m & 3;
   const uint32_t w = q == 0 ? r.x : (q == 1 ? r.y : (q == 2 ? r.z : r.w));
-  mask[i] = (uint8_t)(thresh == 0 || w >= thresh);
+  return w >= thresh;
+}
+
+__global__ void k_ff_mask(uint8_t* mask, int M, int N, uint32_t thresh, uint32_t thresh8, uint64_t seed,
+                          uint32_t off, uint32_t layer) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * N) return;
+  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  mask[i] = (uint8_t)ff_keep(m, n, thresh, thresh8, seed, off, layer);
+}
+
+// x-transformers GLU project-in (ff_glu) + the feed-forward dropout: u = [value | gate] [M][2 ff] (the
+// GLU projection's output), h[m][j] = drop(u[m][j] GELU(u[m][ff + j])) with the FF1 epilogue's keep
+// stream (torch's erf GELU); backward du = [dh~ GELU(g) | dh~ a GELU'(g)], dh~ = drop(dh).  One
+// thread per hidden element (HBM bound: 12 bytes read + 4 written forward, 16 + 8 backward)
+__device__ __forceinline__ float gelu_deriv_erf(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  return cdf + x * (0.39894228040143268f * expf(-0.5f * x * x));
+}
+__global__ void k_glu_fwd(const float* u, int ldu, float* h, int ldh, int M, int ff, uint32_t thresh, uint32_t thresh8,
+                          float inv_keep, uint64_t seed, uint32_t off, uint32_t layer) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * ff) return;
+  const int m = (int)(i / ff), j = (int)(i - (int64_t)m * ff);
+  const float a = u[(int64_t)m * ldu + j], g = u[(int64_t)m * ldu + ff + j];
+  const bool keep = ff_keep(m, j, thresh, thresh8, seed, off, layer);
+  h[(int64_t)m * ldh + j] = keep ? (a * geluf_(g)) * inv_keep : 0.f;
+}
+__global__ void k_glu_bwd(const float* dh, int lddh, const float* u, int ldu, float* du, int lddu, int M, int ff,
+                          uint32_t thresh, uint32_t thresh8, float inv_keep, uint64_t seed, uint32_t off,
+                          uint32_t layer) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * ff) return;
+  const int m = (int)(i / ff), j = (int)(i - (int64_t)m * ff);
+  const float a = u[(int64_t)m * ldu + j], g = u[(int64_t)m * ldu + ff + j];
+  const bool keep = ff_keep(m, j, thresh, thresh8, seed, off, layer);
+  const float dk = keep ? dh[(int64_t)m * lddh + j] * inv_keep : 0.f;
+  du[(int64_t)m * lddu + j] = dk * geluf_(g);
+  du[(int64_t)m * lddu + ff + j] = (dk * a) * gelu_deriv_erf(g);
+}
+
+int glu_fwd(const float* u, int ldu, float* h, int ldh, int M, int ff, float p, uint64_t seed, uint32_t off,
+            uint32_t layer, hipStream_t s) {
+  if ((int64_t)M * ff == 0) return XTRL_OK;
+  hipLaunchKernelGGL(k_glu_fwd, dim3((unsigned)(((int64_t)M * ff + 255) / 256)), dim3(256), 0, s, u, ldu, h, ldh, M, ff,
+                     dropout_thresh(p), dropout_thresh8(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed, off, layer);
+  XTRL_LAUNCHED("glu_fwd");
+  return XTRL_OK;
+}
+int glu_bwd(const float* dh, int lddh, const float* u, int ldu, float* du, int lddu, int M, int ff, float p,
+            uint64_t seed, uint32_t off, uint32_t layer, hipStream_t s) {
+  if ((int64_t)M * ff == 0) return XTRL_OK;
+  hipLaunchKernelGGL(k_glu_bwd, dim3((unsigned)(((int64_t)M * ff + 255) / 256)), dim3(256), 0, s, dh, lddh, u, ldu, du,
+                     lddu, M, ff, dropout_thresh(p), dropout_thresh8(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed, off,
+                     layer);
+  XTRL_LAUNCHED("glu_bwd");
+  return XTRL_OK;
 }
 
 // ---- fractal learn step (fractal_rl.py:116-136, 274-346 made causal; xtrl_amd/fractal.py) -------
@@ -1016,6 +1070,8 @@ int validate(const XtrlTrainDesc* D) {
   XTRL_REQUIRE(D->dh % 2 == 0 && D->rot_dim <= D->dh, "train: bad rotary dims");
   XTRL_REQUIRE(D->in_dim == D->d * (D->evolutionary ? 3 : 2), "train: in_dim mismatch");
   XTRL_REQUIRE(D->ld_ff == 0 || (D->ld_ff >= D->ff && D->ld_ff % 4 == 0), "train: ld_ff %d (ff %d)", D->ld_ff, D->ff);
+  XTRL_REQUIRE(!D->ff_glu || (D->ld_u2 >= 2 * D->ff && D->ld_u2 % 4 == 0 && D->glu_dh),
+               "train: ff_glu needs ld_u2 >= 2 ff (a multiple of 4) and glu_dh");
   XTRL_REQUIRE(!D->evolutionary || (D->latent && D->lat_e), "train: evolutionary needs latent buffers");
   XTRL_REQUIRE(D->S <= EMB_MAXS, "train: state_dim %d > %d unsupported", D->S, EMB_MAXS);
   XTRL_REQUIRE(D->continuous || D->A <= EMB_MAXA, "train: %d discrete actions > %d unsupported", D->A, EMB_MAXA);
@@ -1160,9 +1216,15 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
         return rc;
       if ((rc = ln_fwd(c, Ly.x_ff, c.P(Ly.ln_ff), Ly.xn_ff, d, nullptr, 0, Ly.st_ff))) return rc;
     }
-    if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, lf, T, ff, d, EPI_GELU_DROP, nullptr,
-                         Ly.u, lf, 1 << 30, 0, D->ff_offset, (uint32_t)li)))
+    if (D->ff_glu) {   // GLU projection [T][2 ff] into u, then drop(value * GELU(gate)) into hd
+      if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.u, D->ld_u2, T, 2 * ff, d, EPI_NONE)))
+        return rc;
+      if ((rc = glu_fwd(Ly.u, D->ld_u2, Ly.hd, lf, T, ff, D->dropout, D->seed, D->ff_offset, (uint32_t)li, s)))
+        return rc;
+    } else if ((rc = linear_fwd(c, Ly.xn_ff, d, c.P(Ly.w_ff1), c.P(Ly.b_ff1), Ly.hd, lf, T, ff, d, EPI_GELU_DROP,
+                                nullptr, Ly.u, lf, 1 << 30, 0, D->ff_offset, (uint32_t)li))) {
       return rc;
+    }
     float* x_out = li + 1 < D->L ? D->layers[li + 1].x_attn : D->x_final;
     if (fuse && li + 1 < D->L) {   // + the next block's attention pre-norm
       const XtrlTrainLayer& Ln = D->layers[li + 1];
@@ -1277,7 +1339,9 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   const int64_t Td = (int64_t)T * d;
   auto Gx = [&](int slot) { return per ? D->dx + slot * Td : D->dx; };
   auto Gx2 = [&](int li) { return per ? D->dx2 + li * Td : D->dx2; };
-  auto Gff = [&](int li) { return per ? D->dff + (int64_t)li * T * lf : D->dff; };
+  // dff: the FF1 output gradient [T][ld_f1] (GLU: the projection's [T][2 ff] on the ld_u2 stride)
+  const int f1 = D->ff_glu ? 2 * ff : ff, ld_f1 = D->ff_glu ? D->ld_u2 : lf;
+  auto Gff = [&](int li) { return per ? D->dff + (int64_t)li * T * ld_f1 : D->dff; };
   auto Gpr = [&](int li) { return per ? D->dproj + (int64_t)li * T * maxq : D->dproj; };
   auto wait = [&](hipEvent_t e) { return per ? XTRL_OK : F.wait(e); };
   hipEvent_t e_ff1 = nullptr, e_proj = nullptr, e_out_prev = nullptr;
@@ -1291,19 +1355,26 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     if ((rc = wgrad(cw, gout, d, Ly.hd, lf, c.G(Ly.w_ff2), T, d, ff, c.G(Ly.b_ff2)))) return rc;
     hipEvent_t e_ff2 = F.mark();
     if ((rc = wait(e_ff1))) return rc;
-    if ((rc = linear_dgrad(c, gout, d, c.P(Ly.w_ff2), dff, lf, T, d, ff, EPI_MUL_AUX, Ly.u, lf))) return rc;
+    if (D->ff_glu) {   // d hd, then the GLU backward into the projection gradient
+      if ((rc = linear_dgrad(c, gout, d, c.P(Ly.w_ff2), D->glu_dh, lf, T, d, ff, EPI_NONE))) return rc;
+      if ((rc = glu_bwd(D->glu_dh, lf, Ly.u, D->ld_u2, dff, ld_f1, T, ff, D->dropout, D->seed, D->ff_offset,
+                        (uint32_t)li, s)))
+        return rc;
+    } else if ((rc = linear_dgrad(c, gout, d, c.P(Ly.w_ff2), dff, lf, T, d, ff, EPI_MUL_AUX, Ly.u, lf))) {
+      return rc;
+    }
     if ((rc = F.fork())) return rc;
-    if ((rc = wgrad(cw, dff, lf, Ly.xn_ff, d, c.G(Ly.w_ff1), T, ff, d, c.G(Ly.b_ff1)))) return rc;
+    if ((rc = wgrad(cw, dff, ld_f1, Ly.xn_ff, d, c.G(Ly.w_ff1), T, f1, d, c.G(Ly.b_ff1)))) return rc;
     e_ff1 = F.mark();
     float* xg = D->dx;   // gradient w.r.t. the attention block's output
     if (fuse) {
       if ((rc = wait(e_out_prev))) return rc;   // the deeper block's out-projection weight gradient read dx2
-      if ((rc = dgrad_ln_bwd(c, dff, lf, c.P(Ly.w_ff1), ff, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), gout, Gx2(li),
+      if ((rc = dgrad_ln_bwd(c, dff, ld_f1, c.P(Ly.w_ff1), f1, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), gout, Gx2(li),
                              c.G(Ly.ln_ff), &csq)))
         return rc;
       xg = Gx2(li);
     } else {
-      if ((rc = linear_dgrad(c, dff, lf, c.P(Ly.w_ff1), D->dxn, d, T, ff, d, EPI_NONE))) return rc;
+      if ((rc = linear_dgrad(c, dff, ld_f1, c.P(Ly.w_ff1), D->dxn, d, T, f1, d, EPI_NONE))) return rc;
       if ((rc = F.wait(e_ff2))) return rc;
       if ((rc = ln_bwd(c, D->dxn, d, 1.f, nullptr, 0, Ly.x_ff, Ly.st_ff, c.P(Ly.ln_ff), D->dx, D->dx, c.G(Ly.ln_ff))))
         return rc;
@@ -1805,6 +1876,22 @@ extern "C" int xtrl_linear_gelu_drop(const float* X, int ldx, const float* W, co
   g.drop_thresh8 = xtrl::dropout_thresh8(p);
   g.inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
   return xtrl::gemm_run(g, 0, 0, xtrl::EPI_GELU_DROP, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_glu_drop_fwd(const float* u, int ldu, float* h, int ldh, int M, int ff, float p, uint64_t seed,
+                                 uint32_t offset, uint32_t layer, void* stream) {
+  XTRL_REQUIRE(layer < (1u << 22), "glu_drop_fwd: layer %u out of range", layer);
+  XTRL_REQUIRE(u && h && M >= 0 && ff > 0 && ldu >= 2 * ff && ldh >= ff && p >= 0.f && p < 1.f,
+               "glu_drop_fwd: bad arguments");
+  return xtrl::glu_fwd(u, ldu, h, ldh, M, ff, p, seed, offset, layer, xtrl::as_stream(stream));
+}
+
+extern "C" int xtrl_glu_drop_bwd(const float* dh, int lddh, const float* u, int ldu, float* du, int lddu, int M, int ff,
+                                 float p, uint64_t seed, uint32_t offset, uint32_t layer, void* stream) {
+  XTRL_REQUIRE(layer < (1u << 22), "glu_drop_bwd: layer %u out of range", layer);
+  XTRL_REQUIRE(dh && u && du && M >= 0 && ff > 0 && lddh >= ff && ldu >= 2 * ff && lddu >= 2 * ff && p >= 0.f && p < 1.f,
+               "glu_drop_bwd: bad arguments");
+  return xtrl::glu_bwd(dh, lddh, u, ldu, du, lddu, M, ff, p, seed, offset, layer, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_ff_dropout_mask(uint8_t* mask, int M, int N, float p, uint64_t seed, uint32_t offset,

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -28,7 +28,8 @@ LOSS_TOK, LOSS_STATS = 30, 32
 
 class DecodeLayer(C.Structure):
     _fields_ = [(n, P) for n in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1', 'b_ff1', 'w_ff2', 'b_ff2',
-                                 'k_cache', 'v_cache', 'w_out_t', 'w_ff1x', 'w_ff2x', 'w_qkv_t', 'w_ff1_t', 'w_ff2_t')]
+                                 'k_cache', 'v_cache', 'w_out_t', 'w_ff1x', 'w_ff2x', 'w_qkv_t', 'w_ff1_t', 'w_ff2_t',
+                                 'w_ff1f', 'w_ff2f')]
 
 
 class RngState(C.Structure):
@@ -52,7 +53,8 @@ class DecodeDesc(C.Structure):
                 + [('prof_events', C.POINTER(C.c_void_p))]
                 + [(n, P) for n in ('w_h1_t', 'w_h2_t')]
                 + [('layers_dev', C.POINTER(DecodeLayer))]
-                + [(n, P) for n in ('w_h1x', 'heads_part', 'heads_cnt')])
+                + [(n, P) for n in ('w_h1x', 'heads_part', 'heads_cnt', 'row_part', 'row_cnt')]
+                + [('ff_glu', I32), ('hglu', P)])
 
 
 class FractalLevel(C.Structure):
@@ -99,7 +101,7 @@ class TrainDesc(C.Structure):
                 + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer)),
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P),
                    ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32),
-                   ('scratch_per_layer', I32)])
+                   ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P)])
 
 
 class FractalTrainLevel(C.Structure):
@@ -147,6 +149,10 @@ SIGNATURES = {
     'xtrl_dgemm_packed_floats': (I64, [I32, I32]),
     'xtrl_dgemm_pack_x6': (I32, [P, I32, I32, I32, P, P]),
     'xtrl_dgemm_packed_x6_elems': (I64, [I32, I32]),
+    'xtrl_dgemm_pack_f8': (I32, [P, I32, I32, I32, P, P]),
+    'xtrl_glu_drop_fwd': (I32, [P, I32, P, I32, I32, I32, F32, U64, U32, U32, P]),
+    'xtrl_glu_drop_bwd': (I32, [P, I32, P, I32, P, I32, I32, I32, F32, U64, U32, U32, P]),
+    'xtrl_dgemm_packed_f8_floats': (I64, [I32, I32]),
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P, P, P]),
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),

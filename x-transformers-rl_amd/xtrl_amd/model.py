@@ -46,6 +46,7 @@ class ModelConfig:
     learned_mix: bool = False
     ff_mult: int = 4
     ff_no_bias: bool = False             # x-transformers FeedForward no_bias (world_model['ff_no_bias'])
+    ff_glu: bool = False                 # x-transformers FeedForward glu (world_model['ff_glu']): GELU-gated project-in
     rotary_abs_rollout: bool = False     # decision log: reference semantics = rotary position 0 in rollout
     hl_reduction_mean: bool = True       # decision log: hl-gauss-pytorch default reduction
     hl_sigma_ratio: float = 2.0
@@ -89,12 +90,21 @@ class XAttention(nn.Module):
             nn.init.zeros_(self.to_value_residual_mix[0].bias)
 
 
+class XGLU(nn.Module):
+    """x-transformers GLU (FeedForward glu = True): proj = Linear(dim, 2 inner) with a bias (value
+    rows, then gate rows), out = value * gelu(gate) — state_dict names ff.0.proj.*"""
+
+    def __init__(self, dim, inner):
+        super().__init__()
+        self.proj = nn.Linear(dim, 2 * inner)
+
+
 class XFeedForward(nn.Module):
     def __init__(self, c: ModelConfig):
         super().__init__()
         inner, bias = c.dim * c.ff_mult, not c.ff_no_bias
-        self.ff = nn.Sequential(nn.Sequential(nn.Linear(c.dim, inner, bias=bias), nn.GELU()), nn.Dropout(c.dropout),
-                                nn.Linear(inner, c.dim, bias=bias))
+        project_in = XGLU(c.dim, inner) if c.ff_glu else nn.Sequential(nn.Linear(c.dim, inner, bias=bias), nn.GELU())
+        self.ff = nn.Sequential(project_in, nn.Dropout(c.dropout), nn.Linear(inner, c.dim, bias=bias))
 
 
 class _Residual(nn.Module):
@@ -318,10 +328,13 @@ class WorldModelActorCritic(nn.Module):
                 o = o * gate_pre.sigmoid()
             x = self._lin(o, blk.to_out) + x
             (ln_f, _, _), ffb, _ = ff_l
-            f0 = ffb.ff[0][0]   # Linear + GELU + Dropout in one GEMM epilogue (the fused step's mask stream)
-            h = ops.linear_gelu_drop(ln_f(x), f0.weight, f0.bias, f0.weight.grad,
-                                     f0.bias.grad if f0.bias is not None else None, self._ws, p_drop,
-                                     attn_seed, ff_offset, li)
+            if c.ff_glu:   # GLU projection, then value * gelu(gate) + dropout (the fused step's mask stream)
+                h = ops.glu_drop(self._lin(ln_f(x), ffb.ff[0].proj), p_drop, attn_seed, ff_offset, li)
+            else:
+                f0 = ffb.ff[0][0]   # Linear + GELU + Dropout in one GEMM epilogue (the fused step's mask stream)
+                h = ops.linear_gelu_drop(ln_f(x), f0.weight, f0.bias, f0.weight.grad,
+                                         f0.bias.grad if f0.bias is not None else None, self._ws, p_drop,
+                                         attn_seed, ff_offset, li)
             x = self._lin(h, ffb.ff[2]) + x
         embed = tr.attn_layers.final_norm(x)
         ewa = torch.cat((embed, self.embed_actions(next_actions)), dim=-1)

@@ -157,6 +157,42 @@ def linear_gelu_drop(x, w, b, wg, bg, ws, p, seed, offset, layer):
     return LinearGeluDropFn.apply(x, w, b, wg, bg, ws, p, seed, offset, layer)
 
 
+class GluDropFn(torch.autograd.Function):
+    """x-transformers GLU project-in after its projection + the feed-forward dropout (world_model
+    ['ff_glu']): u [.., 2 ff] = [value | gate] -> h = drop(value * gelu(gate)) [.., ff]; keep bits of the
+    xtrl_ff_dropout_mask / fused-step stream (xtrl_glu_drop_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, u, p, seed, offset, layer):
+        F2 = u.shape[-1]
+        assert F2 % 2 == 0
+        ff = F2 // 2
+        u2 = _f32c(u.reshape(-1, F2).contiguous())
+        M = u2.shape[0]
+        h = torch.empty(M, ff, device=u.device, dtype=torch.float32)
+        args = (float(p), int(seed) & (2 ** 64 - 1), int(offset) & 0xFFFFFFFF, int(layer))
+        L.check(L.lib().xtrl_glu_drop_fwd(L.ptr(u2), F2, L.ptr(h), ff, M, ff, *args, L.stream()), 'glu_drop_fwd')
+        ctx.save_for_backward(u2)
+        ctx.extra = (args, u.shape)
+        return h.view(*u.shape[:-1], ff)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (u2,) = ctx.saved_tensors
+        args, ushape = ctx.extra
+        M, F2 = u2.shape
+        ff = F2 // 2
+        dh2 = dh.reshape(-1, ff).contiguous()
+        du = torch.empty(M, F2, device=dh.device, dtype=torch.float32)
+        L.check(L.lib().xtrl_glu_drop_bwd(L.ptr(dh2), ff, L.ptr(u2), F2, L.ptr(du), F2, M, ff, *args, L.stream()),
+                'glu_drop_bwd')
+        return du.view(ushape), None, None, None, None
+
+
+def glu_drop(u, p, seed, offset, layer):
+    return GluDropFn.apply(u, p, seed, offset, layer)
+
+
 def layernorm(x, gamma, out=None):
     lib = L.lib()
     M, D = x.shape

@@ -63,11 +63,14 @@ class RolloutEngine:
                          bounds=z(E, Tmax, dt=u8), values=z(E, Tmax, B))
         # scratch
         self.x, self.qkv, self.att = z(E, d), z(E, self.n_qkv), z(E, I)
-        self.hff, self.ac_in, self.logits, self.v1 = z(E, max(ff, 4 * d)), z(E, c.in_dim), z(E, nA), z(E, I)
+        glu = bool(getattr(c, 'ff_glu', False))   # world_model['ff_glu']: FF1 is the GLU projection [2 ff][d]
+        self.hff, self.ac_in, self.logits, self.v1 = z(E, max(2 * ff if glu else ff, 4 * d)), z(E, c.in_dim), \
+            z(E, nA), z(E, I)
+        self.hglu = z(E, ff) if glu else None
         self.xn = z(E, d)
         # one-launch feed-forward (k_mlp): per 16-row panel, one FF2 partial per 128-wide hidden chunk
         # and the panel's arrival counter (the last chunk workgroup sums the partials and resets it)
-        n_chunk = ff // 128 if (ff % 128 == 0 and d % 64 == 0 and d <= 256) else 0
+        n_chunk = ff // 128 if (ff % 128 == 0 and d % 64 == 0 and d <= 256 and not glu) else 0
         self.mlp_part = z(((E + 31) // 32) * 32 * n_chunk * d) if n_chunk else None   # (16- or 32-row panels)
         self.mlp_cnt = z((E + 15) // 16, dt=i32) if n_chunk else None
         self.kv = [(z(E, H, Tmax, dh), z(E, H, Tmax, dh)) for _ in range(c.depth)]
@@ -81,8 +84,11 @@ class RolloutEngine:
         # row-resident step (xtrl_decode_step_rows, which also reads the k-major hidden layer)
         self.w['w_h2_t'] = z(4 * d, _r4(nA + B))
         self.rows_max = self._rows_max(c)
+        self.row_part = self.row_cnt = None
         if self.rows_max:
             self.w['w_h1_t'] = z(c.in_dim, 4 * d)
+            # its heads split over up to 4 workgroups per row: partial outputs and one counter per row
+            self.row_part, self.row_cnt = z(E * 4 * _r4(nA + B)), z(E, dt=i32)
         # the one-launch heads (k_heads_mlp): split-bf16 image of the hidden layer, per 16-row panel one
         # partial output row block per 64-wide hidden chunk and an arrival counter
         if c.in_dim % 64 == 0 and d % 32 == 0:
@@ -105,17 +111,32 @@ class RolloutEngine:
         c = self.c
         d, I, ff = c.dim, c.inner, c.dim * c.ff_mult
         # w_out_t: to_out transposed for the attention kernel's fused out-projection
+        f1 = 2 * ff if getattr(c, 'ff_glu', False) else ff   # (ff_glu: the GLU projection's value | gate rows)
         self.wl = [dict(ln_attn=z(d), w_qkv=z(self.n_qkv, d), b_qkv=z(_r4(self.n_qkv)), w_out=z(d, I), w_out_t=z(I, d),
-                        ln_ff=z(d), w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
+                        ln_ff=z(d), w_ff1=z(f1, d), b_ff1=z(f1), w_ff2=z(d, ff), b_ff2=z(d)) for _ in range(c.depth)]
         if self.rows_max:   # k-major copies for the row-resident step
             for wl in self.wl:
                 wl.update(w_qkv_t=z(d, _r4(self.n_qkv)), w_ff1_t=z(d, ff), w_ff2_t=z(ff, d))
-        # w_ff1x / w_ff2x: split-bf16 images of FF1 / FF2 for the one-launch feed-forward kernel
-        if ff % 128 == 0 and d % 64 == 0 and d <= 256:
-            n1, n2 = (int(L.lib().xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
+        self._alloc_ff_images(z)
+        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
+
+    def _alloc_ff_images(self, z):
+        """FF1 / FF2 fragment images of the one-launch feed-forward kernel: fp32 (w_ff1f / w_ff2f,
+        xtrl_dgemm_pack_f8; the kernel splits the fragments) or, XTRL_MLP_IMG=x6, the pre-split bf16
+        images (w_ff1x / w_ff2x, xtrl_dgemm_pack_x6: 1.5x the bytes)."""
+        c = self.c
+        d, ff = c.dim, c.dim * c.ff_mult
+        if not (ff % 128 == 0 and d % 64 == 0 and d <= 256) or getattr(c, 'ff_glu', False):
+            return
+        lib = L.lib()
+        if os.environ.get('XTRL_MLP_IMG', 'f32') == 'x6':
+            n1, n2 = (int(lib.xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
             for wl in self.wl:
                 wl['w_ff1x'], wl['w_ff2x'] = z(n1, dt=torch.int16), z(n2, dt=torch.int16)
-        self._pk_src += [(wl, k) for wl in self.wl for k in ('w_qkv', 'w_out', 'w_ff1', 'w_ff2')]
+        else:
+            n1, n2 = (int(lib.xtrl_dgemm_packed_f8_floats(*s)) for s in ((ff, d), (d, ff)))
+            for wl in self.wl:
+                wl['w_ff1f'], wl['w_ff2f'] = z(n1), z(n2)
 
     def _wv(self, src, k):
         """The tensor the descriptor points at for weight k of src: its packed image if it has one."""
@@ -131,7 +152,7 @@ class RolloutEngine:
             layers[i] = L.DecodeLayer(*(self._wv(w, k) for k in ('ln_attn', 'w_qkv', 'b_qkv', 'w_out', 'ln_ff', 'w_ff1',
                                                                  'b_ff1', 'w_ff2', 'b_ff2')), rows(kc), rows(vc),
                                       self._wv(w, 'w_out_t'), self._wv(w, 'w_ff1x'), self._wv(w, 'w_ff2x'),
-                                      *(self._wv(w, k) for k in ('w_qkv_t', 'w_ff1_t', 'w_ff2_t')))
+                                      *(self._wv(w, k) for k in ('w_qkv_t', 'w_ff1_t', 'w_ff2_t', 'w_ff1f', 'w_ff2f')))
         D = L.DecodeDesc()
         D.E, D.S, D.A, D.B, D.d, D.L, D.H, D.dh, D.Tmax = (Eg, c.state_dim, c.num_actions, c.num_bins, c.dim,
                                                            c.depth, c.heads, c.dim_head, self.T)
@@ -159,8 +180,9 @@ class RolloutEngine:
         for k in ('states', 'actions', 'actions_f', 'logp', 'rewards', 'bounds', 'values'):
             setattr(D, 'traj_' + k, rows(self.traj[k]))
         for k in ('x', 'qkv', 'att', 'hff', 'ac_in', 'logits', 'v1', 'xn', 'live_rows', 'live_count', 'lat_embed',
-                  'mlp_part', 'mlp_cnt', 'heads_part', 'heads_cnt'):
+                  'mlp_part', 'mlp_cnt', 'heads_part', 'heads_cnt', 'row_part', 'row_cnt', 'hglu'):
             setattr(D, k, rows(getattr(self, k)))
+        D.ff_glu = int(self.hglu is not None)
         if os.environ.get('XTRL_DECODE_MLP', '1') == '0':   # A/B switch: the two-GEMM feed-forward
             D.mlp_part = None
         if os.environ.get('XTRL_DECODE_HEADS', '0') == '0':   # A/B switch: the one-launch heads (opt-in)
@@ -201,10 +223,12 @@ class RolloutEngine:
             wl['w_out'].copy_(blk.to_out.weight)
             wl['w_out_t'].copy_(blk.to_out.weight.t())
             wl['ln_ff'].copy_(ln_f.gamma)
-            wl['w_ff1'].copy_(ffb.ff[0][0].weight)
+            f0 = ffb.ff[0].proj if c.ff_glu else ffb.ff[0][0]   # (ff_glu: the GLU projection)
+            wl['w_ff1'].copy_(f0.weight)
             wl['w_ff2'].copy_(ffb.ff[2].weight)
-            if ffb.ff[0][0].bias is not None:   # (ff_no_bias: the packed biases stay zero)
-                wl['b_ff1'].copy_(ffb.ff[0][0].bias)
+            if f0.bias is not None:   # (ff_no_bias: the packed biases stay zero)
+                wl['b_ff1'].copy_(f0.bias)
+            if ffb.ff[2].bias is not None:
                 wl['b_ff2'].copy_(ffb.ff[2].bias)
         self._pack_gemm_weights()
 
@@ -257,6 +281,11 @@ class RolloutEngine:
                     t = wl[src]
                     L.check(lib.xtrl_dgemm_pack_x6(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(wl[dst]),
                                                    L.stream()), f'dgemm_pack_x6({src})')
+            for src, dst in (('w_ff1', 'w_ff1f'), ('w_ff2', 'w_ff2f')):
+                if dst in wl:
+                    t = wl[src]
+                    L.check(lib.xtrl_dgemm_pack_f8(L.ptr(t), t.shape[1], t.shape[0], t.shape[1], L.ptr(wl[dst]),
+                                                   L.stream()), f'dgemm_pack_f8({src})')
 
     # ------------------------------------------------------------------------------------------
     def _begin(self, seed, update, slot_offset, episode_of_slot, latent, slots=None):
@@ -285,7 +314,8 @@ class RolloutEngine:
         if not self.ROWS or os.environ.get('XTRL_DECODE_ROWS', '1') == '0':
             return 0
         nA = 2 * c.num_actions if c.continuous else c.num_actions
-        if c.dim > 128 or c.depth > 8 or nA > 64 or self.E > 8192 or (c.dim * c.ff_mult) % 4:
+        if (c.dim > 128 or c.depth > 8 or nA > 64 or self.E > 8192 or (c.dim * c.ff_mult) % 4
+                or getattr(c, 'ff_glu', False)):
             return 0
         r4 = lambda x: (x + 3) & ~3
         d, I, ff = c.dim, c.heads * c.dim_head, c.dim * c.ff_mult   # decode.hip row_lds (in_dim <= 3 d)
@@ -481,10 +511,7 @@ class FractalRolloutEngine(RolloutEngine):
                         ln2_w=z(d), ln2_b=z(d),
                         w_ff1=z(ff, d), b_ff1=z(ff), w_ff2=z(d, ff), b_ff2=z(d), ln3_w=z(d), ln3_b=z(d),
                         w_pg=z(2 * d, d), b_pg=z(2 * d), level_emb=z(d), sums=z(E, d)) for _ in range(Lv)]
-        if ff % 128 == 0 and d % 64 == 0 and d <= 256:   # split-bf16 images for the one-launch feed-forward
-            n1, n2 = (int(L.lib().xtrl_dgemm_packed_x6_elems(*s)) for s in ((ff, d), (d, ff)))
-            for wl in self.wl:
-                wl['w_ff1x'], wl['w_ff2x'] = z(n1, dt=torch.int16), z(n2, dt=torch.int16)
+        self._alloc_ff_images(z)   # fragment images for the one-launch feed-forward
         self.fbuf = dict(g=z(E, 2 * d), c2=z(E, d), tmp=z(E, d), x2=z(E, d), mean=z(E, d), allf=z(E, (Lv + 1) * d),
                          hagg=z(E, 2 * d))
         self._pk_src += [(self.w, k) for k in ('w_fa0', 'w_fa2')]

@@ -76,6 +76,9 @@ class FusedTrainStep:
 
         self.layers_py = []
         self.ld_ff = lff = ld_ff(ff)
+        glu = bool(getattr(c, 'ff_glu', False))
+        # ff_glu: u holds the GLU projection's output [T][2 ff] (stride lu2), dff its gradient planes
+        lu2 = ld_ff(2 * ff) if glu else lff
         layers = (L.TrainLayer * L_)()
         X = [E(T, d) for _ in range(L_ + 1)]
         max_qkv = 0
@@ -90,7 +93,7 @@ class FusedTrainStep:
             n_qkv = 3 * I + (I if c.gate_values else 0) + (H if mix else 0)
             max_qkv = max(max_qkv, n_qkv)
             bufs = dict(x_attn=X[li], x_ff=E(T, d), xn_attn=E(T, d), xn_ff=E(T, d), st_attn=E(T, 2), st_ff=E(T, 2),
-                        proj=E(T, n_qkv), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), u=E(T, lff),
+                        proj=E(T, n_qkv), qkv=E(T, 3 * I), o=E(T, I), lse=E(b_max * H * n_max), u=E(T, lu2),
                         hd=E(T, lff))
             bufs['og'] = E(T, I) if c.gate_values else bufs['o']
             self.layers_py.append(bufs)
@@ -98,7 +101,8 @@ class FusedTrainStep:
             Ly.ln_attn, Ly.w_proj = off(pa + '0.0.gamma'), span_off(wn)
             Ly.b_proj = span_off(bn) if bn else -1
             Ly.w_out, Ly.ln_ff = off(pa + '1.to_out.weight'), off(pf + '0.0.gamma')
-            Ly.w_ff1, Ly.b_ff1 = off(pf + '1.ff.0.0.weight'), off(pf + '1.ff.0.0.bias')
+            f1 = pf + ('1.ff.0.proj.' if glu else '1.ff.0.0.')
+            Ly.w_ff1, Ly.b_ff1 = off(f1 + 'weight'), off(f1 + 'bias')
             Ly.w_ff2, Ly.b_ff2 = off(pf + '1.ff.2.weight'), off(pf + '1.ff.2.bias')
             Ly.n_qkv, Ly.mix = n_qkv, int(mix)
             for k, t in bufs.items():
@@ -110,12 +114,14 @@ class FusedTrainStep:
                         hp=E(T, ldp), z1=E(T, 4 * d), h1=E(T, 4 * d), lat_e=E(max(b_max, 1), d),
                         raw=E(T, n_out), values=E(T, B), pred=E(T, 2 * (S + 1)), done=E(T),
                         d_raw=E(T, n_out), d_values=E(T, B), d_pred=E(T, 2 * (S + 1)), d_done=E(T),
-                        dx=E(L_ + 1, T, d), dx2=E(L_, T, d), dxn=E(T, d), dff=E(L_, T, lff), dproj=E(L_, T, max_qkv),
+                        dx=E(L_ + 1, T, d), dx2=E(L_, T, d), dxn=E(T, d), dff=E(L_, T, lu2), dproj=E(L_, T, max_qkv),
                         dog=E(T, I), dvfirst=E(T, I),
                         dz1=E(T, 4 * d), dac=E(T, c.in_dim), dzp=E(T, ldp), dewa=E(T, 2 * d),
                         delta=E(b_max * H * n_max))
         # the library states its own partial-sum needs (LayerNorm-backward row blocks, column sums)
-        part = max(256 * max(ff, 4 * d, B, max_qkv), 1024 * max(A, 1) * d,
+        if glu:
+            self.buf['glu_dh'] = E(T, lff)
+        part = max(256 * max((2 if glu else 1) * ff, 4 * d, B, max_qkv), 1024 * max(A, 1) * d,
                    int(L.lib().xtrl_train_part_floats(T, b_max, d, A)))
         self.buf['part'] = E(part)
         self.tok = torch.empty(b_max, n_max, L.LOSS_TOK, **f32)
@@ -139,6 +145,7 @@ class FusedTrainStep:
         D.layers = C.cast(layers, C.POINTER(L.TrainLayer))
         D.ld_ff = lff
         D.scratch_per_layer = 1   # per-layer backward planes (no mid-backward stream waits)
+        D.ff_glu, D.ld_u2 = int(glu), (lu2 if glu else 0)
         self.D = D
 
     # ------------------------------------------------------------------------------------------
