@@ -934,9 +934,16 @@ def test_fused_train_step_large_tiles_matches_autograd():
     _fused_vs_autograd(False, False, True, 0.25, 130, depth=2, episodes=96, batch=96, hazard=9, dim=128)
 
 
-def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, dim, fractal=None):
+@pytest.mark.gpu
+def test_ff_glu_fused_train_step_matches_autograd():
+    """ff_glu: the fused learn step (GLU projection GEMM + k_glu_fwd / k_glu_bwd) against the
+    reference-mode autograd step (xlinear + ops.glu_drop) with dropout on, at large-tile sizes."""
+    _fused_vs_autograd(False, True, True, 0.25, 70, depth=2, episodes=16, batch=16, hazard=6, dim=128, ff_glu=True)
+
+
+def _fused_vs_autograd(cont, evo, gates, p, T, depth, episodes, batch, hazard, dim, fractal=None, ff_glu=False):
     learner, env, _ = make_learner(depth=depth, gates=gates, evo=evo, cont=cont, T=T, episodes=episodes,
-                                   batch=batch, seed=9, hazard=hazard, dim=dim, fractal_levels=fractal)
+                                   batch=batch, seed=9, hazard=hazard, dim=dim, fractal_levels=fractal, ff_glu=ff_glu)
     agent = learner.agent
     agent.cfg.dropout = p
     agent.model.cfg.dropout = p

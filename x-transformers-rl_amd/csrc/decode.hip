@@ -1728,7 +1728,7 @@ constexpr int ROW_MAX_L = 64;
 constexpr int ROW_G = 4;      // workgroups per row at most (the heads split across them)
 constexpr int ROW_CUS = 256;  // (rows x workgroups per row kept within one workgroup per CU)
 
-// G > 1: with few live rows, Ge = min(G, 256 / live) workgroups carry each row — every one runs the
+// G > 1: with few live rows, Ge in {4, 2} (<= G, rows x Ge <= 256) workgroups carry each row — every one runs the
 // row's embedding and layers (identical arithmetic; only the first stores the shared state), then
 // takes 4 d / Ge of the heads' hidden units and its partial of the last Linear; the partials meet
 // through k_mlp's hand-off (sc1 stores, one counter per row) and the last arriver sums them in
@@ -1770,7 +1770,8 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
   const float scale = 1.0f / sqrtf((float)DH);
   constexpr int F4 = DH / 4, LPK = DH / 4, KPI = 64 / LPK;   // P.V: lanes per key row, key rows per wave pass
-  const int Ge = max(1, min(G, ROW_CUS / max(n_live, 1)));   // workgroups per row (uniform)
+  // workgroups per row (uniform): 4, 2 or 1 — a divisor of 4 d / 4 hidden units — with rows x Ge <= 256
+  const int Ge = min(G, n_live <= ROW_CUS / 4 ? 4 : (n_live <= ROW_CUS / 2 ? 2 : 1));
   const int gs = blockIdx.x % Ge, nrw = (int)gridDim.x / Ge;
   const bool lead = gs == 0;   // stores the row's shared state
   __shared__ int last_sh;
