@@ -352,34 +352,41 @@ def host_cores():
     return phys, share
 
 
-def cpu_baseline(cfg, seed, budget_s, threads=None, episodes=None):
-    """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn), one
-    update on a bounded number of episodes of the same workload."""
+def cpu_baseline(cfg, seed, budget_s, threads=None, episodes=None, reps=5):
+    """The oracle's batch-1 CPU restatement of the reference Learner (rollout + learn): ``reps``
+    updates (seeds seed .. seed + reps - 1) on a bounded number of episodes of the same workload,
+    the median rate reported (BASELINE.md's plan: the median of >= 5 updates)."""
     from oracle import ref_port as R
     threads = threads or int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     episodes = episodes or (32 if cfg.get('fractal') else 96 if cfg['T'] >= 100 else 512)
-    batch = min(8, episodes)
-    c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
-                        dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],
-                        learned_mix=cfg['gates'], evolutionary=False, max_timesteps=cfg['T'], batch_size=batch,
-                        num_episodes_per_update=episodes, sim_mode=cfg['mode'], hazard_log2=cfg['hazard_log2'],
-                        seed=seed, dropout=cfg['dropout'])
+    per = max(2, episodes // reps)   # episodes per update: the whole sample split over the reps
+    batch = min(8, per)
     factory = None
     if cfg.get('fractal'):
         from oracle import fractal_ref as FR
         factory = lambda mc: FR.OracleFractalPolicy(mc, cfg['fractal'])   # noqa: E731
-    oracle = R.OracleLearner(c, model_factory=factory)
-    t0 = time.perf_counter()
-    eps, fit = oracle.rollout(0)
-    t1 = time.perf_counter()
-    oracle.learn(eps, fit, 0)
-    t2 = time.perf_counter()
-    steps = sum(ep['len'] for ep in eps)
-    return dict(value=steps / (t2 - t0), unit='env-steps/s', cores=threads, kind='port',
-                sample=f'1 update, {episodes} episodes ({steps} env-steps), batch {batch}, same model/config, '
-                       f'rollout {t1 - t0:.1f}s + learn {t2 - t1:.1f}s (oracle/ref_port.OracleLearner, batch-1 '
-                       f'KV-cached decode like xtrl.py:1250-1341)')
+    rates, steps_all, t_roll, t_learn = [], 0, 0., 0.
+    for r in range(reps):
+        c = R.LearnerConfig(cfg['S'], cfg['A'], (-5., 5.), dim=cfg['dim'], depth=cfg['depth'], heads=cfg['heads'],
+                            dim_head=cfg['dim_head'], gate_values=cfg['gates'], value_residual=cfg['gates'],
+                            learned_mix=cfg['gates'], evolutionary=False, max_timesteps=cfg['T'], batch_size=batch,
+                            num_episodes_per_update=per, sim_mode=cfg['mode'], hazard_log2=cfg['hazard_log2'],
+                            seed=seed + r, dropout=cfg['dropout'])
+        oracle = R.OracleLearner(c, model_factory=factory)
+        t0 = time.perf_counter()
+        eps, fit = oracle.rollout(0)
+        t1 = time.perf_counter()
+        oracle.learn(eps, fit, 0)
+        t2 = time.perf_counter()
+        steps = sum(ep['len'] for ep in eps)
+        rates.append(steps / (t2 - t0))
+        steps_all, t_roll, t_learn = steps_all + steps, t_roll + (t1 - t0), t_learn + (t2 - t1)
+    return dict(value=float(np.median(rates)), unit='env-steps/s', cores=threads, kind='port',
+                rates=[round(x, 1) for x in rates],
+                sample=f'median of {reps} updates x {per} episodes ({steps_all} env-steps in all), batch {batch}, '
+                       f'same model/config, rollout {t_roll:.1f}s + learn {t_learn:.1f}s in all '
+                       f'(oracle/ref_port.OracleLearner, batch-1 KV-cached decode like xtrl.py:1250-1341)')
 
 
 def ppo_loss_delta(learner, env, cfg):
@@ -590,7 +597,7 @@ def main():
             cpu = cpu_baseline(cfg, args.seed, 20.)
             phys, share = host_cores()
             one = cpu_baseline(cfg, args.seed, 20., threads=1,
-                               episodes=8 if cfg.get('fractal') else 32 if cfg['T'] >= 100 else 128)
+                               episodes=8 if cfg.get('fractal') else 32 if cfg['T'] >= 100 else 128, reps=3)
             cpu.update(host_physical_cores=phys, host_cpu_share=share,
                        single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
