@@ -2,6 +2,7 @@
 
 Tolerances: integer / index / mask outputs bit-exact; fp32 outputs within 1e-4 relative (BASELINE
 north_star), tighter where the computation is short."""
+import contextlib
 import math
 
 import numpy as np
@@ -435,6 +436,39 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
     return learner, env, oracle
 
 
+@contextlib.contextmanager
+def _loss_kinks():
+    """While the oracle computes a minibatch loss: the smallest distance of a valid token to a kink of
+    the losses — the PPO ratio at 1 -/+ eps_clip (xtrl.py:413-444) and the clipped-value critic's
+    strict comparisons of v with the return and v_old -/+ value_clip (xtrl.py:446-477)."""
+    out = {'distance': float('inf')}
+    orig_a, orig_c = R.actor_loss, R.critic_loss
+
+    def actor(cfg, hl, raw, actions, old_lp, returns, old_values, mask):
+        lp = R.continuous_log_prob(raw, actions, cfg.squash) if cfg.continuous else R.discrete_log_prob(raw, actions)
+        r = (lp - old_lp).exp().detach()
+        m = mask.reshape(*mask.shape, *((1,) * (r.ndim - mask.ndim))).expand_as(r).bool()
+        d = torch.minimum((r - (1 - cfg.eps_clip)).abs(), (r - (1 + cfg.eps_clip)).abs())[m]
+        if d.numel():
+            out['distance'] = min(out['distance'], float(d.min()))
+            out['ratio'] = float(d.min())
+        return orig_a(cfg, hl, raw, actions, old_lp, returns, old_values, mask)
+
+    def critic(cfg, hl, values, returns, old_values):
+        v, v_old = hl(values).detach(), hl(old_values).detach()
+        d = torch.stack([(v - returns).abs(), (v - (v_old - cfg.value_clip)).abs(),
+                         (v - (v_old + cfg.value_clip)).abs()]).min(0).values
+        out['distance'] = min(out['distance'], float(d.min()))
+        out['value'] = float(d.min())
+        return orig_c(cfg, hl, values, returns, old_values)
+
+    R.actor_loss, R.critic_loss = actor, critic
+    try:
+        yield out
+    finally:
+        R.actor_loss, R.critic_loss = orig_a, orig_c
+
+
 def compare_rollout(traj, lens, episodes, cont=False, rows=None, prefix=None):
     """Device trajectory rows vs the oracle's episodes (rows[i] <-> episodes[i]; default row i).
     ``prefix``: the oracle ran at most ``prefix`` steps — compare the first min(len, prefix) steps."""
@@ -768,6 +802,7 @@ def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac, ff):
     agent = learner.agent
     c = oracle.c
     worst = [0.]
+    kinked = []
     for u in range(2):
         traj, lens, genes, cum = learner.rollout_device(env, u, 10)
         episodes, fitness = oracle.rollout(u)      # oracle rollout under its own (drifting) weights
@@ -795,21 +830,32 @@ def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac, ff):
                              egenes[idx], elens[idx])
             latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if evo else None
             keep = R.reward_coin(c.seed, u, epoch, mbi, c.reward_dropout)
-            ref_loss, _, _, _ = R.minibatch_loss(oracle.model, rs, mb, latent, c.weights, keep)
+            with _loss_kinks() as kinks:
+                ref_loss, _, _, _ = R.minibatch_loss(oracle.model, rs, mb, latent, c.weights, keep)
             ref_loss.backward()
             l_gpu, l_ref = float(loss.detach()), float(ref_loss.detach())
             assert abs(l_gpu - l_ref) <= 1e-4 * abs(l_ref) + 1e-6, (u, epoch, mbi, l_gpu, l_ref)
+            if kinks['distance'] < 1e-5:
+                # a token sits on a kink of the PPO / clipped-value loss (its gradient is one-sided there,
+                # and the two implementations' last-bit differences pick different sides): the loss is
+                # checked, the gradients are not
+                kinked.append((u, epoch, mbi, kinks))
+                return
             gpu_g = dict(zip(agent.flat.names, (p.grad.detach().cpu() for p in agent.flat.params)))
             scale = max(float(p.grad.abs().max()) for p in oracle.model.parameters() if p.grad is not None)
+            bad = []
             for name, p in oracle.model.named_parameters():
                 if p.grad is None:
                     continue
                 err = float((gpu_g[name] - p.grad).abs().max())
                 worst[0] = max(worst[0], err / scale)
-                assert err <= 1e-4 * scale + 1e-7, (name, err, scale)
+                if err > 1e-4 * scale + 1e-7:
+                    bad.append((name, err, float(p.grad.abs().max())))
+            assert not bad, (u, epoch, mbi, scale, sorted(bad, key=lambda x: -x[1])[:8], len(bad))
 
         agent.learn(traj, lens, genes, fit, update=u, probe=probe)
-    print(f'worst gradient error / gradient scale: {worst[0]:.2e}')
+    print(f'worst gradient error / gradient scale: {worst[0]:.2e}; minibatches on a loss kink: {kinked}')
+    assert len(kinked) <= 1, kinked
 
 
 @pytest.mark.parametrize('evo,gates,frac', [(False, False, None), (True, True, None), (False, False, 2),

@@ -1748,11 +1748,23 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   //      stepped: a Sim row ended at this step has alive 0 and lens t + 1 and still counts; a bootstrap
   //      row keeps alive 2 through the launch (sample_row keep_boot) — so every workgroup ranks the
   //      rows live at the step's start
+  // (every chunk's alive byte and length loaded in one batch, then ranked chunk by chunk)
   int n_live = 0;
-  for (int c0 = 0; c0 < D.E; c0 += ROW_T) {
+  constexpr int CH = EMB_MAX_E / ROW_T;
+  uint8_t alv[CH];
+  int lnv[CH];
+#pragma unroll
+  for (int ci = 0; ci < CH; ++ci) {
+    const int ec = min(ROW_T * ci + tid, D.E - 1);
+    alv[ci] = D.alive[ec];
+    lnv[ci] = D.lens[ec];
+  }
+#pragma unroll
+  for (int ci = 0; ci < CH; ++ci) {
+    const int c0 = ROW_T * ci;
+    if (c0 >= D.E) break;   // (uniform)
     const int e = c0 + tid;
-    const int ec = min(e, D.E - 1);
-    const bool al = e < D.E && (D.alive[ec] != 0 || (D.sim_mode >= 0 && D.lens[ec] == t + 1));
+    const bool al = e < D.E && (alv[ci] != 0 || (D.sim_mode >= 0 && lnv[ci] == t + 1));
     const uint64_t bal = __ballot(al);
     if (lane == 0) wsum[w] = __popcll(bal);
     __syncthreads();
@@ -1853,7 +1865,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
         wave_sync();
         const float4* q4 = reinterpret_cast<const float4*>(att + h * DH);
         // scores of the cached keys, one key per lane, NP 64-key passes in flight
-        constexpr int NP = DH == 16 ? 2 : 1;
+        constexpr int NP = DH == 16 ? 4 : (DH == 32 ? 2 : 1);   // (256 / 128 / 64 keys per round trip)
         float mx = kn;
         for (int j0 = 0; j0 < t; j0 += 64 * NP) {
           float4 kr[NP][F4];
@@ -1895,15 +1907,16 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
         // P.V: lane (kk = key in a pass, cq = channel quad), float4 value rows, 8 passes in flight
         const int kk = lane % KPI, cq = lane / KPI;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int j0 = 0; j0 < t; j0 += 8 * KPI) {
-          float4 vr[8];
+        constexpr int VB = 8;   // value rows in flight per lane (128 / 64 / 32 keys a pass; 16 spilled)
+        for (int j0 = 0; j0 < t; j0 += VB * KPI) {
+          float4 vr[VB];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < VB; ++u) {
             const int j = min(j0 + kk + KPI * u, t - 1);
             vr[u] = *reinterpret_cast<const float4*>(Ly.v_cache + cb + (int64_t)j * DH + 4 * cq);
           }
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < VB; ++u) {
             const int j = j0 + kk + KPI * u;
             const float p = j < t ? sc[j] : 0.f;
             acc.x += p * vr[u].x;
