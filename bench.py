@@ -477,8 +477,12 @@ def main():
     learner, env = build_learner(cfg, args.seed, use_graph=not args.no_graph, world=world)
     T = cfg['T']
 
-    for _ in range(args.warmup):
+    def progress(msg):   # stderr progress outside the timed region (long multi-rank runs stay visibly alive)
+        print(f'[bench rank {rank}] {msg}', file=sys.stderr, flush=True)
+
+    for i in range(args.warmup):
         one_update(learner, env, T)
+        progress(f'warmup update {i + 1}/{args.warmup}')
     host = bool(cfg.get('host'))
     # Roofline timers — HIP events around every decode-attention launch (inside the captured rollout
     # graph) and every weight-gradient GEMM launch of the learn step — run in a PROBED pass of
@@ -511,6 +515,7 @@ def main():
         gtimer.collect()
         gtimer.detach()
         timer.detach()
+        progress(f'probed pass: {n_probed} updates, {value_probed:.0f} env-steps/s')
         one_update(learner, env, T)    # re-capture the rollout graph without the event records
     if world > 1:
         dist.barrier()
@@ -528,6 +533,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    progress(f'timed: {args.steps} updates in {elapsed:.2f} s')
     lens_last = lens_last.cpu().numpy() if lens_last is not None else None
     el = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
     if world > 1:
