@@ -2059,10 +2059,14 @@ int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s
   XTRL_REQUIRE(row_ok(D), "decode rows: the row-resident step needs the k-major weights (w_*_t), d <= 256, "
                           "E <= %d, at most %d layers, layers_dev and its LDS within 96 KiB", EMB_MAX_E, ROW_MAX_L);
   XTRL_REQUIRE(max_rows > 0, "decode rows: max_rows %d", max_rows);
-  static const int g_env = [] {   // XTRL_ROW_G: workgroups per row at most (1, 2 or 4; default 4)
+  // XTRL_ROW_G: workgroups per row at most (1, 2 or 4; default 1 — on one box C2 rollout 30.8–31.7
+  // vs 31.3–31.5 ms and the host-env decode step 57.6 vs 74.1 us at 1 vs 4: the redundant layer work
+  // and the hand-off cost more than the split heads save; the step is bound by its ~20 dependent
+  // phases, not by its weight stream)
+  static const int g_env = [] {
     const char* e = getenv("XTRL_ROW_G");
-    const int v = e ? atoi(e) : ROW_G;
-    return (v == 1 || v == 2 || v == 4) ? v : ROW_G;
+    const int v = e ? atoi(e) : 1;
+    return (v == 1 || v == 2 || v == 4) ? v : 1;
   }();
   const int G = (D->row_part && D->row_cnt && D->d % 4 == 0) ? g_env : 1;
   const dim3 grid(std::min(max_rows, D->E) * G);
