@@ -1733,7 +1733,7 @@ constexpr int ROW_CUS = 256;  // (rows x workgroups per row kept within one work
 // takes 4 d / Ge of the heads' hidden units and its partial of the last Linear; the partials meet
 // through k_mlp's hand-off (sc1 stores, one counter per row) and the last arriver sums them in
 // workgroup order, adds b2 and samples.  The heads are ~40 % of a row's weight bytes (C2).
-template <int DH>
+template <int DH, int KP = (DH == 16 ? 2 : 1)>   // KP: 64-key K passes per round trip
 __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t, int G) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_sh[EMB_MAX_E];
@@ -1865,7 +1865,8 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
         wave_sync();
         const float4* q4 = reinterpret_cast<const float4*>(att + h * DH);
         // scores of the cached keys, one key per lane, NP 64-key passes in flight
-        constexpr int NP = DH == 16 ? 4 : (DH == 32 ? 2 : 1);   // (256 / 128 / 64 keys per round trip)
+        constexpr int NP = KP;   // (DH 16: 128 keys per round trip; 256 measured slower: C2 rollout
+                                 //  31.06-31.26 vs 30.80-30.92 ms, A/B x3)
         float mx = kn;
         for (int j0 = 0; j0 < t; j0 += 64 * NP) {
           float4 kr[NP][F4];
