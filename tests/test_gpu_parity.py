@@ -523,6 +523,29 @@ def test_rollout_matches_oracle(depth, gates, evo, decode_path):
         tol(learner.fitness(cum, torch.tensor([g for _, g in learner.episode_genes])), fitness, 1e-5, 1e-5)
 
 
+@pytest.mark.parametrize('variant', ['mlp_f32_images', 'heads_one_launch', 'two_gemm_ff'])
+def test_rollout_opt_in_decode_variants_match_oracle(variant, monkeypatch):
+    """The opt-in decode kernels against the oracle on the multi-kernel step (d = 128, EPO latents in
+    the heads' input: in_dim = 384): the one-launch feed-forward on fp32 fragment images
+    (XTRL_MLP_IMG=f32, split per fragment in the kernel), the one-launch heads (XTRL_DECODE_HEADS=1:
+    hidden layer + SiLU + last Linear + sampling, k_heads_mlp) and the two-GEMM feed-forward
+    (XTRL_DECODE_MLP=0)."""
+    monkeypatch.setenv('XTRL_DECODE_ROWS', '0')
+    monkeypatch.setenv({'mlp_f32_images': 'XTRL_MLP_IMG', 'heads_one_launch': 'XTRL_DECODE_HEADS',
+                        'two_gemm_ff': 'XTRL_DECODE_MLP'}[variant],
+                       {'mlp_f32_images': 'f32', 'heads_one_launch': '1', 'two_gemm_ff': '0'}[variant])
+    learner, env, oracle = make_learner(depth=2, gates=True, evo=True, dim=128, episodes=12)
+    eng = learner._engine_for(env, 12)
+    if variant == 'mlp_f32_images':
+        assert 'w_ff1f' in eng.wl[0] and 'w_ff1x' not in eng.wl[0]
+    if variant == 'heads_one_launch':
+        assert eng.desc.heads_part
+    traj, lens, _, cum = learner.rollout_device(env, 0, 12)
+    torch.cuda.synchronize()
+    episodes, fitness = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes)
+
+
 @pytest.mark.parametrize('ff', [4, 2])
 def test_rollout_d256_matches_oracle(ff):
     """The C3 width (d = 256, 4 x 16 heads; the decode embedding kernel's fused layer-0 pre-norm, the
