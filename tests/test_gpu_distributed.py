@@ -64,7 +64,6 @@ def _worker(rank, world, port, out_dir, mode):
                       LOCAL_RANK='0')
     if mode == 'c5grad':   # one collective per backward bucket (no coalescing of the small test buckets)
         os.environ['XTRL_DP_BUCKET_FLOATS'] = '1'
-        os.environ['XTRL_DP_BUCKETS'] = '1'   # (the buckets over gloo, where they are off by default)
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)

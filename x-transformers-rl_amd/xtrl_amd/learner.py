@@ -479,13 +479,9 @@ class Agent(nn.Module):
         self.step += 1
 
     def bucket_allreduce(self):
-        """The overlapped bucketed all-reduce of the fused learn step (None: one process, or one
-        all-reduce after the backward: XTRL_DP_BUCKETS=0, and by default over gloo — a gloo collective
-        blocks the host, so buckets only add per-call cost there: C5 layout 37.6 vs 12.8 ms a step,
-        tools/gloo_ar_probe.py; XTRL_DP_BUCKETS=1 forces the buckets, e.g. to test them over gloo)."""
-        mode = os.environ.get('XTRL_DP_BUCKETS', 'auto')
-        if not dist_.is_distributed() or mode == '0' \
-                or (mode != '1' and torch.distributed.get_backend() == 'gloo') \
+        """The overlapped bucketed all-reduce of the fused learn step (None: one process, or
+        XTRL_DP_BUCKETS=0 for one all-reduce after the backward)."""
+        if not dist_.is_distributed() or os.environ.get('XTRL_DP_BUCKETS', '1') == '0' \
                 or not hasattr(self.model, 'flat_bucket_ranges') or self.flat.flat.device.type != 'cuda':
             return None
         bar = getattr(self, '_bar', None)
