@@ -151,7 +151,8 @@ typedef struct XtrlDecodeDesc {
   int32_t* prev_action;    /* [E] (-1 at t = 0) */
   float* prev_action_f;    /* [E][A] continuous */
   float* prev_reward;      /* [E] */
-  uint8_t* alive;          /* [E] */
+  uint8_t* alive;          /* [E] 0 dead, 1 live, 2 bootstrap step pending, 3 + (t & 1) ended at step t by
+                              xtrl_decode_step_rows (dead from step t + 1 on) */
   int32_t* lens;           /* [E] episode length so far */
   double* cum_reward;      /* [E] cumulative reward (fitness, xtrl.py:1310, 1345-1346) */
   const int32_t* episode_of_slot;  /* [E] episode index keying the Sim stream */
@@ -226,8 +227,11 @@ int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream);
  * outputs to fp32 rounding): one workgroup carries a live row through compaction, embeddings, every
  * layer, the heads and the sampling + Sim step in ONE launch, min(max_rows, E) workgroups taking
  * live rows b, b + grid, ...  Needs the k-major weights (w_qkv_t / w_ff1_t / w_ff2_t, w_out_t,
- * w_h1_t / w_h2_t), d <= 256, E <= 8192, L <= 8, n_act <= 64 (the reference loop it replaces:
- * x_transformers_rl.py:1250-1341). */
+ * w_h1_t / w_h2_t), d <= 256, E <= 8192, L <= 64, n_act <= 64, layers_dev, its LDS within 96 KiB (the
+ * reference loop it replaces: x_transformers_rl.py:1250-1341).  Its GEMVs read whole float4 columns:
+ * b_qkv must hold round4(n_qkv) floats and b_h2 round4(n_act + B), the padding zero.  The step never
+ * turns a slot it ranks from live to dead: a Sim episode it ends reads alive = 3 + (t & 1) until the
+ * next step's compaction clears it to 0 (every compaction treats 3 + (t & 1) as live at step t only). */
 int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void* stream);
 /* Host env results of step t (xtrl.py:1297-1336) for the live rows: next_state [E][S], reward [E],
  * terminated [E] (stored as is_boundary), truncated [E] or NULL.  An episode ends when terminated,

@@ -582,6 +582,39 @@ def test_rollout_graph_replay_equals_eager(dim, decode_path):
         assert torch.equal(v, traj[k]), k
 
 
+def test_row_step_oversubscribed_grid_matches_multi_kernel_and_oracle(monkeypatch):
+    """The row-resident step with far more workgroups than the chip holds at once (2048 rows, one
+    workgroup each, from step 0), so most workgroups start after others have already stepped and
+    ended their rows within the same launch: every workgroup must still rank the rows live at the
+    step's start (the alive byte's ended-at-step marker; a row skipped or stepped twice would shift
+    every later row).  Lengths, terminations and the Sim's states (independent of the actions) are
+    bit-identical to the multi-kernel step for all 2048 rows; actions / log-probs / values match the
+    oracle's batch-1 loop for every row's first 4 steps and 16 whole episodes."""
+    E, T = 2048, 12
+    learner, env, oracle = make_learner(depth=2, T=T, episodes=E, batch=64, hazard=2)
+    eng = learner._engine_for(env, T)
+    assert eng.rows_max > 0
+    monkeypatch.setattr(eng, 'rows_max', E)   # every step row-resident, grid = E workgroups
+    traj, lens, _, _ = learner.rollout_device(env, 0, T)
+    torch.cuda.synchronize()
+    rows_out = {k: v.clone() for k, v in traj.items() if v is not None}
+    rows_lens = lens.clone()
+    assert set(eng.alive.cpu().tolist()) <= {0, 3, 4}   # (dead, or ended by the last row step)
+    monkeypatch.setattr(eng, 'rows_max', 0)   # the multi-kernel step
+    traj, lens, _, _ = learner.rollout_device(env, 0, T)
+    torch.cuda.synchronize()
+    assert torch.equal(rows_lens, lens)
+    for k in ('states', 'bounds'):
+        assert torch.equal(rows_out[k], traj[k]), k
+    assert int((lens < T).sum()) > E // 2          # most episodes ended inside a row-step launch
+    episodes, _ = oracle.rollout(0, max_timesteps=4)
+    compare_rollout(rows_out, rows_lens, episodes, prefix=4)
+    longest = torch.argsort(rows_lens.cpu(), descending=True, stable=True)[:8].tolist()
+    rows = sorted(set(longest + [int(x) for x in torch.linspace(7, E - 9, 8).round().long().tolist()]))
+    episodes, _ = oracle.rollout(0, slots=rows)
+    compare_rollout(rows_out, rows_lens, episodes, rows=rows)
+
+
 # ---- the causal fractal policy body (SURVEY 8(f)-3, oracle/fractal_ref.OracleFractalPolicy) ------------
 
 

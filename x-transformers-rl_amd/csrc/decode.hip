@@ -44,6 +44,18 @@ __device__ __forceinline__ float f4c(const float4& v, int k) {
 
 __device__ __forceinline__ const int32_t* rows_of(const XtrlDecodeDesc& D, int t) { return D.live_rows + (t & 1) * D.E; }
 
+// The alive byte of an episode slot: 0 dead, 1 live, 2 truncation-bootstrap step pending (host envs),
+// ALIVE_END + (t & 1): a Sim episode the row-resident step ended at step t.  That step's workgroups
+// rank the live slots while others already step theirs, so the step never turns a slot it ranks
+// from live to dead: a row it ends goes 1 -> ALIVE_END + (t & 1), live for step t, dead for step
+// t + 1 (whose compaction clears it to 0 — before step t + 2, where the parity would repeat).  One
+// byte, one store: the ranking needs no ordering between stores of different arrays.
+constexpr uint8_t ALIVE_END = 3;
+__device__ __forceinline__ bool live_at(uint8_t al, int t) {
+  return al == 1 || al == 2 || al == (uint8_t)(ALIVE_END + (t & 1));
+}
+__device__ __forceinline__ bool ended_before(uint8_t al, int t) { return al == (uint8_t)(ALIVE_END + ((t + 1) & 1)); }
+
 // ---------------------------------------------------------------------------------------------
 // live-row compaction: one workgroup lists the episode slots with alive != 0 in slot order
 // (live_rows[t & 1][0 .. n-1], live_count[t & 1] = n) — deterministic, one launch
@@ -56,7 +68,9 @@ __global__ __launch_bounds__(1024) void k_compact(const XtrlDecodeDesc D, int t)
   if (tid == 0) base_sh = 0;
   for (int e0 = 0; e0 < D.E; e0 += 1024) {
     const int e = e0 + tid;
-    const bool al = e < D.E && D.alive[e] != 0;
+    const uint8_t a8 = e < D.E ? D.alive[e] : 0;
+    const bool al = live_at(a8, t);
+    if (ended_before(a8, t)) D.alive[e] = 0;
     const uint64_t bal = __ballot(al);
     if (lane == 0) wsum[w] = __popcll(bal);
     __syncthreads();
@@ -108,7 +122,7 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, c
     }
   }
   int n_live = 0;   // (CMP: the live count, the same in every thread)
-  if constexpr (CMP) {   // rank the live slots (alive != 0) in slot order
+  if constexpr (CMP) {   // rank the live slots (live_at) in slot order
     uint8_t alv[EMB_MAX_E / 1024];
 #pragma unroll
     for (int c = 0; c < EMB_MAX_E / 1024; ++c) {
@@ -120,7 +134,8 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, c
     for (int c = 0; c < EMB_MAX_E / 1024; ++c) {
       if (1024 * c >= D.E) break;   // (uniform)
       const int e = 1024 * c + tid;
-      const bool al = e < D.E && alv[c] != 0;
+      const bool al = e < D.E && live_at(alv[c], t);
+      if (blockIdx.x == 0 && e < D.E && ended_before(alv[c], t)) D.alive[e] = 0;
       const uint64_t bal = __ballot(al);
       if (lane == 0) wsum[w] = __popcll(bal);
       __syncthreads();
@@ -610,10 +625,11 @@ __device__ __forceinline__ SampleIn sample_load(const XtrlDecodeDesc& D, int e) 
 
 // the sample and the Sim step of one live row (slot e) by its SAMPLE_L lanes (sub = lane of the
 // row's aligned group, every lane of the group active); lg = the row's actor outputs in LDS.
-// keep_boot: a truncation-bootstrap row (alive 2) keeps alive = 2 (the next k_env_feedback clears it)
-// — the row-resident step, whose workgroups rank the live rows while others already sample
+// row_step: the row-resident step, whose workgroups rank the live rows while others already sample —
+// a truncation-bootstrap row (alive 2) keeps alive = 2 (the next k_env_feedback clears it) and a Sim
+// row ending here is marked ALIVE_END + (t & 1), never 0 (live_at)
 __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e, int sub, const float* lg,
-                                           const SampleIn& in, bool keep_boot = false) {
+                                           const SampleIn& in, bool row_step = false) {
   const XtrlRngState& R = in.R;
   const int al = in.al;
   const uint32_t ep = in.ep;
@@ -636,7 +652,7 @@ __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e
   tw = __shfl(tw, base + 2, 64);
   if (sub != 0) return;
   if (al == 2) {   // truncation-bootstrap step of a host env: its value logits are all it needed
-    if (!keep_boot) D.alive[e] = 0;
+    if (!row_step) D.alive[e] = 0;
     return;
   }
   int a = 0;
@@ -687,7 +703,7 @@ __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e
     D.prev_reward[e] = reward;
     D.cum_reward[e] = cum + (double)reward;
     D.lens[e] = t + 1;
-    if (term || t + 1 >= D.Tmax) D.alive[e] = 0;
+    if (term || t + 1 >= D.Tmax) D.alive[e] = row_step ? (uint8_t)(ALIVE_END + (t & 1)) : (uint8_t)0;
   }
 }
 
@@ -1745,26 +1761,26 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   const int S = D.S, d = D.d, H = D.H, I = H * DH, L = D.L;
   // ---- compaction (as k_embed<CMP>): every workgroup ranks the live slots itself.  Workgroups that
   //      start late (the grid need not be resident at once) may find rows that others have already
-  //      stepped: a Sim row ended at this step has alive 0 and lens t + 1 and still counts; a bootstrap
-  //      row keeps alive 2 through the launch (sample_row keep_boot) — so every workgroup ranks the
-  //      rows live at the step's start
-  // (every chunk's alive byte and length loaded in one batch, then ranked chunk by chunk)
+  //      stepped: a Sim row ended at this step reads ALIVE_END + (t & 1) and a bootstrap row keeps
+  //      alive 2 through the launch (sample_row row_step) — both still live_at(t) — so every workgroup
+  //      ranks the rows live at the step's start, whichever value of the one byte it sees
+  // (every chunk's alive byte loaded in one batch, then ranked chunk by chunk)
   int n_live = 0;
   constexpr int CH = EMB_MAX_E / ROW_T;
   uint8_t alv[CH];
-  int lnv[CH];
 #pragma unroll
   for (int ci = 0; ci < CH; ++ci) {
     const int ec = min(ROW_T * ci + tid, D.E - 1);
     alv[ci] = D.alive[ec];
-    lnv[ci] = D.lens[ec];
   }
 #pragma unroll
   for (int ci = 0; ci < CH; ++ci) {
     const int c0 = ROW_T * ci;
     if (c0 >= D.E) break;   // (uniform)
     const int e = c0 + tid;
-    const bool al = e < D.E && (alv[ci] != 0 || (D.sim_mode >= 0 && lnv[ci] == t + 1));
+    const bool al = e < D.E && live_at(alv[ci], t);
+    // (a slot ended at step t - 1 is dead here: cleared before step t + 1 reads the same parity)
+    if (blockIdx.x == 0 && e < D.E && ended_before(alv[ci], t)) D.alive[e] = 0;
     const uint64_t bal = __ballot(al);
     if (lane == 0) wsum[w] = __popcll(bal);
     __syncthreads();

@@ -52,7 +52,7 @@ EMA_DEFAULTS = dict(update_after_step=100, update_every=10, inv_gamma=1., power=
 # x-transformers Decoder / Attention / FeedForward options (>= 2.3, the reference's pin, pyproject.toml:35)
 # at their default values: passing one of them explicitly builds the network the MI355X decoder runs
 XT_DEFAULTS = dict(
-    causal=True, cross_attend=False, only_cross=False, use_scalenorm=False, use_rmsnorm=False, use_simple_rmsnorm=False,
+    cross_attend=False, only_cross=False, use_scalenorm=False, use_rmsnorm=False, use_simple_rmsnorm=False,
     alibi_pos_bias=False, rel_pos_bias=False, dynamic_pos_bias=False, rotary_xpos=False, residual_attn=False,
     cross_residual_attn=False, macaron=False, pre_norm=True, gate_residual=False, scale_residual=False,
     shift_tokens=0, sandwich_norm=False, resi_dual=False, zero_init_branch_output=False, layer_dropout=0.,
@@ -118,6 +118,8 @@ class Agent(nn.Module):
         # accepted too.
         for k in ('attn_flash', 'attn_onnxable'):
             wm.pop(k, None)
+        # x-transformers' Decoder refuses an explicit causal flag (it always is causal)
+        assert 'causal' not in wm, 'cannot set causality on decoder'
         for k, default in XT_DEFAULTS.items():
             if k in wm and wm[k] == default:
                 wm.pop(k)

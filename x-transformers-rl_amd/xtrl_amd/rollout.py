@@ -453,6 +453,7 @@ class RolloutEngine:
                 break
             if not live.any():   # only bootstrap rows: their decode step, no env step
                 self.step(t, rows_max > 0)
+                self.alive.zero_()   # (the row-resident step leaves them at 2 for a feedback that never comes)
                 break
             self._host_decode(t, rows_max, desc, act_p, stream)
             pending[:] = False
