@@ -62,7 +62,7 @@ def _worker(rank, world, port, out_dir, mode):
     sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK='0')
-    if mode == 'c5grad':   # one collective per backward bucket (no coalescing of the small test buckets)
+    if mode in ('c5grad', 'c5w8'):   # one collective per backward bucket (no coalescing of the small test buckets)
         os.environ['XTRL_DP_BUCKET_FLOATS'] = '1'
     import torch.distributed as dist
     torch.cuda.set_device(0)
@@ -71,7 +71,7 @@ def _worker(rank, world, port, out_dir, mode):
         gene_mode = mode in ('genes', 'c5')
         if mode == 'c5':     # population 8 over 4 ranks (2 genes each), fractal body
             learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
-        elif mode == 'c5grad':
+        elif mode in ('c5grad', 'c5w8'):   # c5w8: population 8 over 8 ranks, gene g on rank g
             learner, env = _make(world, shard_by_gene=True, genes=8, episodes=2, fractal=2)
         elif mode == 'c4':   # the C4 partition: one policy, the episodes split 8 ways (torch.chunk)
             learner, env = _make(world, episodes=16, evo=False)
@@ -83,12 +83,13 @@ def _worker(rank, world, port, out_dir, mode):
         grads = []
         from xtrl_amd import distributed as dist_
         coll0 = dist_.COUNTS['all_reduce']
-        if mode in ('grad', 'c4', 'c5grad'):
+        if mode in ('grad', 'c4', 'c5grad', 'c5w8'):
             lr = a.opt_cfg['lr']
             a.opt_cfg['lr'] = 0.     # weights fixed: every minibatch gradient at the same point
             a.learn(traj, lens, genes, first['fit'], update=0, probe=_grad_probe(a, grads))
             first['allreduces'] = dist_.COUNTS['all_reduce'] - coll0
-            if mode == 'c4':         # then one full learning update: the ranks must stay in lockstep
+            first['genes_after'] = a.gene_pool.genes.clone() if a.gene_pool is not None else torch.zeros(1)
+            if mode in ('c4', 'c5w8'):   # then one full learning update: the ranks must stay in lockstep
                 a.opt_cfg['lr'] = lr
                 learner(env, 1)
         else:
@@ -289,3 +290,64 @@ def test_c5_fractal_bucketed_allreduce_gradient(tmp_path):
         got = r[0]['grads'][i]
         scale = float(want.abs().max())
         assert float((got - want).abs().max()) <= 1e-6 * scale + 1e-9, i
+
+
+@pytest.mark.gpu
+def test_c5_population8_eight_ranks_one_gene_each(tmp_path):
+    """The C5 partition exactly as BASELINE configs[4] names it — EPO population 8, ONE gene per rank
+    (gene g on rank g), the fractal policy body — with 8 gloo ranks on one GPU at reduced size (2
+    episodes per gene).  Each rank's rollout reproduces the single-process rollout at its global pair
+    slots and the fitness summed over ranks equals the single-process fitness (x_transformers_rl.py:
+    1345-1362); with the learning rate at 0, every optimiser step makes one collective per gradient
+    bucket (levels + 2, no coalescing) and every rank holds the same gradient, equal to the mean of the
+    8 per-rank minibatch gradients a single process computes; the genes after that update's
+    evolve_ calls (evolution.py:76-184, every minibatch) agree with the single process's; after one
+    more full learning update the 8 ranks' weights, EMA, RSNorm statistics and genes are bitwise
+    identical (x_transformers_rl.py:1143-1154)."""
+    world, levels = 8, 2
+    r = _run(tmp_path, 'c5w8', world=world)
+    for rank in range(world):
+        assert {g for _, g in r[rank]['pairs']} == {rank}
+        assert len(r[rank]['pairs']) == 2
+    steps = len(r[0]['grads'])
+    assert steps > 0
+    assert r[0]['first']['allreduces'] == steps * (levels + 2), (r[0]['first']['allreduces'], steps)
+    for i in range(1, world):
+        assert len(r[i]['grads']) == steps
+        for g0, gi in zip(r[0]['grads'], r[i]['grads']):
+            assert torch.equal(g0, gi)
+    learner, env = _make(1, genes=8, episodes=2, fractal=levels)
+    a = learner.agent
+    a.opt_cfg['lr'] = 0.
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    fit = learner.fitness(cum, genes)
+    for rank in range(world):
+        slots = torch.tensor(r[rank]['slots'])
+        assert torch.equal(r[rank]['first']['lens'], lens.cpu()[slots])
+        assert torch.equal(r[rank]['first']['actions'], traj['actions'].cpu()[slots])
+        torch.testing.assert_close(r[rank]['first']['fit'], fit, rtol=1e-6, atol=1e-6)
+    flat0 = a.flat.flat.clone()
+    genes0 = a.gene_pool.genes.clone()
+    rs0 = (a.rs_mean.clone(), a.rs_var.clone(), a.rs_step)
+    per_rank = []
+    for rank in range(world):
+        a.rs_mean, a.rs_var, a.rs_step = rs0[0].clone(), rs0[1].clone(), rs0[2]
+        a.step = 0
+        a.gene_pool.genes.copy_(genes0)
+        rows = torch.tensor(r[rank]['slots'], device=lens.device)
+        sub = {k: (v[rows].contiguous() if v is not None else None) for k, v in traj.items()}
+        grads = []
+        a.learn(sub, lens[rows].contiguous(), genes[rows].contiguous(), fit, update=0, probe=_grad_probe(a, grads))
+        assert torch.equal(a.flat.flat, flat0) and len(grads) == steps
+        per_rank.append(grads)
+        # evolve_ sees the same global fitness on every rank: the same genes as the 8-rank run
+        torch.testing.assert_close(a.gene_pool.genes.cpu(), r[rank]['first']['genes_after'].cpu(), rtol=0, atol=0)
+    for i in range(steps):
+        want = sum(per_rank[k][i] for k in range(world)) / world
+        got = r[0]['grads'][i]
+        scale = float(want.abs().max())
+        assert float((got - want).abs().max()) <= 1e-6 * scale + 1e-9, i
+    for k in ('flat', 'ema', 'rs_mean', 'rs_var', 'genes'):
+        for rank in range(1, world):
+            assert torch.equal(r[0][k], r[rank][k]), (k, rank)
+    assert torch.isfinite(r[0]['flat']).all() and not torch.equal(r[0]['flat'], flat0.cpu())

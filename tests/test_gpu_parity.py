@@ -941,6 +941,85 @@ def test_learner_two_updates_match_oracle(evo, gates, frac):
             np.testing.assert_allclose(ours, theirs, rtol=5e-2, atol=5e-3)
 
 
+@pytest.mark.parametrize('name', ['learner_readme', 'learner_lander_evo'])
+def test_learner_replays_reference_learner_fixture(golden, name):
+    """The device Learner against the REFERENCE's own Learner run (tests/golden/make_golden.py
+    gen_learner executes x_transformers_rl.py:1174-1380 — rollout, Agent.learn, EMA, EPO — with the
+    shared sampling / reward-coin / minibatch-order / evolve-seed protocol patched in): the same
+    initial weights (reference state_dict names, strict load) and genes, then two updates.
+    Rollouts: lengths, actions, terminations, states and rewards bit-exact, log-probs and critic
+    logits within 1e-4, per-gene fitness within 1e-5.  Logs: update 0's minibatches within 1e-4;
+    update 1's first three within 1e-4 and all within the free-running drift bound of
+    test_learner_two_updates_match_oracle (5e-2: AdoptAtan2's cautious mask).  Final online / EMA
+    weights: 99 % of the elements within 1e-5 of the reference's, every element within 16 lr (one
+    full step per optimiser step: a flipped cautious-mask bit moves an element by at most that);
+    RSNorm statistics within 1e-5, final genes within 1e-5 (README config: no EPO)."""
+    from xtrl_amd import Learner, SynthVecSim
+    g = golden(name)
+    seed, S, A, Tm, depth, gates, evo, episodes, batch, updates, hz, gdim = (int(x) for x in g['cfg'])
+    wm = dict(attn_dim_head=16, heads=4, depth=depth)
+    if gates:
+        wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
+    gp = dict(dim=gdim, num_genes_per_island=3, num_selected=2, tournament_size=2)
+    learner = Learner(state_dim=S, num_actions=A, reward_range=(-2., 2.), world_model=wm, max_timesteps=Tm,
+                      batch_size=batch, num_episodes_per_update=episodes, evolutionary=bool(evo), evolve_every=1,
+                      evolve_after_step=0, latent_gene_pool=gp,
+                      agent_kwargs=dict(dropout=0., seed=seed, reward_dropout=float(g['reward_dropout'])),
+                      use_graph=False)
+    agent = learner.agent
+    sd = {k[5:]: torch.from_numpy(g[k]) for k in g.files if k.startswith('init.')}
+    with torch.no_grad():
+        agent.model.load_state_dict(sd, strict=True)
+        agent.ema_flat.copy_(agent.flat.flat)
+        if evo:
+            agent.gene_pool.genes.copy_(torch.from_numpy(g['init_genes']).to(agent.gene_pool.genes.device))
+    env = SynthVecSim(S, A, str(g['mode']), hazard_log2=hz)
+    keys = list(g['log_keys'])
+    n_mb = g['logs'].shape[0] // updates
+    for u in range(updates):
+        traj, lens, genes, cum = learner.rollout_device(env, u, Tm)
+        torch.cuda.synchronize()
+        lens_c = lens.cpu().numpy()
+        np.testing.assert_array_equal(lens_c, g[f'u{u}.lens'])
+        n = int(lens_c.max())
+        np.testing.assert_array_equal(traj['actions'][:, :n].cpu().numpy(), g[f'u{u}.actions'])
+        np.testing.assert_array_equal(traj['states'][:, :n].cpu().numpy(), g[f'u{u}.states'])
+        np.testing.assert_array_equal(traj['rewards'][:, :n].cpu().numpy(), g[f'u{u}.rewards'])
+        np.testing.assert_array_equal(traj['bounds'][:, :n].cpu().numpy().astype(bool), g[f'u{u}.bounds'])
+        tol(traj['logp'][:, :n], torch.from_numpy(g[f'u{u}.logp']), 1e-4, 1e-5)
+        tol(traj['values'][:, :n], torch.from_numpy(g[f'u{u}.values']), 1e-4, 1e-4)
+        np.testing.assert_array_equal(genes.cpu().numpy(), g[f'u{u}.genes'])
+        fit = learner.fitness(cum, genes)
+        if evo:
+            tol(fit, torch.from_numpy(g[f'u{u}.fitness']), 1e-5, 1e-5)
+        agent.learn(traj, lens, genes, fit, update=u)
+        ours = np.array([[lg[k] for k in keys] for lg in agent.pop_logs()])
+        ref = g['logs'][u * n_mb:(u + 1) * n_mb]
+        assert ours.shape == ref.shape
+        if u == 0:
+            np.testing.assert_allclose(ours, ref, rtol=1e-4, atol=1e-5)
+        else:
+            np.testing.assert_allclose(ours[:3], ref[:3], rtol=1e-4, atol=1e-5)
+            np.testing.assert_allclose(ours, ref, rtol=5e-2, atol=5e-3)
+    lr = 8e-4
+    steps = updates * n_mb
+    worst, off = 0., 0
+    for pre, model in (('final.', agent.model), ('ema.', agent.ema_model)):
+        for k, p in model.state_dict().items():
+            ref = torch.from_numpy(g[pre + k])
+            d = (p.detach().cpu() - ref).abs()
+            worst = max(worst, float(d.max()))
+            off += int((d > 1e-5 + 1e-5 * ref.abs()).sum())
+            assert float(d.max()) <= steps * lr, (pre + k, float(d.max()))
+            assert float((d > 1e-5 + 1e-5 * ref.abs()).float().mean()) <= 0.01, (pre + k, float(d.max()))
+    print(f'{name}: final weights max |delta| {worst:.2e}, {off} elements beyond 1e-5')
+    tol(agent.rs_mean, torch.from_numpy(g['rs_mean']), 1e-5, 1e-6)
+    tol(agent.rs_var, torch.from_numpy(g['rs_var']), 1e-5, 1e-6)
+    assert agent.rs_step == int(g['rs_step'])
+    if evo:
+        tol(agent.gene_pool.genes, torch.from_numpy(g['final_genes']), 1e-5, 1e-6)
+
+
 # ----------------------------------------------------------------------------------------------
 # the reference's own test contract (tests/test_x_transformers_rl.py:4-53) on the host-env path
 # ----------------------------------------------------------------------------------------------
