@@ -525,9 +525,11 @@ def main():
     t0 = time.perf_counter()
     total = torch.zeros((), device='cuda', dtype=torch.int64)
     lens_last = None
+    per_update = []
     for _ in range(args.steps):
         steps, lens = one_update(learner, env, T, phases=True)
         total += steps
+        per_update.append(steps)
         lens_last = lens
     torch.cuda.synchronize()
     if world > 1:
@@ -541,6 +543,17 @@ def main():
         dist.all_reduce(total)
     elapsed = float(el)
     env_steps = int(total)
+    # the median per-update rate beside the mean: each timed update's env-steps over its
+    # event-timed duration (rollout start -> learn end on the stream; the host gap between updates is
+    # not in it), summed / max-ed over ranks like the headline
+    upd_steps = torch.stack(per_update).to(torch.float64)
+    upd_ms = torch.tensor([e[0].elapsed_time(e[2]) for e in PHASES[-args.steps:]], device='cuda', dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(upd_steps)
+        dist.all_reduce(upd_ms, op=dist.ReduceOp.MAX)
+    upd_rate = (upd_steps / upd_ms * 1e3).cpu()
+    value_median = float(upd_rate.median())
+    ms_median = float(upd_ms.cpu().median())
     # collectives of the timed updates (per rank): the bucketed gradient all-reduces, RSNorm rides in
     # the last bucket, fitness sums
     coll = {k: (dist_.COUNTS[k] - coll0[k]) / args.steps for k in coll0} if world > 1 else None
@@ -608,6 +621,7 @@ def main():
                        single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
         line = dict(metric='env-steps/s (rollout+update)', value=round(value, 1), unit='env-steps/s', n_gpus=world,
+                    value_median=round(value_median, 1), ms_per_step_median=round(ms_median, 2),
                     value_probed=None if value_probed is None else round(value_probed, 1),
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
                     higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
