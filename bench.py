@@ -65,6 +65,16 @@ CONFIGS = {
                                  'one env.step per action as the reference loop (xtrl.py:1220-1341)',
                         S=8, A=4, episodes=64, T=500, depth=4, dim=48, heads=4, dim_head=16, gates=True, evo=True,
                         batch=8, hazard_log2=6, dropout=0.25, mode='lander', host=True),
+    # the north-star drop-in at its batch (BASELINE.json configs[2] through the host-env path): 1024 numpy
+    # LunarLander-shaped sub-envs behind gym's vector-env contract, stepped on the host once per timestep
+    # through Learner.rollout_host's vector waves (one batched decode, one action copy to the host and
+    # one env-result copy to the device per step), the C3 model
+    'lander_hostvec': dict(workload='drop-in at the north-star batch: 1024 numpy LunarLander-shaped host sub-envs '
+                                    '(vector-env contract, S=8, A=4, hazard 1/64) x 128 steps through '
+                                    'Learner.rollout_host vector waves, C3 model (depth 4, d=256, 4x16-head gated '
+                                    'value-residual), batch 128 episodes, 4 epochs, dropout 0.25, no EPO',
+                           S=8, A=4, episodes=1024, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True,
+                           evo=False, batch=128, hazard_log2=6, dropout=0.25, mode='lander', host=True, vector=1024),
     # configs[0] — README Sim plumbing case
     'c1': dict(workload='C1: README Sim (S=5, A=2, T=10), depth 1, d=48, 64 episodes, batch 8',
                S=5, A=2, episodes=64, T=10, depth=1, dim=48, heads=4, dim_head=16, gates=False, evo=False,
@@ -93,13 +103,36 @@ class HostLanderSim:
         return state, reward, bool(self.rng.random() < self.p), False, {}
 
 
+class HostLanderVec:
+    """W LunarLander-shaped sub-envs behind gym's vector-env contract (num_envs; reset(seed=[...]) ->
+    (states [W][S], info); step(actions [W]) -> (states, rewards [W], terminated [W], truncated [W],
+    info)), the same distributions as HostLanderSim, drawn for all sub-envs at once by numpy on the
+    host (gym's SyncVectorEnv steps its LunarLanders one by one; the host cost here is the numpy draw)."""
+
+    def __init__(self, W, S, A, hazard_log2, seed=0):
+        self.num_envs, self.S, self.A, self.p = W, S, A, 2.0 ** -hazard_log2
+        self.rng = np.random.default_rng(seed)
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.rng = np.random.default_rng([int(x) for x in np.asarray(seed).reshape(-1)[:4]])
+        return self.rng.standard_normal((self.num_envs, self.S), dtype=np.float32), {}
+
+    def step(self, actions):
+        W = self.num_envs
+        state = self.rng.standard_normal((W, self.S), dtype=np.float32)
+        reward = self.rng.standard_normal(W) + 0.1 * (np.asarray(actions).reshape(W) - self.A / 2)
+        term = self.rng.random(W) < self.p
+        return state, reward, term, np.zeros(W, dtype=bool), {}
+
+
 def build_learner(cfg, seed, use_graph=True, world=1):
     from xtrl_amd import Learner, SynthVecSim
     wm = dict(attn_dim_head=cfg['dim_head'], heads=cfg['heads'], depth=cfg['depth'])
     if cfg['gates']:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
     extra = dict(policy_body='fractal', fractal_levels=cfg['fractal']) if cfg.get('fractal') else {}
-    if cfg.get('host'):   # train_lander.py:42-49
+    if cfg.get('host') and not cfg.get('vector'):   # train_lander.py:42-49
         extra.update(actor_loss_weight=0.5)
     learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
                       max_timesteps=cfg['T'], batch_size=cfg['batch'],
@@ -110,8 +143,10 @@ def build_learner(cfg, seed, use_graph=True, world=1):
                       agent_kwargs=dict(hidden_dim=cfg['dim'], dropout=cfg['dropout'], seed=seed,
                                         save_path='/tmp/xtrl_bench_ppo.pt', **extra),
                       use_graph=use_graph, shard_by_gene=bool(cfg.get('fractal')),
-                      **(dict(frac_actor_critic_head_gradient=0.1) if cfg.get('host') else {}))
+                      **(dict(frac_actor_critic_head_gradient=0.1) if cfg.get('host') and not cfg.get('vector') else {}))
     # (C5: episodes per update = 128 x world over 8 genes, gene-sharded: 1024 pairs per GPU at any N)
+    if cfg.get('vector'):
+        return learner, HostLanderVec(cfg['vector'], cfg['S'], cfg['A'], cfg['hazard_log2'], seed)
     if cfg.get('host'):
         return learner, HostLanderSim(cfg['S'], cfg['A'], cfg['hazard_log2'], seed)
     env = SynthVecSim(cfg['S'], cfg['A'], cfg['mode'], cfg['hazard_log2'])
@@ -119,6 +154,7 @@ def build_learner(cfg, seed, use_graph=True, world=1):
 
 
 PHASES = []   # (start, after rollout, after learn) events of the timed updates
+HOST_TIMES = {}   # host envs: seconds of the timed updates' steps in decode (+ wait) / env step / feedback
 
 
 def one_update(learner, env, T, probe=None, phases=False):
@@ -127,10 +163,13 @@ def one_update(learner, env, T, probe=None, phases=False):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if phases else None
     if ev:
         ev[0].record()
-    if isinstance(env, HostLanderSim):   # the reference's scalar env contract (Learner.forward's host branch)
+    if isinstance(env, (HostLanderSim, HostLanderVec)):   # host envs (Learner.forward's host branch)
         g = torch.Generator().manual_seed(agent.seed * 31 + u)
         seeds = torch.randint(0, int(1e7), (learner.num_episodes_per_update,), generator=g) if agent.evolutionary else None
         traj, lens, genes, cum = learner.rollout_host(env, u, T, seeds)
+        if phases:   # the host side of the timed updates' steps (rollout.run_host_wave)
+            for k, v in learner._engine[1].host_times.items():
+                HOST_TIMES[k] = HOST_TIMES.get(k, 0) + v
     else:
         traj, lens, genes, cum = learner.rollout_device(env, u, T)
     if ev:
@@ -625,7 +664,8 @@ def main():
                     value_probed=None if value_probed is None else round(value_probed, 1),
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
                     higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
-                    data=('synthetic (numpy LunarLander-shaped scalar host env, random-init weights)' if host else
+                    data=('synthetic (numpy LunarLander-shaped host vector env, random-init weights)' if cfg.get('vector') else
+                          'synthetic (numpy LunarLander-shaped scalar host env, random-init weights)' if host else
                           'synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)'),
                     config=dict(workload=cfg['workload'],
                                 global_batch=cfg['episodes'] * (cfg.get('genes', 3) if cfg['evo'] else 1) * world,
@@ -633,6 +673,13 @@ def main():
                     roofline=roofline, attention_roofline=attn_roofline, total_roofline=total_roof,
                     cpu_baseline=cpu, ppo_loss=loss_delta,
                     phase_ms=phase_ms)
+        if HOST_TIMES.get('steps'):
+            n = HOST_TIMES['steps']
+            line['host_step_us'] = dict(
+                {k: round(1e6 * HOST_TIMES[k] / n, 1) for k in ('decode', 'env', 'feedback')}, steps=n,
+                note='per host-env step, host clock: decode = the decode launches + the wait for the actions '
+                     '(device->host copy included); env = the env step; feedback = staging + host->device copy + '
+                     'the feedback kernel launch')
         if coll is not None:
             mb = learner.agent.epochs * (len(learner.episode_genes_for_process) // learner.agent.batch_size)
             line['dp'] = dict(backend=dist.get_backend(), collectives_per_update=coll,

@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 16
+#define XTRL_ABI_VERSION 17
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -215,6 +215,17 @@ typedef struct XtrlDecodeDesc {
    * are not used) */
   int ff_glu;
   float* hglu;
+  /* world_model['attn_qk_norm']: q and k of the new token l2-normalised per head before the rotary
+   * (the cache holds normalised, rotated keys); attn_scale: the score scale (qk_norm_scale with qk
+   * norm), 0 = dh^-0.5.  xpos_base: rotary xPos scale base (0 = off) — with rotary_abs the rotated
+   * pair j of q at position t is scaled by ((j + 0.4 rot_dim) / (1.4 rot_dim)) ^ ((t - (t + 1) / 2) /
+   * xpos_base), k by its inverse (the reference's cached decode rotates at position 0: identity) */
+  int qk_norm;
+  float attn_scale;
+  float xpos_base;
+  /* world_model['use_rmsnorm']: every pre-norm and the final norm are x-transformers' RMSNorm
+   * (F.normalize(x) sqrt(d) g) instead of its LayerNorm; 0: LayerNorm */
+  int rms_norm;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
@@ -494,6 +505,18 @@ typedef struct XtrlTrainDesc {
   int ff_glu;
   int ld_u2;
   float* glu_dh;
+  /* world_model['attn_qk_norm'] (x-transformers qk norm): q and k are l2-normalised per head
+   * (F.normalize, eps 1e-12) before the rotary, and attn_scale carries qk_norm_scale (default 10).
+   * 0: off */
+  int qk_norm;
+  /* world_model['rotary_xpos'] (x-transformers RotaryEmbedding use_xpos): the rotary scale base
+   * (rotary_xpos_scale_base, default 512), 0 = off.  Rotated channel pair j (even) of q at position p
+   * of the n-step minibatch is multiplied by ((j + 0.4 rot_dim) / (1.4 rot_dim)) ^ ((p - n / 2) /
+   * xpos_base), that of k divided by it */
+  float xpos_base;
+  /* world_model['use_rmsnorm'] (x-transformers RMSNorm: F.normalize(x) sqrt(d) g, no mean, eps 1e-12
+   * on the norm) for every pre-norm and the final norm, forward and backward; 0: LayerNorm */
+  int rms_norm;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

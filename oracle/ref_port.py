@@ -221,6 +221,11 @@ class ModelConfig:
     ff_mult: int = 4          # x-transformers FeedForward mult, reached through world_model['ff_mult']
     ff_no_bias: bool = False  # world_model['ff_no_bias'] (x-transformers FeedForward no_bias)
     ff_glu: bool = False      # world_model['ff_glu'] (x-transformers FeedForward glu: GELU-gated project-in)
+    rms_norm: bool = False    # world_model['use_rmsnorm'] (x-transformers RMSNorm pre-norms / final norm)
+    qk_norm: bool = False     # world_model['attn_qk_norm'] (+ attn_qk_norm_scale)
+    qk_norm_scale: float = 10.
+    rotary_xpos: bool = False  # world_model['rotary_xpos'] (+ rotary_xpos_scale_base)
+    xpos_scale_base: float = 512.
 
 
 class OracleWMAC(nn.Module):
@@ -237,7 +242,9 @@ class OracleWMAC(nn.Module):
                                    verbose=False, attn_gate_values=cfg.gate_values,
                                    add_value_residual=cfg.value_residual,
                                    learned_value_residual_mix=cfg.learned_mix, ff_mult=cfg.ff_mult,
-                                   ff_no_bias=cfg.ff_no_bias, ff_glu=cfg.ff_glu))
+                                   ff_no_bias=cfg.ff_no_bias, ff_glu=cfg.ff_glu, attn_qk_norm=cfg.qk_norm,
+                                   attn_qk_norm_scale=cfg.qk_norm_scale, rotary_xpos=cfg.rotary_xpos,
+                                   rotary_xpos_scale_base=cfg.xpos_scale_base, use_rmsnorm=cfg.rms_norm))
         self.reward_embed = nn.Parameter(torch.ones(d) * 1e-2)
         if cfg.continuous:
             self.action_embeds = nn.Linear(cfg.num_actions, d)
@@ -499,6 +506,11 @@ class LearnerConfig:
     ff_mult: int = 4
     ff_no_bias: bool = False
     ff_glu: bool = False
+    rms_norm: bool = False
+    qk_norm: bool = False
+    qk_norm_scale: float = 10.
+    rotary_xpos: bool = False
+    xpos_scale_base: float = 512.
     continuous: bool = False
     squash: bool = True
     clamp: tuple | None = None
@@ -552,7 +564,8 @@ class OracleLearner:
                          c.reward_range, 100, c.continuous, c.squash, c.evolutionary,
                          self.gp['dim'] if c.evolutionary else 0, c.frac_head_grad, c.beta_s, c.eps_clip,
                          c.value_clip, c.dropout, c.reward_dropout, True, c.gate_values, c.value_residual,
-                         c.learned_mix, c.ff_mult, c.ff_no_bias, c.ff_glu)
+                         c.learned_mix, c.ff_mult, c.ff_no_bias, c.ff_glu, rms_norm=c.rms_norm, qk_norm=c.qk_norm,
+                         qk_norm_scale=c.qk_norm_scale, rotary_xpos=c.rotary_xpos, xpos_scale_base=c.xpos_scale_base)
         self.model = model_factory(mc) if model_factory is not None else OracleWMAC(mc)
         if init_state_dict is not None:
             self.model.load_state_dict(init_state_dict)

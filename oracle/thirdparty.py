@@ -176,15 +176,44 @@ class LayerNorm(nn.Module):
         return F.layer_norm(x, (self.dim,), eps=1e-5) * self.gamma
 
 
+class RMSNorm(nn.Module):
+    """x-transformers RMSNorm (Decoder use_rmsnorm): F.normalize(x, dim=-1) * dim ** 0.5 * g (no
+    unit offset); parameter ``g``."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.scale = dim ** 0.5
+        self.g = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return F.normalize(x, dim=-1) * self.scale * self.g
+
+
 class RotaryEmbedding(nn.Module):
-    def __init__(self, dim, base=10000.):
+    """x-transformers RotaryEmbedding; ``use_xpos`` (Decoder rotary_xpos): the xPos scale
+    ((arange(0, dim, 2) + 0.4 dim) / (1.4 dim)) ** ((pos - max_pos // 2) / scale_base), max_pos =
+    pos.max() + 1, interleaved like the frequencies (q times it, k divided by it; x-transformers
+    apply_rotary_pos_emb).  The scale table is a non-persistent buffer here (parity unpinned)."""
+
+    def __init__(self, dim, base=10000., use_xpos=False, scale_base=512.):
         super().__init__()
         inv_freq = 1. / (base ** (torch.arange(0, dim, 2).float() / dim))
         self.register_buffer('inv_freq', inv_freq)
+        self.use_xpos, self.scale_base = use_xpos, scale_base
+        self.register_buffer('xpos_scale', (torch.arange(0, dim, 2).float() + 0.4 * dim) / (1.4 * dim),
+                             persistent=False)
 
     def forward(self, pos):
         freqs = pos.float()[:, None] * self.inv_freq[None, :]
         return torch.stack((freqs, freqs), dim=-1).reshape(pos.shape[0], -1)   # interleaved
+
+    def xpos(self, pos):
+        """The per-(position, channel) xPos factor for q (k takes its inverse), or None."""
+        if not self.use_xpos:
+            return None
+        power = (pos.float() - (int(pos.max()) + 1) // 2) / self.scale_base
+        sc = self.xpos_scale[None, :] ** power[:, None]
+        return torch.stack((sc, sc), dim=-1).reshape(pos.shape[0], -1)
 
 
 def rotate_half(x):
@@ -193,10 +222,10 @@ def rotate_half(x):
     return torch.stack((-x2, x1), dim=-1).reshape(*x.shape[:-2], -1)
 
 
-def apply_rotary(t, freqs):
+def apply_rotary(t, freqs, scale=1.):
     rot = freqs.shape[-1]
     tr, tu = t[..., :rot], t[..., rot:]
-    tr = tr * freqs.cos() + rotate_half(tr) * freqs.sin()
+    tr = tr * freqs.cos() * scale + rotate_half(tr) * freqs.sin() * scale
     return torch.cat((tr, tu), dim=-1)
 
 
@@ -206,10 +235,16 @@ class _Rearrange(nn.Module):
 
 
 class Attention(nn.Module):
-    def __init__(self, dim, heads, dim_head, dropout=0., gate_values=True, learned_value_residual_mix=False):
+    """``qk_norm`` (Decoder attn_qk_norm): q and k l2-normalised per head (F.normalize) after the
+    projections and before the rotary, the scores scaled by ``qk_norm_scale`` instead of dh ** -0.5
+    (x-transformers Attention qk_norm, qk_norm_groups = 1, no dim scale)."""
+
+    def __init__(self, dim, heads, dim_head, dropout=0., gate_values=True, learned_value_residual_mix=False,
+                 qk_norm=False, qk_norm_scale=10.):
         super().__init__()
         inner = heads * dim_head
         self.heads, self.dim_head = heads, dim_head
+        self.qk_norm, self.qk_norm_scale = qk_norm, qk_norm_scale
         self.to_q = nn.Linear(dim, inner, bias=False)
         self.to_k = nn.Linear(dim, inner, bias=False)
         self.to_v = nn.Linear(dim, inner, bias=False)
@@ -226,7 +261,7 @@ class Attention(nn.Module):
             nn.init.zeros_(self.to_value_residual_mix[0].weight)
             nn.init.zeros_(self.to_value_residual_mix[0].bias)
 
-    def forward(self, x, freqs, key_mask=None, cache_kv=None, value_residual=None):
+    def forward(self, x, freqs, key_mask=None, cache_kv=None, value_residual=None, xpos=None):
         b, n, _ = x.shape
         h, dh = self.heads, self.dim_head
         split = lambda t: t.reshape(b, n, h, dh).permute(0, 2, 1, 3)
@@ -238,13 +273,18 @@ class Attention(nn.Module):
                 v = v.lerp(value_residual, mix)
             else:
                 v = value_residual.lerp(v, mix)
+        scale = dh ** -0.5
+        if self.qk_norm:
+            q, k = F.normalize(q, dim=-1), F.normalize(k, dim=-1)
+            scale = self.qk_norm_scale
         if freqs is not None:
-            q, k = apply_rotary(q, freqs), apply_rotary(k, freqs)
+            xq, xk = (1., 1.) if xpos is None else (xpos, xpos ** -1.)
+            q, k = apply_rotary(q, freqs, xq), apply_rotary(k, freqs, xk)
         if cache_kv is not None:
             k = torch.cat((cache_kv[0], k), dim=-2)
             v = torch.cat((cache_kv[1], v), dim=-2)
         i, j = q.shape[-2], k.shape[-2]
-        sim = torch.einsum('bhid,bhjd->bhij', q, k) * dh ** -0.5
+        sim = torch.einsum('bhid,bhjd->bhij', q, k) * scale
         neg = -torch.finfo(sim.dtype).max
         causal = torch.ones((i, j), dtype=torch.bool, device=x.device).triu(j - i + 1)
         sim = sim.masked_fill(causal, neg)
@@ -343,32 +383,38 @@ class LayerIntermediates:
 class Decoder(nn.Module):
     def __init__(self, dim, depth, heads=8, attn_dim_head=64, rotary_pos_emb=False, attn_dropout=0.,
                  ff_dropout=0., verbose=True, attn_gate_values=False, add_value_residual=False,
-                 learned_value_residual_mix=False, ff_mult=4, ff_no_bias=False, ff_glu=False, **unsupported):
+                 learned_value_residual_mix=False, ff_mult=4, ff_no_bias=False, ff_glu=False, attn_qk_norm=False,
+                 attn_qk_norm_scale=10., rotary_xpos=False, rotary_xpos_scale_base=512., use_rmsnorm=False,
+                 **unsupported):
         super().__init__()
         if unsupported:
             raise NotImplementedError(f'restated Decoder does not model {sorted(unsupported)}')
         self.dim, self.depth, self.causal = dim, depth, True
         self.add_value_residual = add_value_residual
         self.layers = nn.ModuleList()
+        Norm = RMSNorm if use_rmsnorm else LayerNorm
         for ind in range(depth):
             attn = Attention(dim, heads, attn_dim_head, attn_dropout, attn_gate_values,
-                             learned_value_residual_mix=learned_value_residual_mix and add_value_residual and ind > 0)
-            self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]), attn, _Residual()]))
-            self.layers.append(nn.ModuleList([nn.ModuleList([LayerNorm(dim), None, None]),
+                             learned_value_residual_mix=learned_value_residual_mix and add_value_residual and ind > 0,
+                             qk_norm=attn_qk_norm, qk_norm_scale=attn_qk_norm_scale)
+            self.layers.append(nn.ModuleList([nn.ModuleList([Norm(dim), None, None]), attn, _Residual()]))
+            self.layers.append(nn.ModuleList([nn.ModuleList([Norm(dim), None, None]),
                                               FeedForward(dim, ff_mult, ff_dropout, ff_no_bias, ff_glu), _Residual()]))
-        self.rotary_pos_emb = RotaryEmbedding(attn_dim_head // 2) if rotary_pos_emb else None
-        self.final_norm = LayerNorm(dim)
+        self.rotary_pos_emb = RotaryEmbedding(attn_dim_head // 2, use_xpos=rotary_xpos,
+                                              scale_base=rotary_xpos_scale_base) if rotary_pos_emb else None
+        self.final_norm = Norm(dim)
 
     def forward(self, x, mask=None, cache: LayerIntermediates | None = None):
         n = x.shape[1]
         prev = 0 if cache is None else cache.cache_length
-        freqs = None
+        freqs = xpos = None
         if self.rotary_pos_emb is not None:
             if cache is not None and XT.rollout_rotary == 'absolute':
                 pos = torch.arange(prev, prev + n, device=x.device)
             else:
                 pos = torch.arange(n, device=x.device)
             freqs = self.rotary_pos_emb(pos)
+            xpos = self.rotary_pos_emb.xpos(pos)
         caches = iter(cache.attn_intermediates) if cache is not None else None
         new_caches = []
         first_values = None
@@ -378,7 +424,7 @@ class Decoder(nn.Module):
             if isinstance(block, Attention):
                 ckv = next(caches).cached_kv if caches is not None else None
                 out, kv, orig_v = block(xn, freqs, key_mask=mask, cache_kv=ckv,
-                                        value_residual=first_values if self.add_value_residual else None)
+                                        value_residual=first_values if self.add_value_residual else None, xpos=xpos)
                 if first_values is None:
                     first_values = orig_v
                 new_caches.append(_AttnCache(kv))

@@ -409,9 +409,11 @@ def test_ff_dropout_mask_is_host_philox_stream(p, layer):
 
 def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, episodes=8, batch=4, seed=3,
                  hazard=3, mode='lander', dim=48, reward_dropout=0.5, gene_dim=8, agent_extra=None, fractal_levels=None,
-                 ff_mult=4, genes=3, shard_by_gene=False, ff_no_bias=False, ff_glu=False):
+                 ff_mult=4, genes=3, shard_by_gene=False, ff_no_bias=False, ff_glu=False, wm_extra=None):
     """``fractal_levels``: the causal fractal policy body (policy_body='fractal') on both sides.
-    ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult)."""
+    ``ff_mult``: the feed-forward width through world_model['ff_mult'] (x-transformers' FeedForward mult).
+    ``wm_extra``: further world_model options (attn_qk_norm, attn_qk_norm_scale, rotary_xpos,
+    rotary_xpos_scale_base), given to the oracle's Decoder as well."""
     from xtrl_amd import Learner, SynthVecSim
     torch.manual_seed(seed)
     factory = None
@@ -428,6 +430,10 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
         wm['ff_glu'] = True
     if gates:
         wm.update(attn_gate_values=True, add_value_residual=True, learned_value_residual_mix=True)
+    wm.update(wm_extra or {})
+    names = dict(attn_qk_norm='qk_norm', attn_qk_norm_scale='qk_norm_scale', rotary_xpos='rotary_xpos',
+                 rotary_xpos_scale_base='xpos_scale_base', use_rmsnorm='rms_norm')
+    oracle_extra = {names[k]: v for k, v in (wm_extra or {}).items()}
     gp = dict(dim=gene_dim, num_genes_per_island=genes, num_selected=2, tournament_size=2)
     learner = Learner(state_dim=S, num_actions=A, reward_range=(-2., 2.), world_model=wm, max_timesteps=T,
                       batch_size=batch, num_episodes_per_update=episodes, evolutionary=evo, evolve_every=1,
@@ -447,7 +453,8 @@ def make_learner(S=8, A=4, depth=2, gates=True, evo=False, cont=False, T=12, epi
                         learned_mix=gates, continuous=cont, clamp=(-1., 1.) if cont else None, evolutionary=evo,
                         evolve_every=1, evolve_after_step=0, gene_pool=gp, max_timesteps=T, batch_size=batch,
                         num_episodes_per_update=episodes, sim_mode=mode, hazard_log2=hazard, seed=seed,
-                        reward_dropout=reward_dropout, ff_mult=ff_mult, ff_no_bias=ff_no_bias, ff_glu=ff_glu)
+                        reward_dropout=reward_dropout, ff_mult=ff_mult, ff_no_bias=ff_no_bias, ff_glu=ff_glu,
+                        **oracle_extra)
     sd = {k: v.detach().cpu() for k, v in learner.agent.model.state_dict().items()}
     genes = learner.agent.gene_pool.genes.clone() if evo else None
     oracle = R.OracleLearner(c, init_state_dict=sd, genes=genes, model_factory=factory)
@@ -1318,6 +1325,64 @@ def test_ff_glu_rollout_and_learn_match_oracle(dim, gates, no_bias, dropout):
     compare_rollout(traj, lens, episodes_o)
     seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2, dropout=dropout)
     assert len(seen) == 2
+
+
+@pytest.mark.parametrize('opts', [dict(attn_qk_norm=True), dict(rotary_xpos=True, rotary_xpos_scale_base=16.),
+                                  dict(attn_qk_norm=True, attn_qk_norm_scale=6., rotary_xpos=True)],
+                         ids=['qk_norm', 'xpos', 'qk_norm_scale6_xpos'])
+def test_world_model_qk_norm_xpos_rollout_and_learn_match_oracle(opts, decode_path):
+    """world_model['attn_qk_norm'] (q, k l2-normalised per head before the rotary, scores x
+    qk_norm_scale) and world_model['rotary_xpos'] (the xPos scale of the rotary channels: q times,
+    k divided by ((j + 0.4 rot) / (1.4 rot)) ^ ((pos - n // 2) / scale_base); a small scale base so
+    the factors are far from 1 at T = 24): the rollout (decode attention of both decode paths; the
+    reference's cached decode rotates at position 0, where xPos is the identity) and the fused learn
+    step (k_qkv_prep / k_qkv_prep_bwd with the l2-norm and xPos terms, the attention scale) against
+    the oracle's restated x-transformers Attention / RotaryEmbedding."""
+    learner, env, oracle = make_learner(depth=2, gates=True, T=24, episodes=6, batch=3, seed=6, hazard=5,
+                                        wm_extra=opts)
+    c = learner.agent.cfg
+    assert c.qk_norm == bool(opts.get('attn_qk_norm')) and c.rotary_xpos == bool(opts.get('rotary_xpos'))
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 24)
+    torch.cuda.synchronize()
+    episodes_o, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    assert int(lens.max()) > 10
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2)
+    assert len(seen) == 2
+
+
+@pytest.mark.parametrize('dim,T', [(48, 24), (256, 40)])
+def test_world_model_rmsnorm_rollout_and_learn_match_oracle(dim, T, decode_path):
+    """world_model['use_rmsnorm'] (x-transformers RMSNorm, F.normalize(x) sqrt(d) g, parameter .g,
+    for every pre-norm and the final norm): the rollout — the embedding's layer-0 norm, the fused
+    attention's FF norm, k_mlp's next norm (d 256), the decode GEMM prologues, the row-resident step's
+    norms (d 48) — and the fused learn step (the norm epilogues of the GEMMs completing their rows and
+    their backward, the embedding's pre-norm, the final norm) against the oracle's restated RMSNorm."""
+    learner, env, oracle = make_learner(depth=2, gates=True, T=T, episodes=6, batch=3, seed=8, hazard=4, dim=dim,
+                                        wm_extra=dict(use_rmsnorm=True))
+    names = [n for n, _ in learner.agent.model.named_parameters()]
+    assert 'transformer.attn_layers.final_norm.g' in names and not any(n.endswith('.gamma') for n in names)
+    traj, lens, genes, cum = learner.rollout_device(env, 0, T)
+    torch.cuda.synchronize()
+    episodes_o, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2)
+    assert len(seen) == 2
+
+
+def test_rotary_absolute_rollout_with_xpos_matches_oracle(monkeypatch):
+    """The decision-log alternative rotary_abs_rollout=True (absolute positions in the cached
+    decode) with rotary_xpos and attn_qk_norm: the decode kernels' rotation at position t with the
+    xPos factor of a t + 1 long input, against the oracle's Decoder in 'absolute' rollout mode."""
+    monkeypatch.setattr(tp.XT, 'rollout_rotary', 'absolute')
+    learner, env, oracle = make_learner(depth=2, gates=True, T=16, episodes=6, batch=3, seed=7, hazard=4,
+                                        wm_extra=dict(rotary_xpos=True, rotary_xpos_scale_base=8., attn_qk_norm=True),
+                                        agent_extra=dict(rotary_abs_rollout=True))
+    traj, lens, _, _ = learner.rollout_device(env, 0, 16)
+    torch.cuda.synchronize()
+    episodes_o, _ = oracle.rollout(0)
+    compare_rollout(traj, lens, episodes_o)
+    assert int(lens.max()) > 8
 
 
 def test_c3_shape_rollout_and_learn_match_oracle():

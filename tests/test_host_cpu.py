@@ -278,6 +278,16 @@ def test_world_model_options_defaults_accepted_others_named():
     assert len(proj) == 1 and tuple(g[proj[0]].shape) == (2 * 4 * 16, 16)
     assert tuple(g[proj[0].replace('weight', 'bias')].shape) == (2 * 4 * 16,)
     assert not any(k.endswith('ff.0.0.weight') for k in g)
-    for opt in (dict(ff_swish=True), dict(attn_qk_norm=True), dict(use_rmsnorm=True), dict(attn_kv_heads=2)):
+    for opt in (dict(ff_swish=True), dict(macaron=True), dict(use_scalenorm=True), dict(attn_kv_heads=2)):
         with pytest.raises(NotImplementedError, match=next(iter(opt))):
             Learner(5, 2, (-1., 1.), world_model=dict(base, **opt), **kw)
+    with pytest.raises(AssertionError, match='causality'):   # x-transformers Decoder refuses the flag
+        Learner(5, 2, (-1., 1.), world_model=dict(base, causal=True), **kw)
+    # attn_qk_norm / rotary_xpos build the same parameters (the qk norm has no dim scale, the xPos
+    # table is not a parameter)
+    q = Learner(5, 2, (-1., 1.), world_model=dict(base, attn_qk_norm=True, rotary_xpos=True), **kw)
+    assert list(q.agent.model.state_dict()) == list(b.agent.model.state_dict())
+    assert q.agent.cfg.qk_norm and q.agent.cfg.rotary_xpos and q.agent.cfg.qk_norm_scale == 10.
+    # use_rmsnorm: x-transformers RMSNorm's gain is named g (LayerNorm's gamma)
+    r = Learner(5, 2, (-1., 1.), world_model=dict(base, use_rmsnorm=True), **kw).agent.model.state_dict()
+    assert [k.replace('.gamma', '.g') for k in b.agent.model.state_dict()] == list(r)

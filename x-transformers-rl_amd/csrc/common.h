@@ -116,6 +116,12 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // activations, written the way PyTorch's CPU kernels evaluate them
+// x-transformers pre-norms: LayerNorm (no affine, eps 1e-5; sq = the centred second moment) or,
+// rms (Decoder use_rmsnorm), RMSNorm = F.normalize(x, eps 1e-12) sqrt(d) (the caller takes mean 0, so
+// sq = the raw sum of squares) — the row's multiplier either way: y = (x - mean) * rstd * g
+__device__ __forceinline__ float norm_rstd(float sq, float d, bool rms) {
+  return rms ? sqrtf(d) / fmaxf(sqrtf(sq), 1e-12f) : 1.0f / sqrtf(sq / d + 1e-5f);
+}
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float geluf_(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float siluf_(float x) { return x / (1.0f + expf(-x)); }

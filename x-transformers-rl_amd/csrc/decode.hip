@@ -252,14 +252,14 @@ __global__ __launch_bounds__(1024) void k_embed(const XtrlDecodeDesc D, int t, c
     float sm = 0.f;
 #pragma unroll
     for (int k = 0; k < NC; ++k) sm += lane + 64 * k < d ? xo[k] : 0.f;
-    const float mean = wave_sum_dpp(sm) / (float)d;
+    const float mean = D.rms_norm ? 0.f : wave_sum_dpp(sm) / (float)d;
     float qq = 0.f;
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const float dl = xo[k] - mean;
       qq += lane + 64 * k < d ? dl * dl : 0.f;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+    const float rstd = norm_rstd(wave_sum_dpp(qq), (float)d, D.rms_norm);
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       const int c = lane + 64 * k;
@@ -293,6 +293,37 @@ __device__ __forceinline__ float kpi_sum(float v) {
 // FrPost (fractal body, g1 non-NULL): the fused tail forms the post-norm rows instead —
 // out = LN2(LN1(x + attn W_out^T) g1 + b1 + c[r] ) g2 + b2 (nn.LayerNorm, eps), x itself is not
 // stored (nothing reads it) and no pre-norm is written
+// x-transformers qk norm of the new token's q and k (F.normalize over the head's DH channels, eps
+// 1e-12): lane c = lane % DH holds channel c, a head's DH channels on DH aligned lanes
+template <int DH>
+__device__ __forceinline__ void qk_l2norm(float& q, float& k) {
+  float sq = q * q, sk = k * k;
+#pragma unroll
+  for (int o = DH / 2; o > 0; o >>= 1) {
+    sq += __shfl_xor(sq, o, 64);
+    sk += __shfl_xor(sk, o, 64);
+  }
+  q = q / fmaxf(sqrtf(sq), 1e-12f);
+  k = k / fmaxf(sqrtf(sk), 1e-12f);
+}
+
+// rotary at absolute position t of channel c (< rot_dim; pairs on adjacent lanes), with the xPos scale
+// of an input whose last position is t (max_pos = t + 1): q times, k divided by the pair's factor
+__device__ __forceinline__ void rotary_row(const XtrlDecodeDesc& D, int t, int c, float& q, float& k) {
+  const float f = (float)t * D.inv_freq[c >> 1];
+  const float cs = cosf(f), sn = sinf(f);
+  const float qp = __shfl_xor(q, 1, 64), kp = __shfl_xor(k, 1, 64);
+  const float sgn = (c & 1) ? 1.f : -1.f;   // rotate_half: (-x2, x1)
+  q = q * cs + (sgn * qp) * sn;
+  k = k * cs + (sgn * kp) * sn;
+  if (D.xpos_base > 0.f) {
+    const float rot = (float)D.rot_dim;
+    const float xf = powf(((float)(c & ~1) + 0.4f * rot) / (1.4f * rot), (float)(t - (t + 1) / 2) / D.xpos_base);
+    q *= xf;
+    k *= 1.0f / xf;
+  }
+}
+
 struct FrPost {
   const float *g1 = nullptr, *b1 = nullptr, *g2 = nullptr, *b2 = nullptr, *c = nullptr;
   int ldc = 0;
@@ -386,15 +417,9 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
       v = lerpf_(v, v1v, sigmoidf_(mixv));
     }
   }
+  if (D.qk_norm) qk_l2norm<DH>(q, k);
   // rotary (interleaved pairs on the first rot_dim channels); 'zero' mode = position 0 = identity
-  if (D.rotary_abs && c < D.rot_dim) {
-    const float f = (float)t * D.inv_freq[c >> 1];
-    const float cs = cosf(f), sn = sinf(f);
-    const float qp = __shfl_xor(q, 1, 64), kp = __shfl_xor(k, 1, 64);
-    const float sgn = (c & 1) ? 1.f : -1.f;   // rotate_half: (-x2, x1)
-    q = q * cs + (sgn * qp) * sn;
-    k = k * cs + (sgn * kp) * sn;
-  }
+  if (D.rotary_abs && c < D.rot_dim) rotary_row(D, t, c, q, k);
   if (g == 0) {
     qs[c] = q;
     ks[c] = k;
@@ -403,7 +428,7 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
     Ly.v_cache[cache_base + (int64_t)t * DH + c] = v;
   }
   wave_sync();
-  const float scale = 1.0f / sqrtf((float)DH);
+  const float scale = D.attn_scale > 0.f ? D.attn_scale : 1.0f / sqrtf((float)DH);
   float qreg[DH];
 #pragma unroll
   for (int i = 0; i < DH; ++i) qreg[i] = qs[i];
@@ -572,7 +597,7 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
           if (n < d) *reinterpret_cast<float4*>(fp.out + (int64_t)r * d + n) = y[j];
         }
       } else if (D.xn) {
-        const float mean = wave_sum_dpp(sm) / (float)d;
+        const float mean = D.rms_norm ? 0.f : wave_sum_dpp(sm) / (float)d;
         float qq = 0.f;
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
@@ -581,7 +606,7 @@ __global__ __launch_bounds__(FJ > 0 ? 512 : 256) void k_attn_decode(const XtrlDe
             qq += (dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w);
           }
         }
-        const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+        const float rstd = norm_rstd(wave_sum_dpp(qq), (float)d, D.rms_norm);
 #pragma unroll
         for (int j = 0; j < FJ; ++j) {
           const int n = 4 * lane + 256 * j;
@@ -1262,14 +1287,14 @@ __global__ __launch_bounds__(256, EW ? 1 : 2) void k_mlp(const XtrlDecodeDesc D,
       xv[j] = A1[r * LDA + lane + 64 * j];
       sm += xv[j];
     }
-    const float mean = wave_sum_dpp(sm) / (float)d;
+    const float mean = D.rms_norm ? 0.f : wave_sum_dpp(sm) / (float)d;
     float qq = 0.f;
 #pragma unroll
     for (int j = 0; j < NT2; ++j) {
       const float dl = xv[j] - mean;
       qq += dl * dl;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+    const float rstd = norm_rstd(wave_sum_dpp(qq), (float)d, D.rms_norm);
     if (m < M)
 #pragma unroll
       for (int j = 0; j < NT2; ++j)
@@ -1385,7 +1410,7 @@ int dproj(const XtrlDecodeDesc* D, int t, const float* A, int lda, const float* 
           const int32_t* row_map2 = nullptr) {
   DGemmArgs g;
   g.n_split = n_split; g.C2 = C2; g.ldc2 = ldc2; g.row_map2 = row_map2;
-  g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias; g.gamma = gamma; g.ln_k = ln_k;
+  g.A = A; g.lda = lda; g.W = W; g.ldw = K; g.bias = bias; g.gamma = gamma; g.ln_k = ln_k; g.ln_rms = D->rms_norm;
   g.R = R; g.ldr = ldr; g.C = C; g.ldc = ldc; g.row_map = row_map;
   g.m_dev = D->live_count + (t & 1);
   g.M = D->E; g.N = N; g.K = K;
@@ -1691,7 +1716,7 @@ __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT,
 }
 
 // out[c] = LayerNorm(x)[c] * g[c] (x-transformers: no affine, eps 1e-5, two-pass) by wave 0; d <= 256
-__device__ __forceinline__ void row_layernorm(const float* x, const float* g, int d, float* out) {
+__device__ __forceinline__ void row_layernorm(const float* x, const float* g, int d, float* out, bool rms) {
   const int tid = threadIdx.x;
   if (tid < 64) {
     float v[4], sm = 0.f;
@@ -1701,14 +1726,14 @@ __device__ __forceinline__ void row_layernorm(const float* x, const float* g, in
       v[k] = c < d ? x[c] : 0.f;
       sm += v[k];
     }
-    const float mean = wave_sum_dpp(sm) / (float)d;
+    const float mean = rms ? 0.f : wave_sum_dpp(sm) / (float)d;
     float qq = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float dl = v[k] - mean;
       qq += tid + 64 * k < d ? dl * dl : 0.f;
     }
-    const float rstd = 1.0f / sqrtf(wave_sum_dpp(qq) / (float)d + 1e-5f);
+    const float rstd = norm_rstd(wave_sum_dpp(qq), (float)d, rms);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int c = tid + 64 * k;
@@ -1796,7 +1821,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   if (blockIdx.x == 0 && tid == 0) D.live_count[t & 1] = n_live;
   const int n_act = D.continuous ? 2 * D.A : D.A;
   const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
-  const float scale = 1.0f / sqrtf((float)DH);
+  const float scale = D.attn_scale > 0.f ? D.attn_scale : 1.0f / sqrtf((float)DH);
   constexpr int F4 = DH / 4, LPK = DH / 4, KPI = 64 / LPK;   // P.V: lanes per key row, key rows per wave pass
   // workgroups per row (uniform): 4, 2 or 1 — a divisor of 4 d / 4 hidden units — with rows x Ge <= 256
   const int Ge = min(G, n_live <= ROW_CUS / 4 ? 4 : (n_live <= ROW_CUS / 2 ? 2 : 1));
@@ -1840,7 +1865,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
     // ---- decoder layers
     for (int l = 0; l < L; ++l) {
       const XtrlDecodeLayer& Ly = D.layers_dev[l];   // (device copy: scalar loads, no kernel-argument array)
-      row_layernorm(xs, Ly.ln_attn, d, xn);
+      row_layernorm(xs, Ly.ln_attn, d, xn, D.rms_norm);
       row_gemv<0>(xn, d, Ly.w_qkv_t, nq4, Ly.b_qkv, nq4, qkv, part);
       // attention: head h on wave h (waves past H idle); k_attn_decode's arithmetic and lane roles
       for (int h = w; h < H; h += ROW_T / 64) {
@@ -1857,14 +1882,8 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
             v = lerpf_(v, v1s[h * DH + c], sigmoidf_(qkv[3 * I + (D.gate_values ? I : 0) + h]));
           }
         }
-        if (D.rotary_abs && c < D.rot_dim) {
-          const float f = (float)t * D.inv_freq[c >> 1];
-          const float cs = cosf(f), sn = sinf(f);
-          const float qp = __shfl_xor(q, 1, 64), kp = __shfl_xor(k, 1, 64);
-          const float sgn = (c & 1) ? 1.f : -1.f;
-          q = q * cs + (sgn * qp) * sn;
-          k = k * cs + (sgn * kp) * sn;
-        }
+        if (D.qk_norm) qk_l2norm<DH>(q, k);
+        if (D.rotary_abs && c < D.rot_dim) rotary_row(D, t, c, q, k);
         const int64_t cb = ((int64_t)e * H + h) * D.Tmax * DH;
         if (g == 0) {
           if (lead) {
@@ -1960,12 +1979,12 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
       __syncthreads();
       // out-projection + residual (W_out^T is k-major), then FF: LN, FF1 + GELU, FF2 + residual
       row_gemv<0>(att, I, Ly.w_out_t, d, nullptr, d, xs, part, xs);
-      row_layernorm(xs, Ly.ln_ff, d, xn);
+      row_layernorm(xs, Ly.ln_ff, d, xn, D.rms_norm);
       row_gemv<1>(xn, d, Ly.w_ff1_t, ff, Ly.b_ff1, ff, hs, part);
       row_gemv<0>(hs, ff, Ly.w_ff2_t, d, Ly.b_ff2, d, xs, part, xs);
     }
     // ---- heads: [final LN(x) | state embed | latent] -> SiLU hidden -> block-diagonal last layer
-    row_layernorm(xs, D.ln_final, d, ac);
+    row_layernorm(xs, D.ln_final, d, ac, D.rms_norm);
     const int hw = 4 * d / Ge, hc0 = gs * hw;   // this workgroup's hidden units
     row_gemv<2>(ac, D.in_dim, D.w_h1_t + hc0, 4 * d, D.b_h1 + hc0, hw, hs, part);
     float* out2 = part + ROW_PART;
@@ -2099,7 +2118,7 @@ int fractal_decode_step(const XtrlDecodeDesc* D, const XtrlFractalDesc* F, int t
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(F && F->level && F->levels == D->L && F->levels > 0, "fractal_decode: levels mismatch");
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "fractal_decode: t=%d outside [0, %d)", t, D->Tmax);
-  XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs &&
+  XTRL_REQUIRE(D->state_only && !D->gate_values && !D->value_residual && !D->rotary_abs && !D->qk_norm &&
                    D->n_qkv == 3 * D->H * D->dh && D->d <= 64 * FR_MAXF,
                "fractal_decode: the descriptor must describe plain attention (n_qkv = 3 I) with state_only = 1");
   XTRL_REQUIRE(F->g_init && F->c0 && F->g && F->c2 && F->tmp && F->x2 && F->mean && F->allf && F->hagg,

@@ -133,7 +133,7 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
   hook.landed();
 
   if constexpr (LN) {
-    // x-transformers LayerNorm of columns [0, ln_k): mean, then the centred second moment.  TPR
+    // x-transformers LayerNorm (ln_rms: RMSNorm) of columns [0, ln_k): mean, then the centred second moment.  TPR
     // threads per row (all 256 threads at once), each holding float4s sub + TPR i of the row in
     // registers; butterflies over the TPR lanes of the row.
     constexpr int TPR = 256 / BM, MAXF = 128 / TPR;   // ln_k <= 512
@@ -152,7 +152,7 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
     }
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) sm += __shfl_xor(sm, o, 64);
-    const float mean = sm / D;
+    const float mean = a.ln_rms ? 0.f : sm / D;
     float qq = 0.f;
 #pragma unroll
     for (int i = 0; i < MAXF; ++i) {
@@ -163,7 +163,7 @@ __device__ __forceinline__ void dgemm_body(const DGemmArgs& a, float* As, Hook& 
     }
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) qq += __shfl_xor(qq, o, 64);
-    const float rstd = 1.0f / sqrtf(qq / D + 1e-5f);
+    const float rstd = norm_rstd(qq, D, a.ln_rms);
 #pragma unroll
     for (int i = 0; i < MAXF; ++i) {
       const int f = sub + TPR * i;

@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
         }
 #pragma unroll
         for (int q = 0; q < RB; ++q) {
-          const float mean = wave_sum(s[q]) / (float)K;
+          const float mean = a.ln_rms ? 0.f : wave_sum(s[q]) / (float)K;
           float sq = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
                     ((x.z - mean) * (x.z - mean) + (x.w - mean) * (x.w - mean));
             }
           }
-          const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+          const float rstd = norm_rstd(wave_sum(sq), (float)K, a.ln_rms);
           if (lane == 0 && r0 + q < BM) {
             row_mean[r0 + q] = mean;
             row_rstd[r0 + q] = rstd;
@@ -405,13 +405,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK, (X6 && EPI != EPI_DGATE) ? 2 : 1
           const float* xr = a.A + (int64_t)m * a.lda;
           float s = 0.f;
           for (int k = lane; k < K; k += 64) s += xr[k];
-          mean = wave_sum(s) / (float)K;
+          mean = a.ln_rms ? 0.f : wave_sum(s) / (float)K;
           float q = 0.f;
           for (int k = lane; k < K; k += 64) {
             const float dlt = xr[k] - mean;
             q += dlt * dlt;
           }
-          rstd = 1.0f / sqrtf(wave_sum(q) / (float)K + 1e-5f);
+          rstd = norm_rstd(wave_sum(q), (float)K, a.ln_rms);
         }
         if (lane == 0) {
           row_mean[r] = mean;
@@ -803,10 +803,11 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
       x.x = (v[rr].x + bia.x) + r[rr].x; x.y = (v[rr].y + bia.y) + r[rr].y;
       x.z = (v[rr].z + bia.z) + r[rr].z; x.w = (v[rr].w + bia.w) + r[rr].w;
       if (!cok) x = z4;
-      const float mean = wave_sum((x.x + x.y) + (x.z + x.w)) * inv_n;
+      const float mean = a.ln_rms ? 0.f : wave_sum((x.x + x.y) + (x.z + x.w)) * inv_n;
       float4 dl = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
       if (!cok) dl = z4;
-      const float rstd = 1.0f / sqrtf(wave_sum((dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w)) * inv_n + 1e-5f);
+      const float sq = wave_sum((dl.x * dl.x + dl.y * dl.y) + (dl.z * dl.z + dl.w * dl.w));
+      const float rstd = a.ln_rms ? norm_rstd(sq, (float)N, true) : 1.0f / sqrtf(sq * inv_n + 1e-5f);
       float4 y = make_float4((dl.x * rstd) * gam.x, (dl.y * rstd) * gam.y, (dl.z * rstd) * gam.z,
                              (dl.w * rstd) * gam.w);
       if (a.ln_b) y = make_float4(y.x + beta.x, y.y + beta.y, y.z + beta.z, y.w + beta.w);
@@ -855,7 +856,8 @@ __device__ __forceinline__ void ln_epilogue(const GemmArgs& a, f32x16 (&acc)[2][
         dg.x += g[rr].x * xh.x; dg.y += g[rr].y * xh.y; dg.z += g[rr].z * xh.z; dg.w += g[rr].w * xh.w;
         if constexpr (X) { db.x += g[rr].x; db.y += g[rr].y; db.z += g[rr].z; db.w += g[rr].w; }
       }
-      const float ma = wave_sum((gm.x + gm.y) + (gm.z + gm.w)) * inv_n;
+      // (RMSNorm: no mean in the forward, so no mean(g gamma) term: dx = rstd (g gamma - x^ mean(g gamma x^)))
+      const float ma = a.ln_rms ? 0.f : wave_sum((gm.x + gm.y) + (gm.z + gm.w)) * inv_n;
       const float mb = wave_sum((gm.x * xh.x + gm.y * xh.y) + (gm.z * xh.z + gm.w * xh.w)) * inv_n;
       float4 o;
       o.x = rs * (gm.x - ma - xh.x * mb);

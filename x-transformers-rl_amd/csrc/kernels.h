@@ -64,6 +64,7 @@ struct GemmArgs {
   int xcd_remap = 0;              // 1: workgroup ids permuted so each XCD runs consecutive tiles
   // LayerNorm epilogues (EPI_RES_LN / EPI_LN_BWD)
   const float* ln_g = nullptr;    // gamma [N]
+  int ln_rms = 0;                 // LN prologue / RES_LN / LN_BWD: x-transformers RMSNorm (use_rmsnorm), mean 0
   const float* ln_b = nullptr;    // RES_LN: beta [N] (nn.LayerNorm bias; x-transformers LayerNorm has none)
   const float* ln_b2 = nullptr;   // RES_LN: ln_y2 = LN(C) * ln_g (+ ln_b) + ln_b2 (the next level's input)
   float* ln_y1 = nullptr; int ln_ld1 = 0;   // RES_LN: normalised rows (ln_y2 optional: a second copy)
@@ -138,6 +139,7 @@ struct DGemmArgs {
   const float* W = nullptr; int ldw = 0;
   const float* bias = nullptr;
   const float* gamma = nullptr; int ln_k = 0;
+  int ln_rms = 0;   // the prologue norm is x-transformers' RMSNorm (use_rmsnorm), not its LayerNorm
   const float* R = nullptr; int ldr = 0;
   float* C = nullptr; int ldc = 0;
   const int32_t* row_map = nullptr;

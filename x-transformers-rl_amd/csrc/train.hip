@@ -32,6 +32,7 @@ struct EmbedArgs {
   float keep;
   const float* ln_g;   // (k_embed_ln) layer 0's attention pre-norm: gamma, output rows, (mean, rstd)
   float *xn, *st;
+  int rms;             // the pre-norm is x-transformers' RMSNorm (use_rmsnorm)
 };
 
 constexpr int EMB_TOK = 32, EMB_U = 8, EMB_MAXS = 32;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
     float mean[EMB_U], dl[EMB_U];
 #pragma unroll
     for (int u = 0; u < EMB_U; ++u) {
-      mean[u] = ((red[0][0][u] + red[0][1][u]) + (red[0][2][u] + red[0][3][u])) * inv_d;
+      mean[u] = a.rms ? 0.f : ((red[0][0][u] + red[0][1][u]) + (red[0][2][u] + red[0][3][u])) * inv_d;
       dl[u] = on ? x[u] - mean[u] : 0.f;
       const float q = wave_sum(dl[u] * dl[u]);
       if (lane == 0) red[1][w][u] = q;
@@ -176,7 +177,8 @@ __global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
     for (int u = 0; u < EMB_U; ++u) {
       const int t = t0 + u;
       if (t >= a.T) break;
-      const float rstd = 1.0f / sqrtf(((red[1][0][u] + red[1][1][u]) + (red[1][2][u] + red[1][3][u])) * inv_d + 1e-5f);
+      const float sq = (red[1][0][u] + red[1][1][u]) + (red[1][2][u] + red[1][3][u]);
+      const float rstd = a.rms ? norm_rstd(sq, (float)a.d, true) : 1.0f / sqrtf(sq * inv_d + 1e-5f);
       if (on) {
         a.x0[(int64_t)t * a.d + c] = x[u];
         a.xn[(int64_t)t * a.d + c] = (dl[u] * rstd) * gam;
@@ -206,7 +208,7 @@ __global__ void k_latent_embed(const float* latent, const float* w, const float*
 // ---- LayerNorm (x-transformers: layer_norm without affine, eps 1e-5, times gamma) ------------
 // one wave per row; y written to y1 (and y2 when given); stats = (mean, rstd)
 __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gamma, float* y1, int ld1, float* y2,
-                                                int ld2, float* stats, int T, int d) {
+                                                int ld2, float* stats, int T, int d, int rms) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < kMaxDPerLane; ++k) s += v[k];
-  const float mean = wave_sum(s) / (float)d;
+  const float mean = rms ? 0.f : wave_sum(s) / (float)d;
   float q = 0.f;
 #pragma unroll
   for (int k = 0; k < kMaxDPerLane; ++k) {
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(const float* x, const float* gam
     const float dl = c < d ? v[k] - mean : 0.f;
     q += dl * dl;
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
+  const float rstd = norm_rstd(wave_sum(q), (float)d, rms);
 #pragma unroll
   for (int k = 0; k < kMaxDPerLane; ++k) {
     const int c = lane + 64 * k;
@@ -256,7 +258,8 @@ template <int DPL>
 __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int ldg1, float s1, const float* g2,
                                                           int ldg2, const float* x, const float* stats,
                                                           const float* gamma, const float* dres, float* dx,
-                                                          float* part, float* part_b, int pstride, int T, int d) {
+                                                          float* part, float* part_b, int pstride, int T, int d,
+                                                          int rms) {
   __shared__ float red[LN_WAVES][64 * DPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gam[DPL], dg[DPL], db[DPL];
@@ -304,7 +307,8 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_ln_bwd(const float* g1, int l
         sa += gm[k];
         sb += gm[k] * xh[k];
       }
-      const float ma = wave_sum(sa) / (float)d, mb = wave_sum(sb) / (float)d;
+      // (RMSNorm: no mean in the forward, no mean(g gamma) term in the backward)
+      const float ma = rms ? 0.f : wave_sum(sa) / (float)d, mb = wave_sum(sb) / (float)d;
       if (t < T) {
 #pragma unroll
         for (int k = 0; k < DPL; ++k) {
@@ -350,7 +354,25 @@ struct PrepArgs {
   float* qkv;           // [T][3I]
   const float* inv_freq;
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col;   // mix_col < 0: no mix
+  int qk_norm;          // x-transformers qk norm: q, k l2-normalised per head before the rotary
+  float xpos_base;      // rotary xPos scale base (0: off)
 };
+
+// x-transformers RotaryEmbedding(use_xpos): rotated pair j (even channel) at position pos of an n-token
+// sequence is scaled by ((j + 0.4 rot) / (1.4 rot)) ^ ((pos - n / 2) / scale_base) for q, by its
+// inverse for k (x_transformers.RotaryEmbedding.forward / apply_rotary_pos_emb)
+__device__ __forceinline__ float xpos_factor(int j, int rot, int pos, int n, float base) {
+  const float sc = ((float)j + 0.4f * (float)rot) / (1.4f * (float)rot);
+  return powf(sc, (float)(pos - n / 2) / base);
+}
+
+// the per-head l2 norm of a (q or k) channel pair: the head's dh / 2 pairs sit on consecutive,
+// aligned lanes (every lane of the group active); F.normalize: x / max(||x||, 1e-12)
+__device__ __forceinline__ float head_norm(float2 x, int dh) {
+  float ss = x.x * x.x + x.y * x.y;
+  for (int o = dh >> 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  return fmaxf(sqrtf(ss), 1e-12f);
+}
 
 // grid (pair blocks, n steps, b episodes), PREP_T threads: token and position come from the grid
 // (no 64-bit division per element); one sincosf per rotated pair
@@ -361,15 +383,26 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep(const PrepArgs a) {
   if (pair >= P) return;
   const int pos = blockIdx.y, t = blockIdx.z * a.n + pos, col = 2 * pair;
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
-  const float2 x = *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col);
+  float2 x = *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col);
   float2 y;
   if (seg < 2) {
+    if (a.qk_norm) {
+      const float nrm = head_norm(x, a.dh);
+      x.x = x.x / nrm;
+      x.y = x.y / nrm;
+    }
     if (j < a.rot_dim) {
       const float f = (float)pos * a.inv_freq[j >> 1];
       float sn, cs;
       sincosf(f, &sn, &cs);
       y.x = x.x * cs + (-x.y) * sn;
       y.y = x.y * cs + x.x * sn;
+      if (a.xpos_base > 0.f) {
+        const float xf = xpos_factor(j, a.rot_dim, pos, a.n, a.xpos_base);
+        const float sf = seg == 0 ? xf : 1.0f / xf;
+        y.x *= sf;
+        y.y *= sf;
+      }
     } else {
       y = x;
     }
@@ -395,6 +428,8 @@ struct PrepBwdArgs {
   float* dvfirst;       // [T][I]
   const float* inv_freq;
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col, first_layer, accumulate;
+  int qk_norm;
+  float xpos_base;
 };
 
 __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
@@ -406,6 +441,7 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
   float* g = a.dproj + (int64_t)t * a.n_qkv + col;
   float dm = 0.f, m = 0.f;
+  float2 gqk = make_float2(0.f, 0.f);   // q / k: the gradient w.r.t. the (normalised) pre-rotary pair
   if (valid) {
     float2 gv = *reinterpret_cast<float2*>(g);
     if (seg < 2) {
@@ -413,11 +449,18 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
         const float f = (float)pos * a.inv_freq[j >> 1];
         float sn, cs;
         sincosf(f, &sn, &cs);
-        const float g0 = gv.x, g1 = gv.y;
+        float g0 = gv.x, g1 = gv.y;
+        if (a.xpos_base > 0.f) {
+          const float xf = xpos_factor(j, a.rot_dim, pos, a.n, a.xpos_base);
+          const float sf = seg == 0 ? xf : 1.0f / xf;
+          g0 *= sf;
+          g1 *= sf;
+        }
         gv.x = g0 * cs + g1 * sn;
         gv.y = g1 * cs + (-g0) * sn;
-        *reinterpret_cast<float2*>(g) = gv;
+        if (!a.qk_norm) *reinterpret_cast<float2*>(g) = gv;
       }
+      gqk = gv;
     } else {
       float2* dvf = reinterpret_cast<float2*>(a.dvfirst + (int64_t)t * a.I + within);
       if (a.mix_col >= 0) {
@@ -444,6 +487,27 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
         gv.y += o.y;
         *reinterpret_cast<float2*>(g) = gv;
       }
+    }
+  }
+  if (a.qk_norm) {   // l2-norm backward of q, k: dx = (g - x^ (x^ . g)) / ||x||  (every lane shuffles)
+    const float2 x = valid ? *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col) : make_float2(0.f, 0.f);
+    float ss = x.x * x.x + x.y * x.y;
+    for (int o = a.dh >> 2; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    const float r = sqrtf(ss), nrm = fmaxf(r, 1e-12f);
+    const float hx = x.x / nrm, hy = x.y / nrm;
+    const float2 gg = gqk;
+    float dot = hx * gg.x + hy * gg.y;
+    for (int o = a.dh >> 2; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+    if (valid && seg < 2) {
+      float2 dx;
+      if (r >= 1e-12f) {
+        dx.x = (gg.x - hx * dot) / nrm;
+        dx.y = (gg.y - hy * dot) / nrm;
+      } else {
+        dx.x = gg.x / nrm;
+        dx.y = gg.y / nrm;
+      }
+      *reinterpret_cast<float2*>(g) = dx;
     }
   }
   if (a.mix_col >= 0) {   // every lane takes part in the shuffles (groups of dh / 2 aligned lanes)
@@ -970,7 +1034,7 @@ int colsum(const Ctx& c, const float* src, int ld, int rows, int cols, float* ds
 
 int ln_fwd(const Ctx& c, const float* x, const float* gamma, float* y1, int ld1, float* y2, int ld2, float* st) {
   hipLaunchKernelGGL(k_ln_fwd, dim3(blocks(c.T, 4)), dim3(256), 0, c.s, x, gamma, y1, ld1, y2, ld2, st, c.T,
-                     c.D->d);
+                     c.D->d, c.D->rms_norm);
   XTRL_LAUNCHED("train ln_fwd");
   return XTRL_OK;
 }
@@ -985,10 +1049,10 @@ int ln_bwd(const Ctx& c, const float* g1, int ldg1, float s1, const float* g2, i
   float* pb = dbeta ? c.D->part + d : nullptr;
   const dim3 g(nb), bl(64 * LN_WAVES);
   float* P = c.D->part;
-  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
-  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
-  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
-  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d);
+  if (d <= 64) hipLaunchKernelGGL(k_ln_bwd<1>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d, c.D->rms_norm);
+  else if (d <= 128) hipLaunchKernelGGL(k_ln_bwd<2>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d, c.D->rms_norm);
+  else if (d <= 256) hipLaunchKernelGGL(k_ln_bwd<4>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d, c.D->rms_norm);
+  else hipLaunchKernelGGL(k_ln_bwd<8>, g, bl, 0, c.s, g1, ldg1, s1, g2, ldg2, x, st, gamma, dres, dx, P, pb, ps, c.T, d, c.D->rms_norm);
   if (!dbeta) {
     hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, P, nb, d, dgamma);
   } else if (dbeta == dgamma + d) {
@@ -1020,6 +1084,7 @@ int linear_res_ln(const Ctx& c, const float* A, int lda, const float* W, const f
   GemmArgs g;
   g.A = A; g.lda = lda; g.B = W; g.ldb = K; g.bias = bias; g.C = x_out; g.ldc = d; g.M = c.T; g.N = d; g.K = K;
   g.R = R; g.ldr = d; g.ln_g = gamma; g.ln_y1 = y1; g.ln_ld1 = ld1; g.ln_y2 = y2; g.ln_ld2 = ld2; g.ln_stats = st;
+  g.ln_rms = c.D->rms_norm;
   return gemm_run(g, 0, 0, EPI_RES_LN, c.s);
 }
 
@@ -1035,6 +1100,7 @@ int dgrad_ln_bwd(const Ctx& c, const float* dY, int ldy, const float* W, int N, 
   GemmArgs g;
   g.A = dY; g.lda = ldy; g.B = W; g.ldb = d; g.C = dx; g.ldc = d; g.M = c.T; g.N = d; g.K = N;
   g.ln_g = gamma; g.ln_x = x; g.ln_stats = const_cast<float*>(st); g.ln_dres = dres; g.ln_part = P ? P : c.D->part;
+  g.ln_rms = c.D->rms_norm;
   if ((rc = gemm_run(g, 0, 1, EPI_LN_BWD, c.s))) return rc;
   if (!P)
     hipLaunchKernelGGL(k_colsum_final, dim3(blocks(d, CS_COLS)), dim3(64 * CS_WAVES), 0, c.s, c.D->part, nb, d, dgamma);
@@ -1172,7 +1238,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   EmbedArgs ea{D->swr, c.P(D->w_pin), c.P(D->act_emb), c.P(D->act_emb_b), c.P(D->reward_embed), c.P(D->w_se),
                c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
                D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
-               D->evolutionary, D->reward_keep, nullptr, nullptr, nullptr};
+               D->evolutionary, D->reward_keep, nullptr, nullptr, nullptr, D->rms_norm};
   // fused: every LayerNorm is formed by the kernel that completes its rows — layer 0's attention
   // pre-norm by the embedding, the others in the epilogue of the GEMM before them (out-projection +
   // residual, FF2 + residual)
@@ -1199,7 +1265,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
       return rc;
     const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
     PrepArgs pa{Ly.proj, D->layers[0].proj, Ly.qkv, D->inv_freq, T, D->n, D->H, D->dh, I, Ly.n_qkv,
-                D->layers[0].n_qkv, D->rot_dim, mix_col};
+                D->layers[0].n_qkv, D->rot_dim, mix_col, D->qk_norm, D->xpos_base};
     hipLaunchKernelGGL(k_qkv_prep, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pa);
     XTRL_LAUNCHED("train qkv_prep");
     const AttnProblem ap = attn_problem(c, Ly, li);
@@ -1304,7 +1370,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     GemmArgs g;
     g.A = D->dz1; g.lda = 4 * d; g.B = c.P(D->w_h1); g.ldb = D->in_dim; g.C = dx_top; g.ldc = d;
     g.M = T; g.N = d; g.K = 4 * d;
-    g.ln_g = c.P(D->ln_final); g.ln_x = D->x_final; g.ln_stats = D->st_final;
+    g.ln_g = c.P(D->ln_final); g.ln_x = D->x_final; g.ln_stats = D->st_final; g.ln_rms = D->rms_norm;
     float* P = csq.take_or_flush(nb, d, c.G(D->ln_final), s, &rc);
     if (rc) return rc;
     g.ln_gpre = D->dewa; g.ln_ldg = 2 * d; g.ln_gscale = D->frac_head_grad; g.ln_part = P ? P : D->part;
@@ -1406,7 +1472,7 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     for (int j = li + 1; j < D->L; ++j) deeper_mix = deeper_mix || D->layers[j].mix;
     PrepBwdArgs pb{dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
                    Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
-                   (li == 0 ? any_mix : deeper_mix) ? 1 : 0};
+                   (li == 0 ? any_mix : deeper_mix) ? 1 : 0, D->qk_norm, D->xpos_base};
     hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection

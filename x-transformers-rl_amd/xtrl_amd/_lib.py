@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -54,7 +54,8 @@ class DecodeDesc(C.Structure):
                 + [(n, P) for n in ('w_h1_t', 'w_h2_t')]
                 + [('layers_dev', C.POINTER(DecodeLayer))]
                 + [(n, P) for n in ('w_h1x', 'heads_part', 'heads_cnt', 'row_part', 'row_cnt')]
-                + [('ff_glu', I32), ('hglu', P)])
+                + [('ff_glu', I32), ('hglu', P), ('qk_norm', I32), ('attn_scale', F32), ('xpos_base', F32),
+                   ('rms_norm', I32)])
 
 
 class FractalLevel(C.Structure):
@@ -101,7 +102,8 @@ class TrainDesc(C.Structure):
                 + [('part_floats', I64), ('ws', P), ('ws_floats', I64), ('layers', C.POINTER(TrainLayer)),
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P),
                    ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32),
-                   ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P)])
+                   ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P),
+                   ('qk_norm', I32), ('xpos_base', F32), ('rms_norm', I32)])
 
 
 class FractalTrainLevel(C.Structure):

@@ -124,7 +124,8 @@ class Agent(nn.Module):
             if k in wm and wm[k] == default:
                 wm.pop(k)
         known = {'attn_dim_head', 'heads', 'depth', 'attn_gate_values', 'add_value_residual',
-                 'learned_value_residual_mix', 'ff_mult', 'ff_no_bias', 'ff_glu'}
+                 'learned_value_residual_mix', 'ff_mult', 'ff_no_bias', 'ff_glu', 'attn_qk_norm',
+                 'attn_qk_norm_scale', 'rotary_xpos', 'rotary_xpos_scale_base', 'use_rmsnorm'}
         unknown = set(wm) - known
         if unknown:
             raise NotImplementedError(f'world_model options {sorted(unknown)} are not supported by the MI355X decoder '
@@ -143,16 +144,21 @@ class Agent(nn.Module):
                         gate_values=wm.get('attn_gate_values', False), value_residual=wm.get('add_value_residual', False),
                         learned_mix=wm.get('learned_value_residual_mix', False), ff_mult=int(wm.get('ff_mult', 4)),
                         ff_no_bias=bool(wm.get('ff_no_bias', False)), ff_glu=bool(wm.get('ff_glu', False)),
+                        rms_norm=bool(wm.get('use_rmsnorm', False)), qk_norm=bool(wm.get('attn_qk_norm', False)),
+                        qk_norm_scale=float(wm.get('attn_qk_norm_scale', 10.)),
+                        rotary_xpos=bool(wm.get('rotary_xpos', False)),
+                        xpos_scale_base=float(wm.get('rotary_xpos_scale_base', 512.)),
                         rotary_abs_rollout=rotary_abs_rollout,
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
         # policy body: the x-transformers Decoder (x_transformers_rl.py) or the per-timestep causal
         # fractal encoder (fractal_rl.py:349-619 made causal, fractal.FractalPolicyActorCritic)
         if policy_body == 'fractal':
-            if c.gate_values or c.value_residual or c.ff_no_bias or c.ff_glu:
+            if c.gate_values or c.value_residual or c.ff_no_bias or c.ff_glu or c.qk_norm or c.rotary_xpos or c.rms_norm:
                 raise NotImplementedError('the fractal policy body has no gated values / value residual / bias-free or '
-                                          'GLU feed-forward: set attn_gate_values / add_value_residual / ff_no_bias / '
-                                          'ff_glu to False')
+                                          'GLU feed-forward / qk norm / xPos rotary / RMSNorm: set attn_gate_values / '
+                                          'add_value_residual / ff_no_bias / ff_glu / attn_qk_norm / rotary_xpos / '
+                                          'use_rmsnorm to False')
             levels = int(fractal_levels or c.depth)
             self.model = FractalPolicyActorCritic(c, levels).to(dev)
         elif policy_body == 'decoder':

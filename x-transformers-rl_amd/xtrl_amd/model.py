@@ -47,6 +47,11 @@ class ModelConfig:
     ff_mult: int = 4
     ff_no_bias: bool = False             # x-transformers FeedForward no_bias (world_model['ff_no_bias'])
     ff_glu: bool = False                 # x-transformers FeedForward glu (world_model['ff_glu']): GELU-gated project-in
+    rms_norm: bool = False               # x-transformers use_rmsnorm: RMSNorm pre-norms / final norm (param .g)
+    qk_norm: bool = False                # x-transformers attn_qk_norm: q, k l2-normalised per head, scores x qk_norm_scale
+    qk_norm_scale: float = 10.           # x-transformers attn_qk_norm_scale
+    rotary_xpos: bool = False            # x-transformers rotary_xpos: xPos-scaled rotary (q x s^p, k / s^p)
+    xpos_scale_base: float = 512.        # x-transformers rotary_xpos_scale_base
     rotary_abs_rollout: bool = False     # decision log: reference semantics = rotary position 0 in rollout
     hl_reduction_mean: bool = True       # decision log: hl-gauss-pytorch default reduction
     hl_sigma_ratio: float = 2.0
@@ -68,6 +73,23 @@ class XLayerNorm(nn.Module):
 
     def forward(self, x):
         return F.layer_norm(x, (self.dim,), eps=1e-5) * self.gamma
+
+
+class XRMSNorm(nn.Module):
+    """x-transformers RMSNorm (Decoder use_rmsnorm): F.normalize(x, dim=-1) * sqrt(dim) * g."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+        self.g = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x):
+        return F.normalize(x, dim=-1) * self.dim ** 0.5 * self.g
+
+
+def norm_gain(mod):
+    """The gain of a decoder norm: LayerNorm.gamma or RMSNorm.g."""
+    return mod.g if isinstance(mod, XRMSNorm) else mod.gamma
 
 
 class XAttention(nn.Module):
@@ -116,16 +138,17 @@ class XDecoder(nn.Module):
         super().__init__()
         self.dim = c.dim
         self.layers = nn.ModuleList()
+        Norm = XRMSNorm if c.rms_norm else XLayerNorm
         for ind in range(c.depth):
             mix = c.value_residual and c.learned_mix and ind > 0
-            self.layers.append(nn.ModuleList([nn.ModuleList([XLayerNorm(c.dim), None, None]), XAttention(c, mix),
+            self.layers.append(nn.ModuleList([nn.ModuleList([Norm(c.dim), None, None]), XAttention(c, mix),
                                               _Residual()]))
-            self.layers.append(nn.ModuleList([nn.ModuleList([XLayerNorm(c.dim), None, None]), XFeedForward(c),
+            self.layers.append(nn.ModuleList([nn.ModuleList([Norm(c.dim), None, None]), XFeedForward(c),
                                               _Residual()]))
         self.rotary_pos_emb = nn.Module()
         rot = c.dim_head // 2
         self.rotary_pos_emb.register_buffer('inv_freq', 1. / (10000 ** (torch.arange(0, rot, 2).float() / rot)))
-        self.final_norm = XLayerNorm(c.dim)
+        self.final_norm = Norm(c.dim)
 
 
 class XTransformer(nn.Module):
@@ -300,6 +323,12 @@ class WorldModelActorCritic(nn.Module):
         freqs = (pos[:, None] * inv[None, :]).repeat_interleave(2, dim=-1)
         cos, sin = freqs.cos(), freqs.sin()
         rot = freqs.shape[-1]
+        xq = xk = 1.
+        if c.rotary_xpos:   # x-transformers RotaryEmbedding(use_xpos): scale ** ((pos - n // 2) / scale_base)
+            sc = (torch.arange(0, rot, 2, device=state.device, dtype=torch.float32) + 0.4 * rot) / (1.4 * rot)
+            xq = (sc[None, :] ** ((pos - n // 2) / c.xpos_scale_base)[:, None]).repeat_interleave(2, dim=-1)
+            xk = xq ** -1.
+        scale = c.qk_norm_scale if c.qk_norm else dh ** -0.5
         p_drop = c.dropout if self.training else 0.
         first_v = None
         split = lambda t: t.reshape(b, n, H, dh).permute(0, 2, 1, 3)
@@ -320,9 +349,11 @@ class WorldModelActorCritic(nn.Module):
                 v = v.lerp(first_v, mix)
             if first_v is None:
                 first_v = orig_v
-            q = torch.cat((q[..., :rot] * cos + _rotate_half(q[..., :rot]) * sin, q[..., rot:]), dim=-1)
-            k = torch.cat((k[..., :rot] * cos + _rotate_half(k[..., :rot]) * sin, k[..., rot:]), dim=-1)
-            o = ops.attention(q, k, v, lens, dh ** -0.5, p_drop, attn_seed, attn_offset, li)
+            if c.qk_norm:
+                q, k = F.normalize(q, dim=-1), F.normalize(k, dim=-1)
+            q = torch.cat((q[..., :rot] * cos * xq + _rotate_half(q[..., :rot]) * sin * xq, q[..., rot:]), dim=-1)
+            k = torch.cat((k[..., :rot] * cos * xk + _rotate_half(k[..., :rot]) * sin * xk, k[..., rot:]), dim=-1)
+            o = ops.attention(q, k, v, lens, scale, p_drop, attn_seed, attn_offset, li)
             o = o.permute(0, 2, 1, 3).reshape(b, n, I)
             if gate_pre is not None:
                 o = o * gate_pre.sigmoid()

@@ -17,15 +17,16 @@ sync and terminated episodes cost nothing.
 from __future__ import annotations
 
 import ctypes as C
-import os
 import dataclasses
+import os
+import time
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib as L
 from . import ops
-from .model import WorldModelActorCritic
+from .model import WorldModelActorCritic, norm_gain
 
 SIM_README, SIM_LANDER, SIM_HOST = 0, 1, -1
 
@@ -161,6 +162,10 @@ class RolloutEngine:
         D.continuous, D.squash, D.evolutionary = int(c.continuous), int(c.squash), int(c.evolutionary)
         D.gate_values, D.value_residual, D.learned_mix = int(c.gate_values), int(c.value_residual), int(c.learned_mix)
         D.rotary_abs, D.rot_dim = int(c.rotary_abs_rollout), c.dim_head // 2
+        qk = bool(getattr(c, 'qk_norm', False))
+        D.qk_norm, D.attn_scale = int(qk), float(c.qk_norm_scale) if qk else 0.
+        D.xpos_base = float(c.xpos_scale_base) if getattr(c, 'rotary_xpos', False) else 0.
+        D.rms_norm = int(getattr(c, 'rms_norm', False))
         D.sim_mode, D.hazard_log2, D.rs_eps = self.sim_mode, hazard_log2, 1e-5
         if clamp is not None:
             D.clamp_lo, D.clamp_hi, D.has_clamp = float(clamp[0]), float(clamp[1]), 1
@@ -196,7 +201,7 @@ class RolloutEngine:
         """Copy (EMA) model weights into the decode layout (xtrl.py:721-734, 304-369 names)."""
         c, w = self.c, self.w
         w['w_pin'].copy_(model.transformer.project_in.weight)
-        w['ln_final'].copy_(model.transformer.attn_layers.final_norm.gamma)
+        w['ln_final'].copy_(norm_gain(model.transformer.attn_layers.final_norm))
         inv = model.transformer.attn_layers.rotary_pos_emb.inv_freq
         w['inv_freq'][:inv.numel()].copy_(inv)
         self._pack_common(model, rs_mean, rs_var)
@@ -204,7 +209,7 @@ class RolloutEngine:
         for wl, (attn_l, ff_l) in zip(self.wl, model.blocks()):
             (ln_a, _, _), blk, _ = attn_l
             (ln_f, _, _), ffb, _ = ff_l
-            wl['ln_attn'].copy_(ln_a.gamma)
+            wl['ln_attn'].copy_(norm_gain(ln_a))
             rows = [blk.to_q.weight, blk.to_k.weight, blk.to_v.weight]
             bias = [torch.zeros(3 * I, device=self.dev)]
             if blk.to_v_gate is not None:
@@ -223,7 +228,7 @@ class RolloutEngine:
             torch.cat(bias, out=wl['b_qkv'][:self.n_qkv])
             wl['w_out'].copy_(blk.to_out.weight)
             wl['w_out_t'].copy_(blk.to_out.weight.t())
-            wl['ln_ff'].copy_(ln_f.gamma)
+            wl['ln_ff'].copy_(norm_gain(ln_f))
             f0 = ffb.ff[0].proj if c.ff_glu else ffb.ff[0][0]   # (ff_glu: the GLU projection)
             wl['w_ff1'].copy_(f0.weight)
             wl['w_ff2'].copy_(ffb.ff[2].weight)
@@ -448,6 +453,10 @@ class RolloutEngine:
         act_p, st_p, dst_p = self._host_act.data_ptr(), st.data_ptr(), dst.data_ptr()
         rows_max = self.rows_max if 0 < E <= self.rows_max else 0
         pending = np.zeros(E, dtype=bool)    # rows taking their bootstrap decode step
+        # host-side time of the wave's steps (seconds): decode launch + the step's wait for the actions,
+        # the env step, the feedback (staging + H2D copy + kernel launch) — bench.py reports them
+        ht = self.host_times = dict(decode=0., env=0., feedback=0., steps=0)
+        clock = time.perf_counter
         for t in range(T + 1):
             if not live.any() and not pending.any():
                 break
@@ -455,10 +464,13 @@ class RolloutEngine:
                 self.step(t, rows_max > 0)
                 self.alive.zero_()   # (the row-resident step leaves them at 2 for a feedback that never comes)
                 break
+            c0 = clock()
             self._host_decode(t, rows_max, desc, act_p, stream)
+            c1 = clock()
             pending[:] = False
             act = act_np
             ns, r, term, trunc = env_step(act, live.copy())
+            c2 = clock()
             ns = np.asarray(ns, dtype=np.float32).reshape(E, S)
             r = np.asarray(r, dtype=np.float64).reshape(E)
             term = np.asarray(term).reshape(E).astype(bool)
@@ -470,6 +482,11 @@ class RolloutEngine:
             flags[:E] = term
             flags[E:2 * E] = trunc
             L.check(lib.xtrl_host_feedback(desc, t, st_p, dst_p, T, int(bootstrap), stream), 'host_feedback')
+            c3 = clock()
+            ht['decode'] += c1 - c0
+            ht['env'] += c2 - c1
+            ht['feedback'] += c3 - c2
+            ht['steps'] += 1
             ended = live & (term | trunc | (t + 1 >= T))
             boot_now = live & trunc & ~term & bool(bootstrap)     # the last step (t + 1 == T) included
             boot_rows |= boot_now

@@ -82,6 +82,7 @@ class FusedTrainStep:
         layers = (L.TrainLayer * L_)()
         X = [E(T, d) for _ in range(L_ + 1)]
         max_qkv = 0
+        nw = 'g' if c.rms_norm else 'gamma'   # x-transformers RMSNorm.g / LayerNorm.gamma
         for li in range(L_):
             mix = bool(c.value_residual and c.learned_mix and li > 0)
             pa, pf = f'{pre}{2 * li}.', f'{pre}{2 * li + 1}.'
@@ -98,9 +99,9 @@ class FusedTrainStep:
             bufs['og'] = E(T, I) if c.gate_values else bufs['o']
             self.layers_py.append(bufs)
             Ly = layers[li]
-            Ly.ln_attn, Ly.w_proj = off(pa + '0.0.gamma'), span_off(wn)
+            Ly.ln_attn, Ly.w_proj = off(pa + '0.0.' + nw), span_off(wn)
             Ly.b_proj = span_off(bn) if bn else -1
-            Ly.w_out, Ly.ln_ff = off(pa + '1.to_out.weight'), off(pf + '0.0.gamma')
+            Ly.w_out, Ly.ln_ff = off(pa + '1.to_out.weight'), off(pf + '0.0.' + nw)
             f1 = pf + ('1.ff.0.proj.' if glu else '1.ff.0.0.')
             Ly.w_ff1, Ly.b_ff1 = off(f1 + 'weight'), off(f1 + 'bias')
             Ly.w_ff2, Ly.b_ff2 = off(pf + '1.ff.2.weight'), off(pf + '1.ff.2.bias')
@@ -132,11 +133,14 @@ class FusedTrainStep:
         D.in_dim, D.n_out, D.G = c.in_dim, n_out, c.dim_gene if c.evolutionary else 0
         D.continuous, D.evolutionary, D.gate_values, D.rot_dim = int(c.continuous), int(c.evolutionary), \
             int(c.gate_values), rot
-        D.frac_head_grad, D.attn_scale = float(c.frac_head_grad), float(dh ** -0.5)
+        D.frac_head_grad = float(c.frac_head_grad)
+        D.attn_scale = float(c.qk_norm_scale) if c.qk_norm else float(dh ** -0.5)
+        D.qk_norm, D.xpos_base = int(c.qk_norm), float(c.xpos_scale_base) if c.rotary_xpos else 0.
         D.flat, D.grad = flat.flat.data_ptr(), flat.grad.data_ptr()
         D.w_pin = off('transformer.project_in.weight')
         _heads_desc(D, c, flat)
-        D.ln_final = off('transformer.attn_layers.final_norm.gamma')
+        D.ln_final = off('transformer.attn_layers.final_norm.' + nw)
+        D.rms_norm = int(c.rms_norm)
         D.inv_freq = self.inv_freq.data_ptr()
         for k, t in self.buf.items():
             setattr(D, k, t.data_ptr())
