@@ -46,6 +46,14 @@ CONFIGS = {
                         'policy, actor / critic heads on [embed | state embed], in = 2d)',
                S=8, A=4, episodes=1024, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=False,
                batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
+    # the C3 model conditioned on an EPO gene pool as train_lander.py runs it (3 genes per island, the
+    # heads on [embed | state embed | latent], in = 3d): 384 episodes x 3 genes = 1152 pairs per GPU
+    'c3_evo': dict(workload='C3 with EPO (SURVEY 8 C3 "evo: as C2"): LunarLander-shaped VecSim, 384 episodes x 3 '
+                            'genes (32-dim) x 128 steps per update per GPU, depth-4 d=256 4x16-head gated '
+                            'value-residual policy, heads on [embed | state embed | latent], batch 128, 4 epochs, '
+                            'dropout 0.25',
+                   S=8, A=4, episodes=384, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=True,
+                   batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
     # configs[1] — train_lander defaults (evolutionary, 3 genes), 256 episodes, depth-2 d=128
     'c2': dict(workload='C2: LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 steps, depth-2 d=128 EPO',
                S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,

@@ -113,7 +113,9 @@ def show(path):
                 qgap = (int(rows[i]['Start_Timestamp']) - last_end[q]) / 1e3 if q in last_end else 0.0
                 idle_q[q] += max(qgap, 0.0)
                 last_end[q] = int(rows[i]['End_Timestamp'])
-                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  q{q} qgap {qgap:6.1f} at {(int(rows[i]["Start_Timestamp"]) - ts) / 1e3:7.1f}  {short(names[i])}')
+                grid = 'x'.join(rows[i].get(f'Grid_Size_{a_}', '?') for a_ in 'XYZ')
+                print(f'  {dur[i]:8.1f} us  gap {gap:6.1f}  q{q} qgap {qgap:6.1f} at {(int(rows[i]["Start_Timestamp"]) - ts) / 1e3:7.1f}  '
+                      f'{short(names[i])} [{grid}]')
             print('  stream idle inside the minibatch: ' + ', '.join(f'{q}: {v:.1f} us' for q, v in idle_q.items()))
         # one decode step: the kernels between two consecutive sampling launches in the rollout
         samples = [i for i in roll if 'k_sample' in names[i] or 'k_heads_sample' in names[i]]
