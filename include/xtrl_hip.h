@@ -244,6 +244,14 @@ int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream);
  * turns a slot it ranks from live to dead: a Sim episode it ends reads alive = 3 + (t & 1) until the
  * next step's compaction clears it to 0 (every compaction treats 3 + (t & 1) as live at step t only). */
 int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void* stream);
+/* Diagnostics of the row-resident step (no reference counterpart): synchronises the device, copies
+ * the phase stamps of the last stamped launch (wall-clock ticks taken by workgroup 0 after each
+ * phase of its first row: start, compaction, embedding, 7 per layer — LN, q|k|v, attention,
+ * out-projection, LN, FF1, FF2 — final LN, hidden, last Linear, sampling) into out[0..cap) — the
+ * wall-clock stamps at [0, n), the same points' shader-clock counters at [n, 2 n), n the returned
+ * capacity — stores the wall-clock tick rate, then turns stamping on (on != 0) or off for later
+ * launches. */
+int xtrl_row_stamps(int on, uint64_t* out, int cap, int64_t* ticks_per_sec);
 /* Host env results of step t (xtrl.py:1297-1336) for the live rows: next_state [E][S], reward [E],
  * terminated [E] (stored as is_boundary), truncated [E] or NULL.  An episode ends when terminated,
  * truncated or t + 1 == t_limit (max_timesteps); with `bootstrap` a truncated, not terminated

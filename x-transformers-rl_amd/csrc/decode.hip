@@ -1686,6 +1686,14 @@ __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT,
   const int tid = threadIdx.x, NC4 = N >> 2;
   const int KG = NC4 >= ROW_T ? 1 : min(32, ROW_T / NC4);
   const int Kc = (K + KG - 1) / KG;
+  // the bias of this thread's first two output columns, loaded beside the weights (after the
+  // barrier below it would be one more dependent round trip)
+  float bpre[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = tid + ROW_T * j;
+    bpre[j] = (bias && n < N) ? bias[n] : 0.f;
+  }
   for (int item = tid; item < KG * NC4; item += ROW_T) {
     const int g = item / NC4, n4 = 4 * (item - g * NC4);
     const int k0 = g * Kc, k1 = min(K, k0 + Kc);
@@ -1703,10 +1711,19 @@ __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT,
     *reinterpret_cast<float4*>(part + g * N + n4) = acc;
   }
   __syncthreads();
-  for (int n = tid; n < N; n += ROW_T) {
+  for (int n = tid, j = 0; n < N; n += ROW_T, ++j) {
+    // the KG partial rows in group order, 8 LDS loads in flight per batch (one load per add left
+    // every add waiting a full LDS latency: ~2.9 k cycles for KG = 32, tools/row_phase_lab.hip)
     float v = part[n];
-    for (int g = 1; g < KG; ++g) v += part[g * N + n];
-    v += bias ? bias[n] : 0.f;
+    for (int g0 = 1; g0 < KG; g0 += 8) {
+      float pv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) pv[u] = part[min(g0 + u, KG - 1) * N + n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (g0 + u < KG) v += pv[u];
+    }
+    v += bias ? (j == 0 ? bpre[0] : (j == 1 ? bpre[1] : bias[n])) : 0.f;
     if constexpr (ACT == 1) v = geluf_(v);
     if constexpr (ACT == 2) v = siluf_(v);
     if (res) v += res[n];
@@ -1719,7 +1736,12 @@ __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT,
 __device__ __forceinline__ void row_layernorm(const float* x, const float* g, int d, float* out, bool rms) {
   const int tid = threadIdx.x;
   if (tid < 64) {
-    float v[4], sm = 0.f;
+    float v[4], gv[4], sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // (the gain issued first: its round trip overlaps the reductions)
+      const int c = tid + 64 * k;
+      gv[k] = c < d ? g[c] : 0.f;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int c = tid + 64 * k;
@@ -1737,7 +1759,7 @@ __device__ __forceinline__ void row_layernorm(const float* x, const float* g, in
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int c = tid + 64 * k;
-      if (c < d) out[c] = ((v[k] - mean) * rstd) * g[c];
+      if (c < d) out[c] = ((v[k] - mean) * rstd) * gv[k];
     }
   }
   __syncthreads();
@@ -1766,6 +1788,12 @@ __host__ __device__ inline RowLds row_lds(const XtrlDecodeDesc& D) {
 }
 
 constexpr int ROW_MAX_L = 64;
+// phase stamps of the row-resident step (xtrl_row_stamps, diagnostics): thread 0 of workgroup 0
+// records the wall clock after each phase of its first row — start, compaction, embedding, 7 per
+// layer (LN, q|k|v, attention, out-projection, LN, FF1, FF2), final LN, hidden, last Linear, sample
+constexpr int ROW_STAMP_MAX = 8 + 7 * ROW_MAX_L;
+__device__ int g_row_stamp_on;
+__device__ uint64_t g_row_stamps[2 * ROW_STAMP_MAX];   // wall clock | shader clock (s_memtime)
 constexpr int ROW_G = 4;      // workgroups per row at most (the heads split across them)
 constexpr int ROW_CUS = 256;  // (rows x workgroups per row kept within one workgroup per CU)
 
@@ -1783,7 +1811,25 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   float *xs = lds + Lo.x, *xn = lds + Lo.xn, *qkv = lds + Lo.qkv, *att = lds + Lo.att, *v1s = lds + Lo.v1;
   float *hs = lds + Lo.h, *ac = lds + Lo.ac, *part = lds + Lo.part, *lg = lds + Lo.lg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bool stamp = blockIdx.x == 0 && tid == 0 && g_row_stamp_on;
+  int ns = 0;
+  auto mark = [&]() {
+    if (stamp && ns < ROW_STAMP_MAX) {
+      g_row_stamps[ROW_STAMP_MAX + ns] = (uint64_t)clock64();
+      g_row_stamps[ns++] = (uint64_t)wall_clock64();
+    }
+  };
+  mark();
   const int S = D.S, d = D.d, H = D.H, I = H * DH, L = D.L;
+  // the layer descriptors (pointers) copied to LDS in one batch of vector loads: read lazily from
+  // layers_dev, each layer phase's pointers were a cold scalar load ahead of its data (a round trip per phase)
+  __shared__ XtrlDecodeLayer ly_sh[ROW_MAX_L];
+  {
+    constexpr int LW = (int)(sizeof(XtrlDecodeLayer) / sizeof(uint32_t));
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(D.layers_dev);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(ly_sh);
+    for (int i = tid; i < L * LW; i += ROW_T) dst[i] = src[i];   // (visible after the compaction's barriers)
+  }
   // ---- compaction (as k_embed<CMP>): every workgroup ranks the live slots itself.  Workgroups that
   //      start late (the grid need not be resident at once) may find rows that others have already
   //      stepped: a Sim row ended at this step reads ALIVE_END + (t & 1) and a bootstrap row keeps
@@ -1819,6 +1865,7 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
     __syncthreads();
   }
   if (blockIdx.x == 0 && tid == 0) D.live_count[t & 1] = n_live;
+  mark();
   const int n_act = D.continuous ? 2 * D.A : D.A;
   const int nq4 = round4i(D.n_qkv), n2 = round4i(n_act + D.B), ff = D.ff;
   const float scale = D.attn_scale > 0.f ? D.attn_scale : 1.0f / sqrtf((float)DH);
@@ -1862,11 +1909,14 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
       if (D.evolutionary && D.lat_embed) ac[2 * d + c] = D.lat_embed[(int64_t)e * d + c];
     }
     __syncthreads();
+    mark();
     // ---- decoder layers
     for (int l = 0; l < L; ++l) {
-      const XtrlDecodeLayer& Ly = D.layers_dev[l];   // (device copy: scalar loads, no kernel-argument array)
+      const XtrlDecodeLayer& Ly = ly_sh[l];   // (the LDS copy of layers_dev)
       row_layernorm(xs, Ly.ln_attn, d, xn, D.rms_norm);
+      mark();
       row_gemv<0>(xn, d, Ly.w_qkv_t, nq4, Ly.b_qkv, nq4, qkv, part);
+      mark();
       // attention: head h on wave h (waves past H idle); k_attn_decode's arithmetic and lane roles
       for (int h = w; h < H; h += ROW_T / 64) {
         const int c = lane % DH, g = lane / DH;
@@ -1977,18 +2027,26 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
         }
       }
       __syncthreads();
+      mark();
       // out-projection + residual (W_out^T is k-major), then FF: LN, FF1 + GELU, FF2 + residual
       row_gemv<0>(att, I, Ly.w_out_t, d, nullptr, d, xs, part, xs);
+      mark();
       row_layernorm(xs, Ly.ln_ff, d, xn, D.rms_norm);
+      mark();
       row_gemv<1>(xn, d, Ly.w_ff1_t, ff, Ly.b_ff1, ff, hs, part);
+      mark();
       row_gemv<0>(hs, ff, Ly.w_ff2_t, d, Ly.b_ff2, d, xs, part, xs);
+      mark();
     }
     // ---- heads: [final LN(x) | state embed | latent] -> SiLU hidden -> block-diagonal last layer
     row_layernorm(xs, D.ln_final, d, ac, D.rms_norm);
+    mark();
     const int hw = 4 * d / Ge, hc0 = gs * hw;   // this workgroup's hidden units
     row_gemv<2>(ac, D.in_dim, D.w_h1_t + hc0, 4 * d, D.b_h1 + hc0, hw, hs, part);
+    mark();
     float* out2 = part + ROW_PART;
     row_gemv<0>(hs, hw, D.w_h2_t + (int64_t)hc0 * n2, n2, Ge == 1 ? D.b_h2 : nullptr, n2, out2, part);
+    mark();
     if (Ge > 1) {   // the partials meet (k_mlp's hand-off); the last arriver sums them in order + b2
       float* rp = D.row_part + (int64_t)r * ROW_G * n2;
       for (int n = tid; n < n2; n += ROW_T)
@@ -2027,6 +2085,8 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
       sample_row(D, t, e, tid, lg, in, true);
     }
     __syncthreads();
+    mark();
+    stamp = false;   // (the first row only)
   }
 }
 
@@ -2249,6 +2309,23 @@ int sim_reset(float* state, int E, int S, uint64_t seed, uint32_t update, const 
 
 extern "C" int xtrl_decode_step_rows(const XtrlDecodeDesc* desc, int t, int max_rows, void* stream) {
   return xtrl::decode_step_rows(desc, t, max_rows, xtrl::as_stream(stream));
+}
+extern "C" int xtrl_row_stamps(int on, uint64_t* out, int cap, int64_t* ticks_per_sec) {
+  XTRL_REQUIRE(cap >= 0 && (cap == 0 || out), "row_stamps: bad arguments");
+  if (hipDeviceSynchronize() != hipSuccess) return XTRL_E_HIP;
+  const int n = std::min(cap, 2 * xtrl::ROW_STAMP_MAX);
+  if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(xtrl::g_row_stamps), n * sizeof(uint64_t)) != hipSuccess)
+    return XTRL_E_HIP;
+  if (ticks_per_sec) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+      return XTRL_E_HIP;
+    *ticks_per_sec = (int64_t)khz * 1000;
+  }
+  const int v = on ? 1 : 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(xtrl::g_row_stamp_on), &v, sizeof(int)) != hipSuccess) return XTRL_E_HIP;
+  return xtrl::ROW_STAMP_MAX;
 }
 extern "C" int xtrl_decode_step(const XtrlDecodeDesc* desc, int t, void* stream) {
   return xtrl::decode_step(desc, t, xtrl::as_stream(stream));

@@ -142,6 +142,7 @@ SIGNATURES = {
     'xtrl_rollout_begin': (I32, [C.POINTER(DecodeDesc), P]),
     'xtrl_decode_step': (I32, [C.POINTER(DecodeDesc), I32, P]),
     'xtrl_decode_step_rows': (I32, [C.POINTER(DecodeDesc), I32, I32, P]),
+    'xtrl_row_stamps': (I32, [I32, P, I32, P]),
     'xtrl_host_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P, P]),
     'xtrl_host_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, I32, I32, P]),
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
