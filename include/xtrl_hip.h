@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 17
+#define XTRL_ABI_VERSION 18
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -226,6 +226,11 @@ typedef struct XtrlDecodeDesc {
   /* world_model['use_rmsnorm']: every pre-norm and the final norm are x-transformers' RMSNorm
    * (F.normalize(x) sqrt(d) g) instead of its LayerNorm; 0: LayerNorm */
   int rms_norm;
+  /* host-env loop (xtrl_host_decode): pinned host memory the device can address (int32 [E] actions,
+   * continuous: float [E][A]), or NULL.  When set, the sampling also stores each row's action
+   * there (and the rollout start its -1 / 0 reset), so xtrl_host_decode passed this same buffer only
+   * synchronises — no device->host copy per step */
+  void* act_host;
 } XtrlDecodeDesc;
 
 /* Reset: state_0 = sim reset, prev_action = -1 / 0, prev_reward = 0, alive = 1, lens = 0, and
@@ -265,9 +270,11 @@ int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* ne
  * per half of a step.  The exception to the no-synchronisation rule above: xtrl_host_decode runs
  * decode step t (rows_max > 0: xtrl_decode_step_rows), copies the rows' actions (prev_action [E]
  * int32, continuous prev_action_f [E][A]) to act_host (pinned host memory) and synchronises the
- * stream — the one host wait of a step.  xtrl_host_feedback copies the pinned stage (next_state
+ * stream — the one host wait of a step; when act_host is desc->act_host the sampling already stored
+ * the actions there and no copy runs.  xtrl_host_feedback copies the pinned stage (next_state
  * [E][S] fp32 | reward [E] fp32 | terminated [E] u8 | truncated [E] u8) to dev_stage (device, same
- * layout) and runs xtrl_rollout_env_feedback on it. */
+ * layout) and runs xtrl_rollout_env_feedback on it; dev_stage NULL: the kernel reads the pinned
+ * stage in place (device-addressable pinned memory), no host->device copy. */
 int xtrl_host_decode(const XtrlDecodeDesc* desc, int t, int rows_max, void* act_host, void* stream);
 int xtrl_host_feedback(const XtrlDecodeDesc* desc, int t, const void* host_stage, void* dev_stage, int t_limit,
                        int bootstrap, void* stream);

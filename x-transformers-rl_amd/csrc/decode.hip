@@ -704,6 +704,7 @@ __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e
     D.traj_actions[(int64_t)e * D.Tmax + t] = a;
     D.traj_logp[(int64_t)e * D.Tmax + t] = logf(pa);
     D.prev_action[e] = a;
+    if (D.act_host) static_cast<int32_t*>(D.act_host)[e] = a;
   } else {
     for (int i = 0; i < A; ++i) {
       const float mean = lg[2 * i], lv = lg[2 * i + 1];
@@ -718,6 +719,7 @@ __device__ __forceinline__ void sample_row(const XtrlDecodeDesc& D, int t, int e
       D.traj_actions_f[((int64_t)e * D.Tmax + t) * A + i] = sv;
       D.traj_logp[((int64_t)e * D.Tmax + t) * A + i] = lp;
       D.prev_action_f[e * A + i] = sv;
+      if (D.act_host) static_cast<float*>(D.act_host)[e * A + i] = sv;
     }
   }
   if (D.sim_mode >= 0) {   // the synthetic Sim's step (reward, termination, bookkeeping)
@@ -829,6 +831,12 @@ __global__ void k_rollout_begin(const XtrlDecodeDesc D) {
   D.prev_action[e] = -1;
   if (D.continuous)
     for (int i = 0; i < D.A; ++i) D.prev_action_f[e * D.A + i] = 0.f;
+  if (D.act_host) {   // (the host-side copy of the actions starts as the device one)
+    if (D.continuous)
+      for (int i = 0; i < D.A; ++i) static_cast<float*>(D.act_host)[e * D.A + i] = 0.f;
+    else
+      static_cast<int32_t*>(D.act_host)[e] = -1;
+  }
   D.prev_reward[e] = 0.f;
   D.alive[e] = 1;
   D.lens[e] = 0;
@@ -2274,7 +2282,7 @@ int host_decode(const XtrlDecodeDesc* D, int t, int rows_max, void* act_host, hi
   if (int rc = rows_max > 0 ? decode_step_rows(D, t, rows_max, s) : decode_step(D, t, s)) return rc;
   const size_t bytes = (size_t)D->E * (D->continuous ? D->A : 1) * 4;
   const void* src = D->continuous ? (const void*)D->prev_action_f : (const void*)D->prev_action;
-  if (hipMemcpyAsync(act_host, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if ((act_host != D->act_host && hipMemcpyAsync(act_host, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) ||
       hipStreamSynchronize(s) != hipSuccess) {
     set_error("host_decode: action copy / synchronisation failed");
     return XTRL_E_HIP;
@@ -2286,14 +2294,15 @@ int host_decode(const XtrlDecodeDesc* D, int t, int rows_max, void* act_host, hi
 // (u8) | [E] truncated (u8) to the device stage (same layout), then the feedback kernel on it
 int host_feedback(const XtrlDecodeDesc* D, int t, const void* host_stage, void* dev_stage, int t_limit, int bootstrap,
                   hipStream_t s) {
-  XTRL_REQUIRE(host_stage && dev_stage, "host_feedback: null stage");
+  XTRL_REQUIRE(host_stage, "host_feedback: null stage");
   const int E = D->E, S = D->S;
-  if (hipMemcpyAsync(dev_stage, host_stage, (size_t)4 * E * (S + 1) + 2 * (size_t)E, hipMemcpyHostToDevice, s) !=
-      hipSuccess) {
+  if (dev_stage && hipMemcpyAsync(dev_stage, host_stage, (size_t)4 * E * (S + 1) + 2 * (size_t)E,
+                                  hipMemcpyHostToDevice, s) != hipSuccess) {
     set_error("host_feedback: stage copy failed");
     return XTRL_E_HIP;
   }
-  float* f = static_cast<float*>(dev_stage);
+  // (dev_stage NULL: the feedback kernel reads the pinned stage in place)
+  const float* f = static_cast<const float*>(dev_stage ? dev_stage : host_stage);
   const uint8_t* flags = reinterpret_cast<const uint8_t*>(f + (int64_t)E * (S + 1));
   return env_feedback(D, t, f, f + (int64_t)E * S, flags, flags + E, t_limit, bootstrap, s);
 }

@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -55,7 +55,7 @@ class DecodeDesc(C.Structure):
                 + [('layers_dev', C.POINTER(DecodeLayer))]
                 + [(n, P) for n in ('w_h1x', 'heads_part', 'heads_cnt', 'row_part', 'row_cnt')]
                 + [('ff_glu', I32), ('hglu', P), ('qk_norm', I32), ('attn_scale', F32), ('xpos_base', F32),
-                   ('rms_norm', I32)])
+                   ('rms_norm', I32), ('act_host', P)])
 
 
 class FractalLevel(C.Structure):
