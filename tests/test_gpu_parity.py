@@ -980,7 +980,9 @@ def test_ppo_loss_and_grads_identical_weights(evo, gates, cont, frac, ff):
 def test_learner_two_updates_match_oracle(evo, gates, frac):
     """Free-running: both sides train on their own.  The first update matches at 1e-4; later
     minibatches may drift because AdoptAtan2's cautious mask (sign of m*g) is discontinuous, so a
-    1e-7 gradient difference can flip an element's step size 10x (documented in DESIGN.md)."""
+    1e-7 gradient difference can flip an element's step size 10x (documented in DESIGN.md).  Every
+    step of the same runs is checked tightly by test_optimizer_step_in_learner_matches_restatement
+    (teacher-forced) and every minibatch's loss / gradients by test_ppo_loss_and_grads_identical_weights."""
     learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, T=10, episodes=6, batch=2, seed=5, hazard=2,
                                         fractal_levels=frac)
     agent = learner.agent
@@ -1000,6 +1002,71 @@ def test_learner_two_updates_match_oracle(evo, gates, frac):
         else:
             np.testing.assert_allclose(ours[:3], theirs[:3], rtol=1e-4, atol=1e-5)
             np.testing.assert_allclose(ours, theirs, rtol=5e-2, atol=5e-3)
+
+
+@pytest.mark.parametrize('evo,gates,frac', [(False, True, None), (True, False, None), (False, False, 2)])
+def test_optimizer_step_in_learner_matches_restatement(evo, gates, frac):
+    """Teacher-forced clip + AdoptAtan2 inside the Learner: for every minibatch of two updates the
+    step is recomputed on the host from the GPU's own pre-step weights, gradient and optimiser state
+    (the arithmetic of oracle/thirdparty.AdoptAtan2 and torch's clip_grad_norm_), so nothing drifts
+    and every step is checked tightly — where test_learner_two_updates_match_oracle, free-running,
+    allows 5e-2 after three minibatches.  The cautious mask where(m g > 0, 1, c) is discontinuous in
+    m, so it is taken from the GPU's updated m (itself checked at 2e-6); the clip coefficient at 1e-6;
+    the weight change at 1e-4 of itself + 4 ulp of the weight; v at 2e-6."""
+    learner, env, oracle = make_learner(depth=2, gates=gates, evo=evo, T=10, episodes=6, batch=2, seed=5, hazard=2,
+                                        fractal_levels=frac)
+    agent = learner.agent
+    o = agent.opt_cfg
+    seg = agent.flat.seg.cpu().tolist()
+    snap, checked = {}, []
+
+    def probe(epoch, mbi, idx, loss, stats):
+        torch.cuda.synchronize()
+        snap.update(p=agent.flat.flat.cpu().clone(), g=agent.flat.grad.cpu().clone(), m=agent.opt_m.cpu().clone(),
+                    v=agent.opt_v.cpu().clone(), first=agent.opt_first,
+                    pi=agent.opt_p_init.cpu().clone() if agent.opt_p_init is not None else None)
+
+    def probe_step(epoch, mbi):
+        torch.cuda.synchronize()
+        p1, m1, v1 = agent.flat.flat.cpu(), agent.opt_m.cpu(), agent.opt_v.cpu()
+        g0 = snap['g']
+        norm = float(g0.double().pow(2).sum().sqrt())
+        coef = float(agent.clip_out[1])
+        assert abs(coef - min(1., agent.max_grad_norm / (norm + 1e-6))) <= 1e-6 * coef, (epoch, mbi, coef, norm)
+        g = g0 * coef
+        pp = snap['p'].clone()
+        if o['regen_rate'] > 0 and not snap['first']:
+            pp = torch.lerp(pp, snap['pi'], o['lr'] / o['init_lr'] * o['regen_rate'])
+        if snap['first']:
+            tol(m1, torch.zeros_like(m1), 0., 0.)
+            tol(v1, g * g, 2e-6, 1e-12)
+            tol(p1, pp, 0., 1e-7)
+            checked.append((epoch, mbi, 'first'))
+            return
+        u = torch.atan2(g, o['b'] * snap['v'].sqrt())
+        m = torch.lerp(snap['m'], u, 1. - o['betas'][0])
+        tol(m1, m, 2e-6, 1e-7)
+        tol(v1, torch.lerp(snap['v'], g * g, 1. - o['betas'][1]), 2e-6, 1e-12)
+        delta = torch.empty_like(p1)
+        cf = o['cautious']
+        for a0, b0 in zip(seg[:-1], seg[1:]):
+            mm, gg = m1[a0:b0], g[a0:b0]
+            align = (mm * gg) > 0
+            k = int(align.sum())
+            mean = (k + cf * (b0 - a0 - k)) / (b0 - a0) if cf < 1. else 1.
+            scale = torch.where(align, torch.ones_like(mm), torch.full_like(mm, cf)) / max(mean, 1e-5) \
+                if cf < 1. else torch.ones_like(mm)
+            delta[a0:b0] = -o['lr'] * (mm * scale * o['a'])
+        got = p1 - pp
+        ulp = torch.maximum(pp.abs(), p1.abs()) * 2. ** -23
+        bad = (got - delta).abs() > 1e-4 * delta.abs() + 4 * ulp
+        assert not bad.any(), (epoch, mbi, int(bad.sum()), float((got - delta).abs().max()))
+        checked.append((epoch, mbi))
+
+    for u in range(2):
+        traj, lens, genes, cum = learner.rollout_device(env, u, 10)
+        agent.learn(traj, lens, genes, learner.fitness(cum, genes), update=u, probe=probe, probe_step=probe_step)
+    assert len(checked) >= 8 and checked[0][-1] == 'first', checked
 
 
 @pytest.mark.parametrize('name', ['learner_readme', 'learner_lander_evo'])

@@ -359,9 +359,10 @@ class Agent(nn.Module):
         self._ema_update()
 
     # ---- learn (xtrl.py:808-1023) -----------------------------------------------------------------
-    def learn(self, traj, episode_lens, gene_ids, fitnesses=None, update=None, probe=None):
+    def learn(self, traj, episode_lens, gene_ids, fitnesses=None, update=None, probe=None, probe_step=None):
         """traj: dict of device tensors [N][Tmax][.] (rollout buffers, padded with zeros).
-        ``probe(epoch, minibatch, idx, loss, stats)`` (tests) runs after backward, before the step."""
+        ``probe(epoch, minibatch, idx, loss, stats)`` (tests) runs after backward, before the step;
+        ``probe_step(epoch, minibatch)`` (tests) right after the optimiser step."""
         c, dev = self.cfg, self.device
         update = self.step if update is None else update
         lens = episode_lens.to(dev, torch.int32)
@@ -462,6 +463,8 @@ class Agent(nn.Module):
                 if probe is not None:
                     probe(epoch, mbi, idx, loss, stats)
                 self.optimizer_step()
+                if probe_step is not None:
+                    probe_step(epoch, mbi)
                 # RSNorm copy update with the normalised masked rows (xtrl.py:1005, 598-610)
                 with torch.no_grad():
                     if fused:
