@@ -368,6 +368,11 @@ class Agent(nn.Module):
         lens = episode_lens.to(dev, torch.int32)
         N = lens.shape[0]
         n = int(lens.max().item())
+        # the genes' fitnesses on the host once per learn (evolve_ reads them on the host after every
+        # minibatch: a device tensor there was a host wait per minibatch, the GPU idling while the next
+        # minibatch was enqueued)
+        if c.evolutionary and fitnesses is not None:
+            fitnesses = fitnesses.detach().float().cpu()
         model = self.model
         boot = traj.get('boot')     # host envs: truncation-bootstrap values (NaN: none)
         _, returns = ops.hlgauss_gae(traj['values'], traj['rewards'], traj['bounds'], model.hl_centers, n,
