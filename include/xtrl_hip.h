@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 18
+#define XTRL_ABI_VERSION 19
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -532,6 +532,23 @@ typedef struct XtrlTrainDesc {
   /* world_model['use_rmsnorm'] (x-transformers RMSNorm: F.normalize(x) sqrt(d) g, no mean, eps 1e-12
    * on the norm) for every pre-norm and the final norm, forward and backward; 0: LayerNorm */
   int rms_norm;
+  /* world-model heads over the valid tokens only: Tv = sum over the minibatch of min(lens[e], n)
+   * (from the host), 0 < Tv < b n.  Their outputs feed only masked losses (xtrl.py:944, 949: the
+   * world-model and done terms of padded tokens are dropped), so to_pred / to_pred_done run on the
+   * Tv valid rows, gathered in (episode, step) order (vrows [T], vinv [T] int32 scratch: the row
+   * list and its inverse, -1 for padding), and pred / done / dewa are scattered back with zeros on
+   * the padded rows.  Tv = 0 (or vrows NULL): every row.  Compact buffers, Tv rows each:
+   * ewa_v [2d], hp_v / zp_v / dzp_v [d + 4], pred_v / d_pred_v [2 (S + 1)], dewa_v [2d] */
+  int Tv;
+  int32_t* vrows;
+  int32_t* vinv;
+  float* ewa_v;
+  float* hp_v;
+  float* zp_v;
+  float* pred_v;
+  float* d_pred_v;
+  float* dzp_v;
+  float* dewa_v;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

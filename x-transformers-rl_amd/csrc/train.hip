@@ -1148,6 +1148,84 @@ int validate(const XtrlTrainDesc* D) {
 
 }  // namespace
 
+// ---- valid-token rows of a minibatch (the world-model heads' compact form, XtrlTrainDesc.Tv) ---
+namespace {
+constexpr int VR_MAXB = 4096;
+// vrows[0 .. Tv): the valid tokens' rows e n + t (t < lens[e]) in episode, then step order;
+// vinv[r]: a row's index in that list, -1 for padding.  One workgroup (b <= VR_MAXB).
+__global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b, int n, int32_t* vrows, int32_t* vinv) {
+  __shared__ int off[VR_MAXB + 1];
+  for (int e = threadIdx.x; e < b; e += 1024) off[e + 1] = min(max(lens[e], 0), n);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    off[0] = 0;
+    for (int e = 0; e < b; ++e) off[e + 1] += off[e];
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < b * n; r += 1024) {
+    const int e = r / n, t = r - e * n;
+    if (t < off[e + 1] - off[e]) {
+      vrows[off[e] + t] = r;
+      vinv[r] = off[e] + t;
+    } else {
+      vinv[r] = -1;
+    }
+  }
+}
+// dst[i][0:cols] = src[rows[i]][0:cols] (V = 4: float4 columns)
+template <int V>
+__global__ void k_gather_rows(const float* src, int lds, const int32_t* rows, int nr, int cols, float* dst, int ldd) {
+  const int cv = cols / V;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)nr * cv) return;
+  const int r = (int)(i / cv), c = V * (int)(i - (int64_t)r * cv);
+  const float* sp = src + (int64_t)rows[r] * lds + c;
+  float* dp = dst + (int64_t)r * ldd + c;
+  if constexpr (V == 4) *reinterpret_cast<float4*>(dp) = *reinterpret_cast<const float4*>(sp);
+  else *dp = *sp;
+}
+// dst[r][0:cols] = inv[r] >= 0 ? src[inv[r]][0:cols] : 0 for r < T
+template <int V>
+__global__ void k_scatter_rows(const float* src, int lds, const int32_t* inv, int T, int cols, float* dst, int ldd) {
+  const int cv = cols / V;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)T * cv) return;
+  const int r = (int)(i / cv), c = V * (int)(i - (int64_t)r * cv);
+  const int j = inv[r];
+  float* dp = dst + (int64_t)r * ldd + c;
+  if constexpr (V == 4)
+    *reinterpret_cast<float4*>(dp) = j >= 0 ? *reinterpret_cast<const float4*>(src + (int64_t)j * lds + c)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  else
+    *dp = j >= 0 ? src[(int64_t)j * lds + c] : 0.f;
+}
+bool vec4_ok(const float* a, int lda, const float* b, int ldb, int cols) {
+  return cols % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0;
+}
+void gather_rows(const float* src, int lds, const int32_t* rows, int nr, int cols, float* dst, int ldd, hipStream_t s) {
+  const bool v4 = vec4_ok(src, lds, dst, ldd, cols);
+  const int64_t units = (int64_t)nr * (v4 ? cols / 4 : cols);
+  if (v4) hipLaunchKernelGGL(k_gather_rows<4>, dim3(blocks(units, 256)), dim3(256), 0, s, src, lds, rows, nr, cols, dst, ldd);
+  else hipLaunchKernelGGL(k_gather_rows<1>, dim3(blocks(units, 256)), dim3(256), 0, s, src, lds, rows, nr, cols, dst, ldd);
+}
+void scatter_rows(const float* src, int lds, const int32_t* inv, int T, int cols, float* dst, int ldd, hipStream_t s) {
+  const bool v4 = vec4_ok(src, lds, dst, ldd, cols);
+  const int64_t units = (int64_t)T * (v4 ? cols / 4 : cols);
+  if (v4) hipLaunchKernelGGL(k_scatter_rows<4>, dim3(blocks(units, 256)), dim3(256), 0, s, src, lds, inv, T, cols, dst, ldd);
+  else hipLaunchKernelGGL(k_scatter_rows<1>, dim3(blocks(units, 256)), dim3(256), 0, s, src, lds, inv, T, cols, dst, ldd);
+}
+// the world-model heads run on the valid rows only (XtrlTrainDesc.Tv; XTRL_HEADS_COMPACT=0: every row)
+bool heads_compact(const Ctx& c) {
+  static const bool on = [] {
+    const char* e = getenv("XTRL_HEADS_COMPACT");
+    return !(e && atoi(e) == 0);
+  }();
+  const XtrlTrainDesc* D = c.D;
+  return on && D->Tv > 0 && D->Tv < c.T && D->b <= VR_MAXB && D->vrows && D->vinv && D->ewa_v && D->hp_v &&
+         D->zp_v && D->pred_v && D->d_pred_v && D->dzp_v && D->dewa_v;
+}
+}  // namespace
+
 // ---- the heads every policy body shares (xtrl.py:533-557, fractal_rl.py:586-619) -------------
 // input: ac_in = [embed | state embed (| latent embed)], ewa = [embed | next-action embed]
 int heads_forward(const Ctx& c) {
@@ -1155,14 +1233,29 @@ int heads_forward(const Ctx& c) {
   const int T = c.T, d = D->d, ldp = d + 4;
   const hipStream_t s = c.s;
   int rc;
-  // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
-  if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
-                       nullptr, D->zp, ldp, d)))
-    return rc;
   const int S1x2 = 2 * (D->S + 1);
-  if ((rc = linear_fwd(c, D->hp, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred, S1x2, T, S1x2, d, EPI_NONE)))
-    return rc;
-  hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->hp + d, ldp, D->done, 1, T);
+  if (heads_compact(c)) {
+    // world-model heads over the Tv valid rows: their outputs feed only masked losses (xtrl.py:944,
+    // 949), the padded rows' pred / done are stored as zeros
+    const int Tv = D->Tv;
+    hipLaunchKernelGGL(k_valid_rows, dim3(1), dim3(1024), 0, s, D->lens, D->b, D->n, D->vrows, D->vinv);
+    gather_rows(D->ewa, 2 * d, D->vrows, Tv, 2 * d, D->ewa_v, 2 * d, s);
+    if ((rc = linear_fwd(c, D->ewa_v, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp_v, ldp, Tv, d + 1, 2 * d, EPI_SILU_SAVE,
+                         nullptr, D->zp_v, ldp, d)))
+      return rc;
+    if ((rc = linear_fwd(c, D->hp_v, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred_v, S1x2, Tv, S1x2, d, EPI_NONE)))
+      return rc;
+    scatter_rows(D->pred_v, S1x2, D->vinv, T, S1x2, D->pred, S1x2, s);
+    scatter_rows(D->hp_v + d, ldp, D->vinv, T, 1, D->done, 1, s);
+  } else {
+    // world-model heads: to_pred.0 | to_pred_done in one GEMM (SiLU on the first d columns)
+    if ((rc = linear_fwd(c, D->ewa, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp, ldp, T, d + 1, 2 * d, EPI_SILU_SAVE,
+                         nullptr, D->zp, ldp, d)))
+      return rc;
+    if ((rc = linear_fwd(c, D->hp, ldp, c.P(D->w_pred2), c.P(D->b_pred2), D->pred, S1x2, T, S1x2, d, EPI_NONE)))
+      return rc;
+    hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->hp + d, ldp, D->done, 1, T);
+  }
   // actor | critic first layers in one GEMM, then the two output layers
   if ((rc = linear_fwd(c, D->ac_in, D->in_dim, c.P(D->w_h1), c.P(D->b_h1), D->h1, 4 * d, T, 4 * d, D->in_dim,
                        EPI_SILU_SAVE, nullptr, D->z1, 4 * d)))
@@ -1183,6 +1276,13 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F, bool embed_cols = true)
   const int T = c.T, d = D->d, ldp = d + 4, S1x2 = 2 * (D->S + 1);
   const hipStream_t s = c.s;
   int rc;
+  // (compact world-model heads) their output gradients on the valid rows, before the first fork so
+  // the weight-gradient stream sees them: d_pred -> d_pred_v, d_done -> column d of dzp_v
+  const bool cmp = heads_compact(c);
+  if (cmp) {
+    gather_rows(D->d_pred, S1x2, D->vrows, D->Tv, S1x2, D->d_pred_v, S1x2, s);
+    gather_rows(D->d_done, 1, D->vrows, D->Tv, 1, D->dzp_v + d, ldp, s);
+  }
   // ---- actor / critic heads
   if ((rc = F.fork())) return rc;
   if ((rc = wgrad(cw, D->d_raw, D->n_out, D->h1, 4 * d, c.G(D->w_a2), T, D->n_out, 2 * d, c.G(D->b_a2)))) return rc;
@@ -1215,6 +1315,19 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F, bool embed_cols = true)
     XTRL_LAUNCHED("train latent grad");
   }
   // ---- world-model heads
+  if (cmp) {   // on the Tv valid rows; dewa's padded rows are zero (their dzp rows were)
+    const int Tv = D->Tv;
+    if ((rc = wgrad(cw, D->d_pred_v, S1x2, D->hp_v, ldp, c.G(D->w_pred2), Tv, S1x2, d, c.G(D->b_pred2)))) return rc;
+    if ((rc = linear_dgrad(c, D->d_pred_v, S1x2, c.P(D->w_pred2), D->dzp_v, ldp, Tv, S1x2, d, EPI_MUL_AUX, D->zp_v,
+                           ldp)))
+      return rc;
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dzp_v, ldp, D->ewa_v, 2 * d, c.G(D->w_pd), Tv, d + 1, 2 * d, c.G(D->b_pd)))) return rc;
+    if ((rc = linear_dgrad(c, D->dzp_v, ldp, c.P(D->w_pd), D->dewa_v, 2 * d, Tv, d + 1, 2 * d, EPI_NONE))) return rc;
+    scatter_rows(D->dewa_v, 2 * d, D->vinv, T, 2 * d, D->dewa, 2 * d, s);
+    XTRL_LAUNCHED("train heads backward (compact)");
+    return XTRL_OK;
+  }
   if ((rc = wgrad(cw, D->d_pred, S1x2, D->hp, ldp, c.G(D->w_pred2), T, S1x2, d, c.G(D->b_pred2)))) return rc;
   if ((rc = linear_dgrad(c, D->d_pred, S1x2, c.P(D->w_pred2), D->dzp, ldp, T, S1x2, d, EPI_MUL_AUX, D->zp, ldp))) return rc;
   hipLaunchKernelGGL(k_copy_col, dim3(blocks(T, 256)), dim3(256), 0, s, D->d_done, 1, D->dzp + d, ldp, T);

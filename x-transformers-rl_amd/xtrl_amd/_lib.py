@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -103,7 +103,9 @@ class TrainDesc(C.Structure):
                    ('prof_events', C.POINTER(C.c_void_p)), ('prof_flops', P), ('prof_cap', I32), ('prof_n', P),
                    ('grad_events', C.POINTER(C.c_void_p)), ('ld_ff', I32),
                    ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P),
-                   ('qk_norm', I32), ('xpos_base', F32), ('rms_norm', I32)])
+                   ('qk_norm', I32), ('xpos_base', F32), ('rms_norm', I32),
+                   ('Tv', I32), ('vrows', P), ('vinv', P), ('ewa_v', P), ('hp_v', P), ('zp_v', P), ('pred_v', P),
+                   ('d_pred_v', P), ('dzp_v', P), ('dewa_v', P)])
 
 
 class FractalTrainLevel(C.Structure):

@@ -367,7 +367,8 @@ class Agent(nn.Module):
         update = self.step if update is None else update
         lens = episode_lens.to(dev, torch.int32)
         N = lens.shape[0]
-        n = int(lens.max().item())
+        lens_host = episode_lens.detach().to('cpu', torch.int64)   # (the learn's one length read)
+        n = int(lens_host.max())
         # the genes' fitnesses on the host once per learn (evolve_ reads them on the host after every
         # minibatch: a device tensor there was a host wait per minibatch, the GPU idling while the next
         # minibatch was enqueued)
@@ -388,8 +389,8 @@ class Agent(nn.Module):
         model.train()
         # the epochs' minibatch orders (host generator: bit parity with torch.randperm), uploaded from
         # pinned memory without a host wait — the learn's only host round trip is the length max above
-        perms = torch.stack([epoch_permutation(self.seed, update, e, N) for e in range(self.epochs)])
-        perms = _to_device_async(perms, dev)
+        perms_host = torch.stack([epoch_permutation(self.seed, update, e, N) for e in range(self.epochs)])
+        perms = _to_device_async(perms_host, dev)
         sd = self.rs_var.sqrt().clamp(min=1e-5)
         lo, hi = c.reward_range
         fused = self.fused_learn
@@ -434,8 +435,10 @@ class Agent(nn.Module):
                 attn_seed, attn_off, ff_off = self.seed * 1000003 + update, ordinal * attn_stride, ordinal
                 if self.fused_learn:
                     step = self.train_step(b, n)
+                    # the minibatch's valid-token count, from the host copies (no device read)
+                    n_valid = int(lens_host[perms_host[epoch, k:k + self.batch_size]].clamp(max=n).sum())
                     step.forward(swr, prev_act, mb_act, latent, mb_lens, keep, attn_seed, attn_off, ff_off,
-                                 c.dropout)
+                                 c.dropout, Tv=n_valid)
                 else:
                     act_in = prev_act if c.continuous else prev_act.long()
                     nxt = mb_act if c.continuous else mb_act.long()

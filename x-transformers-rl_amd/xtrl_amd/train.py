@@ -32,6 +32,21 @@ def _span_off(flat, names):
     return flat.index[names[0]][0]
 
 
+def _compact_bufs(D, c, T, dev):
+    """The world-model heads' valid-row buffers (XtrlTrainDesc.Tv): row list / inverse and the compact
+    operands, T rows each (the most a minibatch can have valid)."""
+    d, ldp, S1x2 = c.dim, c.dim + 4, 2 * (c.state_dim + 1)
+    f32 = dict(device=dev, dtype=torch.float32)
+    bufs = dict(vrows=torch.empty(T, device=dev, dtype=torch.int32), vinv=torch.empty(T, device=dev, dtype=torch.int32),
+                ewa_v=torch.empty(T, 2 * d, **f32), hp_v=torch.empty(T, ldp, **f32), zp_v=torch.empty(T, ldp, **f32),
+                pred_v=torch.empty(T, S1x2, **f32), d_pred_v=torch.empty(T, S1x2, **f32),
+                dzp_v=torch.empty(T, ldp, **f32), dewa_v=torch.empty(T, 2 * d, **f32))
+    for k, t in bufs.items():
+        setattr(D, k, t.data_ptr())
+    D.Tv = 0
+    return bufs
+
+
 def _heads_desc(D, c, flat):
     """Offsets of the heads every policy body shares (xtrl.py:533-557, fractal_rl.py:586-619)."""
     off = lambda n: _off(flat, n)
@@ -150,24 +165,29 @@ class FusedTrainStep:
         D.ld_ff = lff
         D.scratch_per_layer = 1   # per-layer backward planes (no mid-backward stream waits)
         D.ff_glu, D.ld_u2 = int(glu), (lu2 if glu else 0)
+        self.cbuf = _compact_bufs(D, c, T, dev)
         self.D = D
 
     # ------------------------------------------------------------------------------------------
     def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                dropout):
+                dropout, Tv=0):
         """swr [b][n][S+1] normalised states | previous reward; actions [b][n] int32 (discrete) or
-        [b][n][A] float (continuous); latent [b][G] or None; lens [b] int32.
+        [b][n][A] float (continuous); latent [b][G] or None; lens [b] int32.  ``Tv``: the number of
+        valid tokens (sum of min(lens, n), known on the host) — the world-model heads then run on
+        those rows only and pred / done hold zeros on the padding; 0: every row.
         Returns views raw [b][n][n_out], values [b][n][B], pred [b][n][2(S+1)], done [b][n]."""
         self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                          dropout)
+                          dropout, Tv)
         L.check(L.lib().xtrl_train_forward(C.byref(self.D), L.stream()), 'train_forward')
         return self._outputs()
 
     def _bind_inputs(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                     dropout):
+                     dropout, Tv=0):
         c, D = self.cfg, self.D
         b, n = swr.shape[0], swr.shape[1]
         assert b <= self.b_max and n <= self.n_max, (b, n, self.b_max, self.n_max)
+        assert 0 <= Tv <= b * n, (Tv, b, n)
+        D.Tv = int(Tv) if Tv < b * n else 0
         for t in (swr, prev_action, next_action, lens):
             assert t.is_cuda and t.is_contiguous()
         self._keep = [swr, prev_action, next_action, latent, lens]
@@ -317,6 +337,7 @@ class FractalTrainStep(FusedTrainStep):
         D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
         D.layers = None
         D.ld_ff = lff
+        self.cbuf = _compact_bufs(D, c, T, dev)
         self.D = D
         Fd = L.FractalTrainDesc()
         Fd.levels = Lv
@@ -331,9 +352,9 @@ class FractalTrainStep(FusedTrainStep):
         self.Fd = Fd
 
     def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                dropout):
+                dropout, Tv=0):
         self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                          dropout)
+                          dropout, Tv)
         L.check(L.lib().xtrl_fractal_train_forward(C.byref(self.D), C.byref(self.Fd), L.stream()),
                 'fractal_train_forward')
         return self._outputs()
