@@ -898,11 +898,21 @@ struct SideStream {
   hipStream_t s = nullptr;
   std::vector<hipEvent_t> ev;
   bool ok = false;
-  // at least n events (false: creation failed, the caller runs single-stream)
+  // at least n events (false: creation failed, the caller runs single-stream).  The fork / join
+  // events only order two streams of this device, so they are recorded with a device-scope
+  // release instead of the default system-scope fence (the kernels' own end-of-kernel release and
+  // start-of-kernel acquire carry the data): the main stream's gap at a fork shrinks, C3 learn
+  // −0.7 ms.  XTRL_FORK_FENCE=0: system scope (the HIP default); 2: no fence at all (A/B only)
   bool ensure(size_t n) {
+    static const unsigned flags = [] {
+      const char* f = getenv("XTRL_FORK_FENCE");
+      const int v = f ? atoi(f) : 1;
+      return (unsigned)hipEventDisableTiming |
+             (v == 1 ? (unsigned)hipEventReleaseToDevice : v == 2 ? (unsigned)hipEventDisableSystemFence : 0u);
+    }();
     while (ok && ev.size() < n) {
       hipEvent_t e = nullptr;
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+      if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return false;
       ev.push_back(e);
     }
     return ok;
