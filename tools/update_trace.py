@@ -46,7 +46,7 @@ def show(path):
     t0 = int(rows[upd[0]]['Start_Timestamp'])
     t1 = int(rows[upd[-1]]['End_Timestamp'])
     print(f'update: {len(upd)} kernels, wall {(t1 - t0) / 1e6:.2f} ms, busy {sum(dur[i] for i in upd) / 1e3:.2f} ms')
-    gathers = [i for i in upd if 'k_gather' in names[i]]
+    gathers = [i for i in upd if 'k_gather' in names[i] and 'k_gather_rows' not in names[i]]
     # (the reference-mode learn step of the fractal body has no device gather: the learn phase then
     # starts at the GAE launch)
     first = gathers[:1] or [i for i in upd if 'k_hlgauss_gae' in names[i]][:1]
