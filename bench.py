@@ -2,7 +2,11 @@
 """Benchmark: env-steps/s of the Learner hot path (rollout + learn) on N MI355X, weak scaling.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5|c1]
-    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+``--gpus N`` with N > 1 and no launcher around it (no WORLD_SIZE) starts the N ranks itself:
+this script re-runs under ``torch.distributed.run`` as a child process (launch_ranks) before the
+parent touches the GPU.  Under a launcher, ``--gpus`` must equal WORLD_SIZE.
 
 One "step" = one learning update of the reference Learner loop (xtrl.py:1204-1373): a rollout of
 every (episode, gene) pair of this rank on the device Sim, then Agent.learn (GAE + epochs x
@@ -436,9 +440,11 @@ def cpu_baseline(cfg, seed, budget_s, threads=None, episodes=None, reps=5):
                        f'(oracle/ref_port.OracleLearner, batch-1 KV-cached decode like xtrl.py:1250-1341)')
 
 
-def ppo_loss_delta(learner, env, cfg):
+def ppo_loss_delta(learner, env, cfg, check=True):
     """|L_gpu - L_cpu| / |L_cpu| on the first minibatch of one more update, identical weights /
-    RSNorm / minibatch tensors; the CPU side is the oracle's restatement."""
+    RSNorm / minibatch tensors; the CPU side is the oracle's restatement.  Every rank
+    runs the update (its learn all-reduces gradients); ``check`` (rank 0) compares its local first
+    minibatch, the others return None."""
     from oracle import ref_port as R
     agent = learner.agent
     c = agent.cfg
@@ -458,7 +464,7 @@ def ppo_loss_delta(learner, env, cfg):
         model = R.OracleWMAC(mc)
 
     def probe(epoch, mbi, idx, loss, stats):
-        if out:
+        if out or not check:
             return
         idx_c = idx.cpu()
         n = int(lens.max())
@@ -487,8 +493,36 @@ def ppo_loss_delta(learner, env, cfg):
     agent.learn(traj, lens, genes, learner.fitness(cum, genes), update=u, probe=probe)
     agent.logs = []
     c.dropout = saved_p
+    if not check:
+        return None
     out['rel_delta'] = abs(out['gpu'] - out['cpu']) / max(abs(out['cpu']), 1e-12)
     return out
+
+
+def launch_ranks(n):
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: run this script under
+    ``torch.distributed.run`` with N local ranks (one per GPU, or ranks sharing the GPUs under
+    XTRL_BENCH_BACKEND=gloo) as a CHILD process and return its exit code — the parent never
+    initialises the GPU (device_count() only reads the topology), so nothing is exec-ed over a live
+    HIP context.  Rank 0's line is the job's line."""
+    import socket
+    import subprocess
+    backend = os.environ.get('XTRL_BENCH_BACKEND', 'nccl')
+    have = torch.cuda.device_count()
+    if backend == 'nccl' and have < n:
+        print(f'bench.py: --gpus {n} needs {n} GPUs, {have} visible (XTRL_BENCH_BACKEND=gloo shares them)',
+              file=sys.stderr)
+        return 2
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')   # RCCL over dmabuf IPC (the pool's driver)
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    print(f'[bench] launching {n} ranks: {" ".join(cmd[1:])}', file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -504,9 +538,14 @@ def main():
     ap.add_argument('--no-loss-delta', action='store_true')
     args = ap.parse_args()
 
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks ourselves (before this process touches the GPU)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks')
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         # XTRL_BENCH_BACKEND=gloo: multi-rank rehearsal on fewer GPUs than ranks (ranks share devices)
@@ -651,27 +690,37 @@ def main():
         total_roof = total_roofline(value, work, roofline.get('mfma_busy') if roofline else None)
     loss_delta = None
     cpu = None
-    # the loss-delta check runs one more update (its learn all-reduces gradients) and the CPU
-    # baseline is an N = 1 figure: both only in single-process runs, so no rank waits in a
-    # collective the others never enter
-    if world == 1:
+    # the loss-delta check runs one more update on EVERY rank (its learn all-reduces gradients; rank 0
+    # compares its local first minibatch with the CPU restatement), then the process group ends and
+    # rank 0 alone times the CPU baseline, so no rank waits in a collective the others never enter
+    if not (args.no_loss_delta or host):
         try:
-            loss_delta = None if (args.no_loss_delta or host) else ppo_loss_delta(learner, env, cfg)
+            loss_delta = ppo_loss_delta(learner, env, cfg, check=(rank == 0))
         except Exception as e:   # reported, never hidden
             loss_delta = dict(error=repr(e))
-        if not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, args.seed, 20.)
-            phys, share = host_cores()
-            one = cpu_baseline(cfg, args.seed, 20., threads=1,
-                               episodes=8 if cfg.get('fractal') else 32 if cfg['T'] >= 100 else 128, reps=3)
-            cpu.update(host_physical_cores=phys, host_cpu_share=share,
-                       single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
+    backend_name = dist.get_backend() if world > 1 else None
+    coll_dp = None
+    if coll is not None:
+        mb = learner.agent.epochs * (len(learner.episode_genes_for_process) // learner.agent.batch_size)
+        coll_dp = dict(backend=backend_name, world_size=dist.get_world_size(), collectives_per_update=coll,
+                       optimiser_steps_per_update=mb, grad_allreduces_per_step=round(coll['all_reduce'] / mb, 3))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, args.seed, 20.)
+        phys, share = host_cores()
+        one = cpu_baseline(cfg, args.seed, 20., threads=1,
+                           episodes=8 if cfg.get('fractal') else 32 if cfg['T'] >= 100 else 128, reps=3)
+        cpu.update(host_physical_cores=phys, host_cpu_share=share,
+                   single_thread=dict(value=one['value'], cores=1, sample=one['sample']))
     if rank == 0:
         line = dict(metric='env-steps/s (rollout+update)', value=round(value, 1), unit='env-steps/s', n_gpus=world,
                     value_median=round(value_median, 1), ms_per_step_median=round(ms_median, 2),
                     value_probed=None if value_probed is None else round(value_probed, 1),
                     steps=args.steps, warmup=args.warmup, ms_per_step=round(1e3 * elapsed / args.steps, 2),
                     higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f32',
+                    backend=backend_name or 'single-process', world_size=world,
                     data=('synthetic (numpy LunarLander-shaped host vector env, random-init weights)' if cfg.get('vector') else
                           'synthetic (numpy LunarLander-shaped scalar host env, random-init weights)' if host else
                           'synthetic (Philox LunarLander-shaped VecSim on device, random-init weights)'),
@@ -688,14 +737,9 @@ def main():
                 note='per host-env step, host clock: decode = the decode launches + the wait for the actions '
                      '(device->host copy included); env = the env step; feedback = staging + host->device copy + '
                      'the feedback kernel launch')
-        if coll is not None:
-            mb = learner.agent.epochs * (len(learner.episode_genes_for_process) // learner.agent.batch_size)
-            line['dp'] = dict(backend=dist.get_backend(), collectives_per_update=coll,
-                              optimiser_steps_per_update=mb,
-                              grad_allreduces_per_step=round(coll['all_reduce'] / mb, 3))
-        print(json.dumps(line))
-    if world > 1:
-        dist.destroy_process_group()
+        if coll_dp is not None:
+            line['dp'] = coll_dp
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == '__main__':

@@ -152,7 +152,9 @@ typedef struct XtrlDecodeDesc {
   float* prev_action_f;    /* [E][A] continuous */
   float* prev_reward;      /* [E] */
   uint8_t* alive;          /* [E] 0 dead, 1 live, 2 bootstrap step pending, 3 + (t & 1) ended at step t by
-                              xtrl_decode_step_rows (dead from step t + 1 on) */
+                              xtrl_decode_step_rows (dead from step t + 1 on; no step clears the markers
+                              of the last step: read alive >= 3 as dead — the Python RolloutEngine
+                              zeroes them when a rollout ends) */
   int32_t* lens;           /* [E] episode length so far */
   double* cum_reward;      /* [E] cumulative reward (fitness, xtrl.py:1310, 1345-1346) */
   const int32_t* episode_of_slot;  /* [E] episode index keying the Sim stream */

@@ -351,3 +351,77 @@ def test_c5_population8_eight_ranks_one_gene_each(tmp_path):
         for rank in range(1, world):
             assert torch.equal(r[0][k], r[rank][k]), (k, rank)
     assert torch.isfinite(r[0]['flat']).all() and not torch.equal(r[0]['flat'], flat0.cpu())
+
+
+def _world1_rccl_worker(rank, port, out_dir):
+    """One rank: a learning update's gradients without a process group, then the same update (same
+    weights, RSNorm state and minibatches) with a world-1 RCCL group and XTRL_DP_WORLD1=1, so every
+    optimiser step's gradient goes through BucketAllReduce: the comm stream waits for the backward's
+    per-bucket events and RCCL all-reduces each bucket."""
+    sys.path[:0] = [str(REPO), str(REPO / 'x-transformers-rl_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1', LOCAL_RANK='0',
+                      XTRL_DP_WORLD1='1', XTRL_DP_BUCKET_FLOATS='1')
+    import torch.distributed as dist
+    from xtrl_amd import distributed as dist_
+    torch.cuda.set_device(0)
+    learner, env = _make(1, evo=False)
+    a = learner.agent
+    a.opt_cfg['lr'] = 0.
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 20)
+    rs0 = (a.rs_mean.clone(), a.rs_var.clone(), a.rs_step)
+    plain = []
+    a.learn(traj, lens, genes, None, update=0, probe=_grad_probe(a, plain))
+    assert a.bucket_allreduce() is None
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda', 0))
+    try:
+        a.rs_mean, a.rs_var, a.rs_step = rs0[0].clone(), rs0[1].clone(), rs0[2]
+        a.step = 0
+        bar = a.bucket_allreduce()
+        assert bar is not None and dist.get_backend() == 'nccl'
+        rccl = []
+        coll0 = dist_.COUNTS['all_reduce']
+        a.learn(traj, lens, genes, None, update=0, probe=_grad_probe(a, rccl))
+        torch.save(dict(plain=plain, rccl=rccl, allreduces=dist_.COUNTS['all_reduce'] - coll0,
+                        buckets=len(bar.groups), depth=a.cfg.depth),
+                   os.path.join(out_dir, 'rank0.pt'))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_world1_rccl_bucket_allreduce_leaves_gradient_unchanged(tmp_path):
+    """The RCCL data path on hardware: a world-1 ``nccl`` (RCCL) process group forced through
+    BucketAllReduce (XTRL_DP_WORLD1=1, one collective per backward bucket).  Every optimiser step's
+    gradient — its all-reduce over one rank divided by 1 — equals bitwise the gradient of the same step
+    without a process group, and each step makes one RCCL all-reduce per bucket (depth + 2)."""
+    mp.start_processes(_world1_rccl_worker, args=(_free_port(), str(tmp_path)), nprocs=1, start_method='spawn')
+    r = torch.load(tmp_path / 'rank0.pt', weights_only=True)
+    steps = len(r['plain'])
+    assert steps > 0 and len(r['rccl']) == steps
+    assert r['buckets'] == r['depth'] + 2
+    assert r['allreduces'] == steps * r['buckets'], (r['allreduces'], steps, r['buckets'])
+    for i, (g0, g1) in enumerate(zip(r['plain'], r['rccl'])):
+        assert torch.equal(g0, g1), i
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_self_launches_two_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher starts two ranks itself (torch.distributed.run as a
+    child process); under XTRL_BENCH_BACKEND=gloo they share the one GPU.  Rank 0's line reports 2 GPUs,
+    the gloo backend, the C3 bucketed all-reduce (3 collectives per optimiser step) and — at N > 1 —
+    the PPO loss delta (every rank ran the extra update)."""
+    import json
+    import subprocess
+    env = dict(os.environ, XTRL_BENCH_BACKEND='gloo')
+    env.pop('WORLD_SIZE', None)
+    p = subprocess.run([sys.executable, '-u', str(REPO / 'bench.py'), '--gpus', '2', '--steps', '1', '--warmup', '0',
+                        '--no-cpu-baseline', '--no-roofline'], cwd=str(REPO), env=env, capture_output=True, text=True,
+                       timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([x for x in p.stdout.splitlines() if x.startswith('{')][-1])
+    assert line['n_gpus'] == 2 and line['world_size'] == 2 and line['backend'] == 'gloo'
+    assert line['config']['parallelism'] == 'dp2'
+    assert line['dp']['world_size'] == 2
+    assert line['dp']['grad_allreduces_per_step'] == 3
+    assert line['ppo_loss'] is not None and line['ppo_loss']['rel_delta'] <= 1e-4, line['ppo_loss']

@@ -659,7 +659,8 @@ def test_row_step_oversubscribed_grid_matches_multi_kernel_and_oracle(monkeypatc
     torch.cuda.synchronize()
     rows_out = {k: v.clone() for k, v in traj.items() if v is not None}
     rows_lens = lens.clone()
-    assert set(eng.alive.cpu().tolist()) <= {0, 3, 4}   # (dead, or ended by the last row step)
+    # the ended-at-step markers (3 / 4) of the last row step are cleared at the rollout's end
+    assert set(eng.alive.cpu().tolist()) <= {0, 1}
     monkeypatch.setattr(eng, 'rows_max', 0)   # the multi-kernel step
     traj, lens, _, _ = learner.rollout_device(env, 0, T)
     torch.cuda.synchronize()
@@ -1794,3 +1795,52 @@ def test_learner_call_runs_batched_vector_env():
     learner, _, _ = make_learner(depth=1, gates=False, T=8, episodes=8, batch=4)
     learner(HostLanderVec(8, ret=5, limit=6), 2)
     assert learner.agent.step == 2 and torch.isfinite(learner.agent.flat.flat).all()
+
+
+@pytest.mark.parametrize('fractal', (None, 2))
+def test_compact_world_model_heads_match_full_rows(fractal):
+    """The world-model heads on the valid rows only (XtrlTrainDesc.Tv = sum(min(lens, n)): the row
+    list, the gather, the compact GEMMs and the scatter back) against the same fused step over every
+    row (Tv = 0), on a first minibatch with ragged episode lengths: pred and done agree on the valid
+    rows and are exactly zero on the padding, the loss agrees, and every gradient tensor — the heads'
+    to_pred / to_pred_done weights included — is within 1e-4 of its own scale."""
+    learner, env, _ = make_learner(depth=2, gates=fractal is None, T=40, episodes=8, batch=8, hazard=4, dim=64,
+                                   fractal_levels=fractal)
+    agent = learner.agent
+    traj, lens, genes, cum = learner.rollout_device(env, 0, 40)
+    fit = learner.fitness(cum, genes)
+    lens_h = lens.cpu()
+    assert lens_h.min() < lens_h.max(), lens_h   # ragged: the minibatch has padding
+    out = {}
+    for compact in (True, False):
+        agent.heads_compact = compact
+        got = {}
+
+        def probe(epoch, mbi, idx, loss, stats, got=got):
+            ts = agent._train_step
+            b, n = ts.D.b, ts.D.n
+            got.update(loss=float(loss.detach()), grad=agent.flat.grad.detach().clone(), n=n,
+                       lens=lens_h[idx.cpu()].clamp(max=n), Tv=ts.D.Tv,
+                       pred=ts.buf['pred'][:b * n].view(b, n, -1).clone(), done=ts.buf['done'][:b * n].view(b, n).clone())
+            raise _Captured()
+
+        with pytest.raises(_Captured):
+            agent.learn(traj, lens, genes, fit, update=0, probe=probe)
+        agent.step = 0
+        out[compact] = got
+    cp, fu = out[True], out[False]
+    assert cp['Tv'] == int(cp['lens'].sum()) > 0 and fu['Tv'] == 0
+    valid = (torch.arange(cp['n'])[None, :] < cp['lens'][:, None]).to(cp['pred'].device)
+    assert (cp['pred'][~valid] == 0).all() and (cp['done'][~valid] == 0).all()
+    for k in ('pred', 'done'):
+        a, b = cp[k][valid], fu[k][valid]
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-7, k
+    assert abs(cp['loss'] - fu['loss']) <= 1e-5 * abs(fu['loss'])
+    bad = []
+    for name, (a0, a1) in agent.flat.index.items():
+        g0, g1 = cp['grad'][a0:a1], fu['grad'][a0:a1]
+        own = float(g1.abs().max())
+        if float((g0 - g1).abs().max()) > 1e-4 * own + 1e-7:
+            bad.append((name, float((g0 - g1).abs().max()), own))
+    assert not bad, bad
+    assert any('to_pred' in n for n in agent.flat.index)

@@ -1,5 +1,7 @@
 """CPU-only checks of the product's host side and of the C-ABI library (no kernel launches)."""
 import ctypes
+import os
+import sys
 import re
 from pathlib import Path
 
@@ -291,3 +293,12 @@ def test_world_model_options_defaults_accepted_others_named():
     # use_rmsnorm: x-transformers RMSNorm's gain is named g (LayerNorm's gamma)
     r = Learner(5, 2, (-1., 1.), world_model=dict(base, use_rmsnorm=True), **kw).agent.model.state_dict()
     assert [k.replace('.gamma', '.g') for k in b.agent.model.state_dict()] == list(r)
+
+
+def test_bench_refuses_gpus_world_size_mismatch():
+    """Under a launcher, ``--gpus`` must equal WORLD_SIZE (bench.py exits before touching the GPU)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE='2', RANK='0', LOCAL_RANK='0')
+    p = subprocess.run([sys.executable, str(REPO / 'bench.py'), '--gpus', '1'], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode != 0 and 'WORLD_SIZE=2' in p.stderr

@@ -1162,8 +1162,12 @@ int validate(const XtrlTrainDesc* D) {
 namespace {
 constexpr int VR_MAXB = 4096;
 // vrows[0 .. Tv): the valid tokens' rows e n + t (t < lens[e]) in episode, then step order;
-// vinv[r]: a row's index in that list, -1 for padding.  One workgroup (b <= VR_MAXB).
-__global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b, int n, int32_t* vrows, int32_t* vinv) {
+// vinv[r]: a row's index in that list, -1 for padding.  One workgroup (b <= VR_MAXB).  Tv (the
+// host's count, sizing the compact GEMMs) is trusted for nothing: list entries at or past Tv are
+// never written and their rows scatter as padding, and list slots past the device count read row 0,
+// so a wrong Tv gives wrong heads outputs but no out-of-range or stale access.
+__global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b, int n, int Tv, int32_t* vrows,
+                                                     int32_t* vinv) {
   __shared__ int off[VR_MAXB + 1];
   for (int e = threadIdx.x; e < b; e += 1024) off[e + 1] = min(max(lens[e], 0), n);
   __syncthreads();
@@ -1174,13 +1178,15 @@ __global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b,
   __syncthreads();
   for (int r = threadIdx.x; r < b * n; r += 1024) {
     const int e = r / n, t = r - e * n;
-    if (t < off[e + 1] - off[e]) {
-      vrows[off[e] + t] = r;
-      vinv[r] = off[e] + t;
+    const int j = off[e] + t;
+    if (t < off[e + 1] - off[e] && j < Tv) {
+      vrows[j] = r;
+      vinv[r] = j;
     } else {
       vinv[r] = -1;
     }
   }
+  for (int j = off[b] + threadIdx.x; j < Tv; j += 1024) vrows[j] = 0;
 }
 // dst[i][0:cols] = src[rows[i]][0:cols] (V = 4: float4 columns)
 template <int V>
@@ -1248,7 +1254,7 @@ int heads_forward(const Ctx& c) {
     // world-model heads over the Tv valid rows: their outputs feed only masked losses (xtrl.py:944,
     // 949), the padded rows' pred / done are stored as zeros
     const int Tv = D->Tv;
-    hipLaunchKernelGGL(k_valid_rows, dim3(1), dim3(1024), 0, s, D->lens, D->b, D->n, D->vrows, D->vinv);
+    hipLaunchKernelGGL(k_valid_rows, dim3(1), dim3(1024), 0, s, D->lens, D->b, D->n, D->Tv, D->vrows, D->vinv);
     gather_rows(D->ewa, 2 * d, D->vrows, Tv, 2 * d, D->ewa_v, 2 * d, s);
     if ((rc = linear_fwd(c, D->ewa_v, 2 * d, c.P(D->w_pd), c.P(D->b_pd), D->hp_v, ldp, Tv, d + 1, 2 * d, EPI_SILU_SAVE,
                          nullptr, D->zp_v, ldp, d)))

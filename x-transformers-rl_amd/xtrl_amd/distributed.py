@@ -21,6 +21,15 @@ def is_distributed():
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+def dp_active():
+    """The learner's gradient collectives run: a process group of more than one rank — or, with
+    XTRL_DP_WORLD1=1, any initialised group, so a test can drive the bucketed RCCL all-reduce at
+    world 1 on a one-GPU box (the mean over one rank leaves the gradient unchanged)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or os.environ.get('XTRL_DP_WORLD1', '0') == '1'
+
+
 def world_and_rank():
     if not is_distributed():
         return 1, 0

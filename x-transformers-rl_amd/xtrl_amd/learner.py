@@ -222,6 +222,8 @@ class Agent(nn.Module):
         self._deploy = None
         self._genes_dev = None
         self.fused_learn = fused_learn   # False: reference-mode autograd learn step (tests)
+        # the world-model heads on the minibatch's valid rows only (XtrlTrainDesc.Tv); False: every row
+        self.heads_compact = True
         # host envs: a truncated (not terminated) episode bootstraps GAE from the next state's value
         # (the intent of xtrl.py:1323-1336, whose bootstrap memory lands outside the episode list)
         self.truncation_bootstrap = truncation_bootstrap
@@ -438,7 +440,7 @@ class Agent(nn.Module):
                     # the minibatch's valid-token count, from the host copies (no device read)
                     n_valid = int(lens_host[perms_host[epoch, k:k + self.batch_size]].clamp(max=n).sum())
                     step.forward(swr, prev_act, mb_act, latent, mb_lens, keep, attn_seed, attn_off, ff_off,
-                                 c.dropout, Tv=n_valid)
+                                 c.dropout, Tv=n_valid if self.heads_compact else 0)
                 else:
                     act_in = prev_act if c.continuous else prev_act.long()
                     nxt = mb_act if c.continuous else mb_act.long()
@@ -500,7 +502,7 @@ class Agent(nn.Module):
     def bucket_allreduce(self):
         """The overlapped bucketed all-reduce of the fused learn step (None: one process, or
         XTRL_DP_BUCKETS=0 for one all-reduce after the backward)."""
-        if not dist_.is_distributed() or os.environ.get('XTRL_DP_BUCKETS', '1') == '0' \
+        if not dist_.dp_active() or os.environ.get('XTRL_DP_BUCKETS', '1') == '0' \
                 or not hasattr(self.model, 'flat_bucket_ranges') or self.flat.flat.device.type != 'cuda':
             return None
         bar = getattr(self, '_bar', None)

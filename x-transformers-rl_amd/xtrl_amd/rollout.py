@@ -361,6 +361,7 @@ class RolloutEngine:
         self._begin(seed, update, slot_offset, episode_of_slot, latent, slots)
         if not self.use_graph:
             self._steps()
+            self._clear_end_markers()
             return self.traj
         if self.graph is None:
             self._steps()   # warm-up launch outside capture (code objects loaded)
@@ -405,7 +406,15 @@ class RolloutEngine:
                 if live == 0:
                     break
                 rows = rows or live <= self.rows_max
+        self._clear_end_markers()
         return self.traj
+
+    def _clear_end_markers(self):
+        """The row-resident step marks a row it ended with alive = ALIVE_END + (t & 1) (3 / 4, live for
+        the rest of that launch; csrc/decode.hip ``live_at``) and the next step's compaction clears it.
+        After the rollout's last step no compaction follows: clear them here so ``alive`` leaves the
+        rollout with 0 = dead, 1 = live only (no host sync: two stream-ordered ops)."""
+        self.alive.mul_(self.alive.lt(3))
 
     def _host_decode(self, t, rows_max, desc, act_p, stream):
         """Decode step t of a host-env wave, its actions to the pinned buffer, one host wait."""
