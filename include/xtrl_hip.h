@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 19
+#define XTRL_ABI_VERSION 20
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -394,6 +394,17 @@ int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t*
                   const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws, int b,
                   int H, int n, int dh, float scale, float dropout_p, uint64_t seed, uint32_t offset, uint32_t sub,
                   void* stream);
+/* xtrl_attn_bwd with a workspace for long episodes (n > 128, dh = 16; same backward, xtrl.py:981 over
+ * the attention of :928-935): the dK / dV kernel forms dQ from the same P / dS per (key tile, query
+ * tile) pair — rows with one contributing key tile get dQ directly (bit-identical to xtrl_attn_bwd),
+ * the others one partial per key tile in dq_part, summed in key-tile order by a reduce launch.
+ * dq_part_floats >= xtrl_attn_bwd_part_floats(b, H, n, dh) = ceil(n / 64) * b * H * n * dh; a smaller
+ * (or NULL) workspace takes xtrl_attn_bwd's kernel pair. */
+int64_t xtrl_attn_bwd_part_floats(int b, int H, int n, int dh);
+int xtrl_attn_bwd_part(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
+                       const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
+                       float* dq_part, int64_t dq_part_floats, int b, int H, int n, int dh, float scale,
+                       float dropout_p, uint64_t seed, uint32_t offset, uint32_t sub, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Learn-step forward / backward of WorldModelActorCritic on one minibatch, hand-scheduled (no
@@ -551,6 +562,10 @@ typedef struct XtrlTrainDesc {
   float* d_pred_v;
   float* dzp_v;
   float* dewa_v;
+  /* long episodes (n > 128, dh = 16): the attention backward's dQ partial workspace
+   * (xtrl_attn_bwd_part_floats(b, H, n, dh) floats), or NULL for the dK / dV + dQ kernel pair */
+  float* dq_part;
+  int64_t dq_part_floats;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);

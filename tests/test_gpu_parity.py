@@ -313,6 +313,45 @@ def test_attention_fused_backward_matches_two_kernel(b, H, n, p):
         assert torch.equal(two[name], fus[name]), (name, report)
 
 
+@pytest.mark.parametrize('b,H,n,p', [(3, 4, 257, 0.25), (2, 4, 430, 0.25), (3, 2, 500, 0.1), (2, 4, 500, 0.)])
+def test_attention_long_backward_dq_folded_matches_two_kernel(b, H, n, p):
+    """Long episodes (n > 128, C2's padded widths): the dK / dV kernel with the dQ pass folded in
+    (xtrl_attn_bwd_part: dQ from the same P / dS per (key tile, query tile) pair, per-key-tile partials
+    for rows with several contributing key tiles, summed in key-tile order) against the dK/dV + dQ
+    kernel pair.  dV, dK and D bit-identical; dQ bit-identical on the rows with one contributing key
+    tile (query tile 0, episodes of <= 64 steps) and within fp32 summation rounding elsewhere.  Lens
+    ragged: one full-length episode, the others random (some <= 64: single-key-tile rows past 64)."""
+    from xtrl_amd import _lib as L
+    g = torch.Generator().manual_seed(n + int(100 * p))
+    q, k, v, do = (torch.randn(b, H, n, 16, generator=g).to(DEV) for _ in range(4))
+    lens = torch.randint(1, n + 1, (b,), generator=g).to(torch.int32)
+    lens[0] = n
+    if b > 2:
+        lens[2] = 40
+    lens = lens.to(DEV)
+    two = _attn_bwd_lib(q, k, v, lens, do, 0.25, p, False)
+    lib = L.lib()
+    nf = int(lib.xtrl_attn_bwd_part_floats(b, H, n, 16))
+    assert nf == -(-n // 64) * b * H * n * 16
+    part = torch.full((nf,), float('nan'), device=DEV)
+    dq, dk, dv = (torch.full_like(q, float('nan')) for _ in range(3))
+    delta = torch.empty(b, H, n, device=DEV)
+    L.check(lib.xtrl_attn_bwd_part(L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(lens), L.ptr(two['o']), L.ptr(two['lse']),
+                                   L.ptr(do), L.ptr(dq), L.ptr(dk), L.ptr(dv), L.ptr(delta), L.ptr(part), nf, b, H, n,
+                                   16, 0.25, p, 3, 1, 0, L.stream()), 'attn_bwd_part')
+    torch.cuda.synchronize()
+    assert torch.equal(dv, two['dv']) and torch.equal(dk, two['dk']) and torch.equal(delta, two['delta'])
+    i = torch.arange(n, device=DEV)
+    sole = torch.minimum((i // 64)[None, :], ((lens.long() - 1) // 64)[:, None]) == 0     # [b][n]
+    sole = sole[:, None, :].expand(b, H, n)
+    assert torch.equal(dq[sole], two['dq'][sole])
+    assert torch.isfinite(dq).all()
+    scale = float(two['dq'].abs().max())
+    err = float((dq - two['dq']).abs().max())
+    assert err <= 2e-6 * scale, (err, scale)
+    assert int((~sole).sum()) > 0
+
+
 def test_attention_dropout_consistent():
     """Same seed -> same mask; the backward differentiates exactly the forward's dropped product."""
     from xtrl_amd import ops

@@ -91,6 +91,16 @@ def show(path):
             print(f'  {qkey} {q}:')
             for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:12]:
                 print(f'    {us / 1e3:8.2f} ms {n:6d} {us / n:8.1f} us  {k}')
+        # the main stream's kernels by launch shape (kernel, grid): which GEMM shape costs what
+        main_q = max(per_q, key=lambda k: per_q[k])
+        agg = defaultdict(lambda: [0, 0.0])
+        for i in seg:
+            if rows[i].get(qkey) == main_q:
+                grid = 'x'.join(rows[i].get(f'Grid_Size_{a_}', '?') for a_ in 'XYZ')
+                a = agg[(short(names[i]), grid)]; a[0] += 1; a[1] += dur[i]
+        print(f'  {qkey} {main_q} by launch shape:')
+        for (k, grid), (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:30]:
+            print(f'    {us / 1e3:8.2f} ms {n:6d} {us / n:8.1f} us  {k} [{grid}]')
         by_next = defaultdict(float)
         for g_us, i in gaps:
             by_next[short(names[i])] += g_us

@@ -44,6 +44,7 @@ __device__ __forceinline__ uint32_t qbyte(const u32x4_t& u, int word, int r) {
 struct AttnArgs {
   const float *Q, *K, *V, *O, *LSE, *dO, *Dl, *G;
   float *Oout, *LSEout, *dQ, *dK, *dV, *Dout, *OGout;
+  float* dQp;         // k_attn_bwd_dkdv<DH, true>: per-key-tile dQ partials [n_key_tiles][b H][n][DH]
   const int32_t* lens;
   int H, n;
   AttnLayout in, out, grad, gate;   // q/k/v; o/do/og; dq/dk/dv; gate
@@ -173,10 +174,18 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int DH>
-__global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const AttnArgs a) {
+// DQ (long episodes, n > FB_MAXN): the dQ kernel's pass is folded in as in k_attn_bwd_fused — per
+// (key tile, query tile) pair, once the four waves' dS images are in LDS, wave w multiplies its 16
+// query rows of dS by the key tile (staged once per workgroup) — but the key tiles stay spread over
+// the grid: a query row whose only contributing key tile is tile 0 (query tile 0, or an episode of
+// <= 64 steps: min(qt, (len - 1) / 64) = 0) gets dQ written here, bit-identical to k_attn_bwd_dq;
+// the other rows get one partial per contributing key tile in dQp, summed in ascending key-tile
+// order by k_attn_dq_reduce.  (141 registers, 3 waves per SIMD: held to 128 it spilled 12.)
+template <int DH, bool DQ = false>
+__global__ __launch_bounds__(256, DH == 16 ? (DQ ? 3 : 4) : 1) void k_attn_bwd_dkdv(const AttnArgs a) {
   constexpr int KS = DH / 4, ND = DH / 16, KST = DH + 2;
   __shared__ float Qs[TQ][KST], dOs[TQ][KST];
+  __shared__ float Ks[DQ ? TK : 1][KST];
   __shared__ float Ls[TQ], Dls[TQ];
   // one per-wave tile image, used for P~ (dV) and then for dS (dK): 26.6 KB of LDS per workgroup,
   // six resident per CU; at dh = 16 the register budget is held to 128 (4 waves per SIMD: 168 gave
@@ -206,6 +215,19 @@ __global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const A
   for (int d = 0; d < ND; ++d) {
     dk[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
     dv[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+  const int kmax = len > 0 ? (len - 1) / TK : 0;   // DQ: the last key tile holding a valid key
+  if constexpr (DQ) {
+    for (int x = tid; x < TK * DH; x += 256) {
+      const int j = x / DH, c = x - j * DH, jj = j0 + j;
+      Ks[j][c] = jj < n ? a.K[ib + (int64_t)jj * isi + c] : 0.f;
+    }
+    if (j0 == 0 && len <= 0) {   // no valid key: the rows' dQ is 0, this workgroup its only writer
+      for (int x = tid; x < n * DH; x += 256) {
+        const int i = x / DH, c = x - i * DH;
+        a.dQ[gb + (int64_t)i * gsi + c] = 0.f;
+      }
+    }
   }
   if (j0 < len) {
     for (int qt = j0 / TQ; qt * TQ < n; ++qt) {
@@ -294,7 +316,35 @@ __global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const A
       for (int d = 0; d < ND; ++d)
 #pragma unroll
         for (int s = 0; s < TQ / 4; ++s) dk[d] = mfma16(Ps[w][lr][4 * s + lg], Qs[4 * s + lg][16 * d + lr], dk[d]);
-      wave_sync();
+      if constexpr (DQ) {
+        __syncthreads();   // every wave's dS image of the pair is in LDS
+        // dQ rows 16 w .. 16 w + 15 of this query tile: dS[query][key] = image [key / 16][key % 16][query]
+        f32x4v dq[ND];
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          dq[d] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < TK / 4; ++s) {
+            const int j = 4 * s + lg;
+            dq[d] = mfma16(Ps[j >> 4][j & 15][16 * w + lr], Ks[j][16 * d + lr], dq[d]);
+          }
+        }
+        const bool sole = min(qt, kmax) == 0;   // (then this is key tile 0)
+        const int64_t pb = ((int64_t)blockIdx.x * gridDim.y + bh) * n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = qt * TQ + 16 * w + 4 * lg + r;
+          if (i < n) {
+#pragma unroll
+            for (int d = 0; d < ND; ++d) {
+              if (sole) a.dQ[gb + (int64_t)i * gsi + 16 * d + lr] = dq[d][r] * a.scale;
+              else a.dQp[(pb + i) * DH + 16 * d + lr] = dq[d][r];
+            }
+          }
+        }
+      } else {
+        wave_sync();
+      }
     }
   }
 #pragma unroll
@@ -308,6 +358,37 @@ __global__ __launch_bounds__(256, DH == 16 ? 4 : 1) void k_attn_bwd_dkdv(const A
       }
     }
   }
+}
+
+// dQ of the rows with more than one contributing key tile: the partials of key tiles
+// 0 .. min(qt, (len - 1) / 64) summed in ascending order (k_attn_bwd_dkdv<DH, true>); thread per
+// (row, 4 channels)
+template <int DH>
+__global__ __launch_bounds__(256) void k_attn_dq_reduce(const AttnArgs a, int BH) {
+  constexpr int C4 = DH / 4;
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n = a.n;
+  if (x >= (int64_t)BH * n * C4) return;
+  const int c4 = (int)(x % C4);
+  const int64_t row = x / C4;
+  const int bh = (int)(row / n), i = (int)(row - (int64_t)bh * n);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int len = a.lens[b];
+  const int m = min(i / TQ, len > 0 ? (len - 1) / TK : 0);
+  if (m == 0) return;   // written by key tile 0
+  float4 acc = *reinterpret_cast<const float4*>(a.dQp + ((int64_t)bh * n + i) * DH + 4 * c4);
+  for (int kt = 1; kt <= m; ++kt) {
+    const float4 p = *reinterpret_cast<const float4*>(a.dQp + (((int64_t)kt * BH + bh) * n + i) * DH + 4 * c4);
+    acc.x += p.x;
+    acc.y += p.y;
+    acc.z += p.z;
+    acc.w += p.w;
+  }
+  float* dst = a.dQ + b * a.grad.sb + h * a.grad.sh + (int64_t)i * a.grad.si + 4 * c4;
+  dst[0] = acc.x * a.scale;
+  dst[1] = acc.y * a.scale;
+  dst[2] = acc.z * a.scale;
+  dst[3] = acc.w * a.scale;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -636,8 +717,15 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
   a.dV = dv;
   // (D = rowsum(dO * O) is formed inside k_attn_bwd_dkdv, whose key-tile-0 workgroups store it for dq)
   dim3 grid((p.n + TQ - 1) / TQ, p.b * p.H);
+  const int64_t part_need = attn_dq_part_floats(p.b, p.H, p.n, p.dh);
   if (p.dh == 16 && p.n <= FB_MAXN && attn_fused_bwd_on()) {   // short episodes: one fused launch
     hipLaunchKernelGGL(k_attn_bwd_fused<16>, dim3(p.b * p.H), dim3(256), 0, s, a);
+  } else if (p.dh == 16 && p.dq_part && p.dq_part_floats >= part_need && attn_fused_bwd_on()) {
+    // long episodes: dK / dV with the dQ pass folded in (partials for multi-key-tile rows) + their sum
+    a.dQp = p.dq_part;
+    hipLaunchKernelGGL((k_attn_bwd_dkdv<16, true>), grid, dim3(256), 0, s, a);
+    const int64_t units = (int64_t)p.b * p.H * p.n * 4;
+    hipLaunchKernelGGL(k_attn_dq_reduce<16>, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, s, a, p.b * p.H);
   } else if (p.dh == 16) {
     hipLaunchKernelGGL(k_attn_bwd_dkdv<16>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_attn_bwd_dq<16>, grid, dim3(256), 0, s, a);
@@ -650,6 +738,10 @@ int attn_bwd_ex(const AttnProblem& p, const float* q, const float* k, const floa
   }
   XTRL_LAUNCHED("attn_bwd");
   return XTRL_OK;
+}
+
+int64_t attn_dq_part_floats(int b, int H, int n, int dh) {
+  return (int64_t)((n + TK - 1) / TK) * b * H * n * dh;
 }
 
 AttnProblem contiguous_problem(const int32_t* lens, int b, int H, int n, int dh, float scale, float p, uint64_t seed,
@@ -667,6 +759,20 @@ extern "C" int xtrl_attn_fwd(const float* q, const float* k, const float* v, con
                              uint32_t offset, uint32_t sub, void* stream) {
   return xtrl::attn_fwd_ex(xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset, sub), q, k, v, o,
                            lse, nullptr, nullptr, xtrl::as_stream(stream));
+}
+
+extern "C" int64_t xtrl_attn_bwd_part_floats(int b, int H, int n, int dh) {
+  return xtrl::attn_dq_part_floats(b, H, n, dh);
+}
+
+extern "C" int xtrl_attn_bwd_part(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,
+                                  const float* lse, const float* dout, float* dq, float* dk, float* dv, float* delta_ws,
+                                  float* dq_part, int64_t dq_part_floats, int b, int H, int n, int dh, float scale,
+                                  float dropout_p, uint64_t seed, uint32_t offset, uint32_t sub, void* stream) {
+  xtrl::AttnProblem pr = xtrl::contiguous_problem(lens, b, H, n, dh, scale, dropout_p, seed, offset, sub);
+  pr.dq_part = dq_part;
+  pr.dq_part_floats = dq_part_floats;
+  return xtrl::attn_bwd_ex(pr, q, k, v, o, lse, dout, dq, dk, dv, delta_ws, xtrl::as_stream(stream));
 }
 
 extern "C" int xtrl_attn_bwd(const float* q, const float* k, const float* v, const int32_t* lens, const float* o,

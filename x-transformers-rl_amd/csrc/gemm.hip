@@ -1041,7 +1041,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
   };
   auto put = [&](__bf16* img, int rows, int row, int k, float4 v) {
     bf16x4 h, m, l;
+#if defined(XTRL_WS_MODE) && XTRL_WS_MODE == 4   // tools/ws_lab.hip: the LDS writes without the split arithmetic
+    h = __builtin_bit_cast(bf16x4, make_uint2(__float_as_uint(v.x), __float_as_uint(v.y)));
+    m = __builtin_bit_cast(bf16x4, make_uint2(__float_as_uint(v.z), __float_as_uint(v.w)));
+    l = __builtin_bit_cast(bf16x4, make_uint2(__float_as_uint(v.x), __float_as_uint(v.w)));
+#else
     split3(v, h, m, l);
+#endif
     __bf16* q = img + row * XRS + k;
     *reinterpret_cast<bf16x4*>(q) = h;
     *reinterpret_cast<bf16x4*>(q + rows * XRS) = m;
@@ -1168,7 +1174,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ws(const GemmArgs a) {
     // hoist the next step's split arithmetic above the workgroup barrier)
     auto pstep = [&](auto C, int t) {
       WS_STAMP(t, 0);
-      if (mode < 2) convert(C, smem + ((t + 1) & 1) * IMG, t + 1 < nk);
+      if (mode < 2 || mode == 4) convert(C, smem + ((t + 1) & 1) * IMG, t + 1 < nk);
       else if (mode == 3) {   // consume the loads without splitting
         float s = 0.f;
 #pragma unroll

@@ -203,7 +203,12 @@ struct AttnProblem {
   AttnLayout gate;            // gate pre-activations (x-transformers attn_gate_values)
   int causal = 1;             // 0: bidirectional (key-padding mask only; forward only)
   uint32_t sub = 0;           // dropout stream sub-index (c3 low 24 bits): the decoder layer
+  // n > 128 (past the one-launch fused backward) at dh = 16: workspace for the per-key-tile dQ
+  // partials of the dK / dV kernel with the dQ pass folded in (attn_dq_part_floats); NULL: the pair
+  float* dq_part = nullptr;
+  int64_t dq_part_floats = 0;
 };
+int64_t attn_dq_part_floats(int b, int H, int n, int dh);
 
 // o (ungated) and lse; if gate != nullptr also og = o * sigmoid(gate) (og in the `out` layout)
 int attn_fwd_ex(const AttnProblem& p, const float* q, const float* k, const float* v, float* o, float* lse,

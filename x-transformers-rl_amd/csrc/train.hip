@@ -1136,6 +1136,8 @@ AttnProblem attn_problem(const Ctx& c, const XtrlTrainLayer& Ly, int li) {
   p.out = attn_layout_tokens(D->n, I, D->dh);
   p.grad = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
   p.gate = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
+  p.dq_part = D->dq_part;
+  p.dq_part_floats = D->dq_part_floats;
   return p;
 }
 
@@ -1768,6 +1770,8 @@ AttnProblem fractal_attn(const Ctx& c, int level) {
   p.out = attn_layout_tokens(D->n, I, D->dh);
   p.grad = attn_layout_tokens(D->n, 3 * I, D->dh);
   p.gate = p.grad;
+  p.dq_part = D->dq_part;
+  p.dq_part_floats = D->dq_part_floats;
   return p;
 }
 

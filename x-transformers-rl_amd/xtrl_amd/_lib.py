@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -105,7 +105,7 @@ class TrainDesc(C.Structure):
                    ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P),
                    ('qk_norm', I32), ('xpos_base', F32), ('rms_norm', I32),
                    ('Tv', I32), ('vrows', P), ('vinv', P), ('ewa_v', P), ('hp_v', P), ('zp_v', P), ('pred_v', P),
-                   ('d_pred_v', P), ('dzp_v', P), ('dewa_v', P)])
+                   ('d_pred_v', P), ('dzp_v', P), ('dewa_v', P), ('dq_part', P), ('dq_part_floats', I64)])
 
 
 class FractalTrainLevel(C.Structure):
@@ -161,6 +161,9 @@ SIGNATURES = {
     'xtrl_hlgauss_gae': (I32, [P, I64, P, P, I64, P, P, P, I32, I32, I32, F32, F32, P, P, P]),
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
+    'xtrl_attn_bwd_part_floats': (I64, [I32, I32, I32, I32]),
+    'xtrl_attn_bwd_part': (I32, [P, P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, F32, F32, U64, U32, U32,
+                                  P]),
     'xtrl_loss_fwd': (I32, [C.POINTER(LossDesc), P]),
     'xtrl_loss_bwd': (I32, [C.POINTER(LossDesc), F32, P]),
     'xtrl_grad_norm': (I32, [P, I64, P, F32, P, P]),

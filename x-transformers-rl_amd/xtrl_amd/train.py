@@ -32,7 +32,7 @@ def _span_off(flat, names):
     return flat.index[names[0]][0]
 
 
-def _compact_bufs(D, c, T, dev):
+def _compact_bufs(D, c, T, dev, b_max, n_max):
     """The world-model heads' valid-row buffers (XtrlTrainDesc.Tv): row list / inverse and the compact
     operands, T rows each (the most a minibatch can have valid)."""
     d, ldp, S1x2 = c.dim, c.dim + 4, 2 * (c.state_dim + 1)
@@ -44,6 +44,12 @@ def _compact_bufs(D, c, T, dev):
     for k, t in bufs.items():
         setattr(D, k, t.data_ptr())
     D.Tv = 0
+    # long episodes (n > 128, dh 16): the attention backward's per-key-tile dQ partials (xtrl_attn_bwd_part)
+    D.dq_part, D.dq_part_floats = None, 0
+    if n_max > 128 and c.dim_head == 16:
+        nf = int(L.lib().xtrl_attn_bwd_part_floats(b_max, c.heads, n_max, c.dim_head))
+        bufs['dq_part'] = torch.empty(nf, **f32)
+        D.dq_part, D.dq_part_floats = bufs['dq_part'].data_ptr(), nf
     return bufs
 
 
@@ -165,7 +171,7 @@ class FusedTrainStep:
         D.ld_ff = lff
         D.scratch_per_layer = 1   # per-layer backward planes (no mid-backward stream waits)
         D.ff_glu, D.ld_u2 = int(glu), (lu2 if glu else 0)
-        self.cbuf = _compact_bufs(D, c, T, dev)
+        self.cbuf = _compact_bufs(D, c, T, dev, b_max, n_max)
         self.D = D
 
     # ------------------------------------------------------------------------------------------
@@ -337,7 +343,7 @@ class FractalTrainStep(FusedTrainStep):
         D.ws, D.ws_floats = ws.data_ptr(), ws.numel()
         D.layers = None
         D.ld_ff = lff
-        self.cbuf = _compact_bufs(D, c, T, dev)
+        self.cbuf = _compact_bufs(D, c, T, dev, b_max, n_max)
         self.D = D
         Fd = L.FractalTrainDesc()
         Fd.levels = Lv
