@@ -58,6 +58,14 @@ CONFIGS = {
                             'dropout 0.25',
                    S=8, A=4, episodes=384, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=True,
                    batch=128, hazard_log2=6, dropout=0.25, mode='lander'),
+    # C3 with the per-token critic reduction (hl_reduction_mean=False, decision log) and the packed learn
+    # step: the minibatch's valid tokens only (no padding computed; exact for this reduction)
+    'c3_tok': dict(workload='C3 with the per-token HL-Gauss critic reduction (hl_reduction_mean=False) and the packed '
+                            'learn step (valid tokens only, XtrlTrainDesc.packed): LunarLander-shaped VecSim, 1024 '
+                            'episodes x 128 steps per update per GPU, depth-4 d=256 4x16-head gated value-residual '
+                            'world-model policy, batch 128 episodes, 4 epochs, dropout 0.25, no EPO',
+                   S=8, A=4, episodes=1024, T=128, depth=4, dim=256, heads=4, dim_head=16, gates=True, evo=False,
+                   batch=128, hazard_log2=6, dropout=0.25, mode='lander', tok=True),
     # configs[1] — train_lander defaults (evolutionary, 3 genes), 256 episodes, depth-2 d=128
     'c2': dict(workload='C2: LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 steps, depth-2 d=128 EPO',
                S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,
@@ -146,6 +154,8 @@ def build_learner(cfg, seed, use_graph=True, world=1):
     extra = dict(policy_body='fractal', fractal_levels=cfg['fractal']) if cfg.get('fractal') else {}
     if cfg.get('host') and not cfg.get('vector'):   # train_lander.py:42-49
         extra.update(actor_loss_weight=0.5)
+    if cfg.get('tok'):
+        extra.update(hl_reduction_mean=False, packed_learn=True)
     learner = Learner(state_dim=cfg['S'], num_actions=cfg['A'], reward_range=(-5., 5.), world_model=wm,
                       max_timesteps=cfg['T'], batch_size=cfg['batch'],
                       num_episodes_per_update=cfg['episodes'] * world,   # weak scaling: episodes per GPU fixed
@@ -446,9 +456,11 @@ def ppo_loss_delta(learner, env, cfg, check=True):
     runs the update (its learn all-reduces gradients); ``check`` (rank 0) compares its local first
     minibatch, the others return None."""
     from oracle import ref_port as R
+    from oracle import thirdparty as tp
     agent = learner.agent
     c = agent.cfg
     out = {}
+    tp.HLGaussLoss.default_reduction = 'mean' if c.hl_reduction_mean else 'none'   # the agent's reduction
     saved_p = c.dropout
     c.dropout = 0.          # dropout masks are not shared with the CPU side
     u = agent.step

@@ -566,6 +566,18 @@ typedef struct XtrlTrainDesc {
    * (xtrl_attn_bwd_part_floats(b, H, n, dh) floats), or NULL for the dK / dV + dQ kernel pair */
   float* dq_part;
   int64_t dq_part_floats;
+  /* packed learn step (per-token critic reduction only, Agent(packed_learn=True); xtrl.py:936-978 with
+   * hl_reduction_mean=False): the minibatch's Tv = sum(min(lens, n)) valid tokens are computed in
+   * episode-then-step order without the padding — the inputs (swr, actions; the minibatch's [b][n]
+   * layout as usual) are gathered into pack_ws, every row-wise kernel runs on Tv rows, the attention
+   * on per-episode row ranges (ep_off [b + 1], written by the forward), rotary positions from the
+   * row list (vrows), the FF dropout keyed by the packed row; raw / values / pred / done are
+   * scattered back to [b][n] (zeros on the padding) for xtrl_loss_*, whose gradients the backward
+   * gathers again.  pack_ws_floats >= xtrl_train_pack_floats(b * n, S, A, n_out, B). */
+  int packed;
+  int32_t* ep_off;
+  float* pack_ws;
+  int64_t pack_ws_floats;
 } XtrlTrainDesc;
 
 int xtrl_train_forward(const XtrlTrainDesc* desc, void* stream);
@@ -650,6 +662,8 @@ int xtrl_glu_drop_bwd(const float* dh, int lddh, const float* u, int ldu, float*
 /* floats of XtrlTrainDesc.part (the partial-sum workspace) a learn step of T = b * n tokens needs;
  * host-only, no device call */
 int64_t xtrl_train_part_floats(int T, int b, int d, int A);
+/* floats of XtrlTrainDesc.pack_ws for up to T packed tokens */
+int64_t xtrl_train_pack_floats(int T, int S, int A, int n_out, int B);
 
 /* ---------------------------------------------------------------------------------------------
  * Minibatch assembly for the learn step (Agent.learn data prep, xtrl.py:816-924): gathers the

@@ -412,16 +412,26 @@ class PhiloxFFDropout(nn.Module):
     def __init__(self, layer, p=0., seed=0, offset=0):
         super().__init__()
         self.layer, self.p, self.seed, self.offset = layer, p, seed, offset
+        self.packed_lens = None
 
     def forward(self, h):
         if not self.training or self.p <= 0.:
             return h
         b, n, f = h.shape
-        keep = torch.from_numpy(ff_dropout_keep(b * n, f, self.p, self.seed, self.offset, self.layer))
+        if self.packed_lens is None:
+            keep = torch.from_numpy(ff_dropout_keep(b * n, f, self.p, self.seed, self.offset, self.layer))
+        else:   # the packed learn step (XtrlTrainDesc.packed): rows numbered over the valid tokens only,
+            # episode after episode; the padded tokens' mask is irrelevant (no loss term reaches them)
+            ln = np.minimum(np.asarray(self.packed_lens, dtype=np.int64), n)
+            kp = ff_dropout_keep(int(ln.sum()), f, self.p, self.seed, self.offset, self.layer)
+            keep = np.ones((b * n, f), dtype=kp.dtype)
+            rows = np.concatenate([e * n + np.arange(ln[e]) for e in range(b)]) if b else np.zeros(0, np.int64)
+            keep[rows] = kp
+            keep = torch.from_numpy(keep)
         return h * keep.reshape(b, n, f).to(h.dtype) / (1. - self.p)
 
 
-def install_philox_dropout(model, p, seed, attn_offset, ff_offset):
+def install_philox_dropout(model, p, seed, attn_offset, ff_offset, packed_lens=None):
     """Point every attention / feed-forward dropout of an OracleWMAC decoder at the learn step's
     counter-based streams for one minibatch (seed = agent seed * 1000003 + update, attention counters
     from ``attn_offset``, FF counter ``ff_offset``; the layer index in the Philox sub-index, as
@@ -435,6 +445,7 @@ def install_philox_dropout(model, p, seed, attn_offset, ff_offset):
         for m, off in ((attn.attn_dropout, attn_offset), (ff.ff[1], ff_offset)):
             m.p, m.seed, m.offset = float(p), int(seed), int(off)
             m.train(model.training)
+        ff.ff[1].packed_lens = None if packed_lens is None else [int(x) for x in packed_lens]
 
 
 # --------------------------------------------------------------------------------------------

@@ -1346,7 +1346,7 @@ def _config_parity(depth, dim, T, hazard, evo, episodes, batch, gene_dim=8, max_
     return seen, lens
 
 
-def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, dropout=0.):
+def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, dropout=0., packed=False):
     """The first ``max_minibatches`` minibatches of Agent.learn against the oracle on the GPU's
     current weights, RSNorm, genes and minibatch (rebuilt from the device trajectory as
     xtrl.py:822-852 does): loss within 1e-4 relative, every gradient within 1e-4 of the gradient
@@ -1375,7 +1375,8 @@ def _learn_parity(learner, oracle, traj, lens, genes, fit, max_minibatches, drop
         ordinal = epoch * n_mb_epoch + mbi        # Agent.learn's dropout counters for this minibatch
         if dropout > 0.:     # (the decoder's dropout streams; the fractal oracle body runs dropout-free)
             R.install_philox_dropout(oracle.model, dropout, agent.seed * 1000003 + 0,
-                                     ordinal * agent.batch_size * agent.cfg.heads, ordinal)
+                                     ordinal * agent.batch_size * agent.cfg.heads, ordinal,
+                                     packed_lens=elens[idx].tolist() if packed else None)
         mb = R.Minibatch(states[idx], actions[idx], rewards[idx], old_lp[idx], returns[idx], values[idx], bounds[idx],
                          egenes[idx], elens[idx])
         latent = R.l2norm(agent.gene_pool.genes[mb.gene_ids]) if evo else None
@@ -1502,13 +1503,94 @@ def test_c3_shape_rollout_and_learn_match_oracle():
 # ---- the bench's own geometry (bench.py CONFIGS): the kernels and grids the timed run uses ------------
 
 
-def _bench_learner(cfg):
+def _bench_learner(cfg, agent_extra=None):
     """make_learner at a bench.py configuration (model, episodes per update, minibatch, T, hazard)."""
     from bench import CONFIGS
     c = CONFIGS[cfg]
     return make_learner(depth=c['depth'], gates=c['gates'], evo=c['evo'], T=c['T'], episodes=c['episodes'],
                         batch=c['batch'], seed=4, hazard=c['hazard_log2'], dim=c['dim'], gene_dim=32,
-                        genes=c.get('genes', 3), fractal_levels=c.get('fractal'))
+                        genes=c.get('genes', 3), fractal_levels=c.get('fractal'), agent_extra=agent_extra)
+
+
+@contextlib.contextmanager
+def _hl_reduction(mean):
+    """The oracle's HL-Gauss reduction (thirdparty.HLGaussLoss.default_reduction) for one test."""
+    prev = tp.HLGaussLoss.default_reduction
+    tp.HLGaussLoss.default_reduction = 'mean' if mean else 'none'
+    try:
+        yield
+    finally:
+        tp.HLGaussLoss.default_reduction = prev
+
+
+def _first_minibatch_state(agent, traj, lens, genes, fit):
+    """Loss, flat gradient and the per-token outputs of the first minibatch of agent.learn."""
+    out = {}
+
+    def probe(epoch, mbi, idx, loss, stats):
+        ts = agent._train_step
+        b, n = ts.D.b, ts.D.n
+        out.update(loss=float(loss.detach()), grad=agent.flat.grad.detach().clone(), n=n, idx=idx.cpu(),
+                   raw=ts.buf['raw'][:b * n].view(b, n, -1).clone(), values=ts.buf['values'][:b * n].view(b, n, -1).clone())
+        raise _Captured()
+
+    with pytest.raises(_Captured):
+        agent.learn(traj, lens, genes, fit, update=0, probe=probe)
+    agent.step = 0
+    return out
+
+
+@pytest.mark.parametrize('evo,gates,T,dim', [(True, True, 40, 64), (False, True, 150, 48), (True, False, 130, 64)])
+def test_packed_learn_matches_padded_step(evo, gates, T, dim):
+    """The packed learn step (Agent(packed_learn=True): only the minibatch's valid tokens, episode after
+    episode — packed inputs, per-episode attention row ranges, rotary positions from the row list, the
+    latent broadcast and gradient per episode range) against the padded fused step on the same
+    weights and minibatch, both with the per-token critic reduction and dropout 0: the loss, the
+    actor / critic outputs on the valid tokens (zeros on the padding for the packed step) and every
+    gradient tensor within 1e-4 of its own scale.  T 150: key tiles past 128 (the long-episode
+    attention backward with per-episode rows)."""
+    res = {}
+    for packed in (False, True):
+        learner, env, _ = make_learner(depth=2, gates=gates, evo=evo, T=T, episodes=8, batch=8, seed=5, hazard=5,
+                                       dim=dim, agent_extra=dict(hl_reduction_mean=False, packed_learn=packed))
+        agent = learner.agent
+        traj, lens, genes, cum = learner.rollout_device(env, 0, T)
+        res[packed] = _first_minibatch_state(agent, traj, lens, genes, learner.fitness(cum, genes))
+        res[packed]['lens'] = lens.cpu()
+    a, b = res[True], res[False]
+    assert torch.equal(a['lens'], b['lens']) and torch.equal(a['idx'], b['idx'])
+    lens_mb = a['lens'][a['idx']].clamp(max=a['n'])
+    assert lens_mb.min() < a['n']    # padding present
+    valid = (torch.arange(a['n'])[None, :] < lens_mb[:, None]).to(a['raw'].device)
+    assert (a['raw'][~valid] == 0).all() and (a['values'][~valid] == 0).all()
+    for k in ('raw', 'values'):
+        x, y = a[k][valid], b[k][valid]
+        assert float((x - y).abs().max()) <= 1e-4 * float(y.abs().max()) + 1e-6, k
+    assert abs(a['loss'] - b['loss']) <= 1e-5 * abs(b['loss']) + 1e-7, (a['loss'], b['loss'])
+    bad = []
+    for name, (o0, o1) in learner.agent.flat.index.items():
+        g0, g1 = a['grad'][o0:o1], b['grad'][o0:o1]
+        own = float(g1.abs().max())
+        if float((g0 - g1).abs().max()) > 1e-4 * own + 1e-7:
+            bad.append((name, float((g0 - g1).abs().max()), own))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize('cfg', ['c3', 'c2'])
+def test_packed_learn_bench_minibatch_matches_oracle(cfg):
+    """The packed learn step at the bench geometry (C3: 128 episodes x 128 steps per minibatch, depth 4,
+    d 256; C2: 32 x ~430, 3-gene EPO, long-episode attention backward) with the per-token critic reduction
+    and dropout 0.25, against the oracle on the padded minibatch: the attention keep masks are the padded
+    step's (keyed by episode and position), the FF masks are numbered over the packed rows (the oracle's
+    PhiloxFFDropout(packed_lens)); loss at 1e-4 relative, every gradient at 1e-4 of its scale, two
+    minibatches."""
+    learner, env, oracle = _bench_learner(cfg, agent_extra=dict(hl_reduction_mean=False, packed_learn=True))
+    T = 128 if cfg == 'c3' else 500
+    traj, lens, genes, cum = learner.rollout_device(env, 0, T)
+    with _hl_reduction(False):
+        seen = _learn_parity(learner, oracle, traj, lens, genes, learner.fitness(cum, genes), 2, dropout=0.25,
+                             packed=True)
+    assert len(seen) == 2
 
 
 def _full_width_rollout(cfg):

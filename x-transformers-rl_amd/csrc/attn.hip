@@ -45,6 +45,7 @@ struct AttnArgs {
   const float *Q, *K, *V, *O, *LSE, *dO, *Dl, *G;
   float *Oout, *LSEout, *dQ, *dK, *dV, *Dout, *OGout;
   float* dQp;         // k_attn_bwd_dkdv<DH, true>: per-key-tile dQ partials [n_key_tiles][b H][n][DH]
+  const int32_t* ep_off;   // packed rows: episode b's tokens are rows ep_off[b] .. + min(lens[b], n) - 1
   const int32_t* lens;
   int H, n;
   AttnLayout in, out, grad, gate;   // q/k/v; o/do/og; dq/dk/dv; gate
@@ -57,6 +58,11 @@ struct AttnArgs {
   int causal;
 };
 
+// first row of episode b in layout L: b * sb (padded [b][n] tokens), or ep_off[b] rows (packed)
+__device__ __forceinline__ int64_t ebase(const AttnArgs& a, const AttnLayout& L, int b) {
+  return a.ep_off ? (int64_t)a.ep_off[b] * L.si : (int64_t)b * L.sb;
+}
+
 // ---------------------------------------------------------------------------------------------
 template <int DH>
 __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
@@ -64,11 +70,13 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
   __shared__ float Ks[TK][KST], Vs[TK][KST];
   __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int bh = blockIdx.y, b = bh / a.H, ns = a.n;
   const int q0 = blockIdx.x * TQ;
   const int len = a.lens[b];
+  const int n = a.ep_off ? min(len, ns) : ns;   // packed rows: the episode's own length
   const int h = bh - b * a.H;
-  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh;
+  if (q0 >= n) return;   // (packed rows: a query tile past the episode; workgroup-uniform)
+  const int64_t ib = ebase(a, a.in, b) + h * a.in.sh, ob = ebase(a, a.out, b) + h * a.out.sh;
   const int isi = a.in.si, osi = a.out.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
@@ -166,9 +174,9 @@ __global__ __launch_bounds__(256) void k_attn_fwd(const AttnArgs a) {
         const float ov = o[d][r] / l[r];
         a.Oout[at] = ov;
         if (a.OGout)   // gated values (x-transformers attn_gate_values)
-          a.OGout[at] = ov * sigmoidf_(a.G[b * a.gate.sb + h * a.gate.sh + (int64_t)i * a.gate.si + 16 * d + lr]);
+          a.OGout[at] = ov * sigmoidf_(a.G[ebase(a, a.gate, b) + h * a.gate.sh + (int64_t)i * a.gate.si + 16 * d + lr]);
       }
-      if (lr == 0) a.LSEout[(int64_t)bh * n + i] = m[r] + logf(l[r]);
+      if (lr == 0) a.LSEout[(int64_t)bh * ns + i] = m[r] + logf(l[r]);
     }
   }
 }
@@ -192,11 +200,12 @@ __global__ __launch_bounds__(256, DH == 16 ? (DQ ? 3 : 4) : 1) void k_attn_bwd_d
   // 3, and a quarter of the C3 grid ran as a second round), so the C3 grid is one round
   __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int bh = blockIdx.y, b = bh / a.H, ns = a.n;
   const int j0 = blockIdx.x * TK;
   const int len = a.lens[b];
+  const int n = a.ep_off ? min(len, ns) : ns;   // packed rows: the episode's own length
   const int h = bh - b * a.H;
-  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  const int64_t ib = ebase(a, a.in, b) + h * a.in.sh, ob = ebase(a, a.out, b) + h * a.out.sh, gb = ebase(a, a.grad, b) + h * a.grad.sh;
   const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
@@ -243,7 +252,7 @@ __global__ __launch_bounds__(256, DH == 16 ? (DQ ? 3 : 4) : 1) void k_attn_bwd_d
       float orow[DH];
       if (tid < TQ) {
         const int ii = qt * TQ + tid;
-        Ls[tid] = ii < n ? a.LSE[(int64_t)bh * n + ii] : 0.f;
+        Ls[tid] = ii < n ? a.LSE[(int64_t)bh * ns + ii] : 0.f;
 #pragma unroll
         for (int c = 0; c < DH; ++c) orow[c] = ii < n ? a.O[ob + (int64_t)ii * osi + c] : 0.f;
       }
@@ -254,7 +263,7 @@ __global__ __launch_bounds__(256, DH == 16 ? (DQ ? 3 : 4) : 1) void k_attn_bwd_d
 #pragma unroll
         for (int c = 0; c < DH; ++c) dsum += dOs[tid][c] * orow[c];
         Dls[tid] = dsum;
-        if (j0 == 0 && ii < n) a.Dout[(int64_t)bh * n + ii] = dsum;
+        if (j0 == 0 && ii < n) a.Dout[(int64_t)bh * ns + ii] = dsum;
       }
       __syncthreads();
       float dsr[4][4];
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(256, DH == 16 ? (DQ ? 3 : 4) : 1) void k_attn_bwd_d
           }
         }
         const bool sole = min(qt, kmax) == 0;   // (then this is key tile 0)
-        const int64_t pb = ((int64_t)blockIdx.x * gridDim.y + bh) * n;
+        const int64_t pb = ((int64_t)blockIdx.x * gridDim.y + bh) * ns;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = qt * TQ + 16 * w + 4 * lg + r;
@@ -367,24 +376,25 @@ template <int DH>
 __global__ __launch_bounds__(256) void k_attn_dq_reduce(const AttnArgs a, int BH) {
   constexpr int C4 = DH / 4;
   const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int n = a.n;
-  if (x >= (int64_t)BH * n * C4) return;
+  const int ns = a.n;
+  if (x >= (int64_t)BH * ns * C4) return;
   const int c4 = (int)(x % C4);
   const int64_t row = x / C4;
-  const int bh = (int)(row / n), i = (int)(row - (int64_t)bh * n);
+  const int bh = (int)(row / ns), i = (int)(row - (int64_t)bh * ns);
   const int b = bh / a.H, h = bh - b * a.H;
   const int len = a.lens[b];
+  if (a.ep_off && i >= min(len, ns)) return;   // packed rows: past the episode's own length
   const int m = min(i / TQ, len > 0 ? (len - 1) / TK : 0);
   if (m == 0) return;   // written by key tile 0
-  float4 acc = *reinterpret_cast<const float4*>(a.dQp + ((int64_t)bh * n + i) * DH + 4 * c4);
+  float4 acc = *reinterpret_cast<const float4*>(a.dQp + ((int64_t)bh * ns + i) * DH + 4 * c4);
   for (int kt = 1; kt <= m; ++kt) {
-    const float4 p = *reinterpret_cast<const float4*>(a.dQp + (((int64_t)kt * BH + bh) * n + i) * DH + 4 * c4);
+    const float4 p = *reinterpret_cast<const float4*>(a.dQp + (((int64_t)kt * BH + bh) * ns + i) * DH + 4 * c4);
     acc.x += p.x;
     acc.y += p.y;
     acc.z += p.z;
     acc.w += p.w;
   }
-  float* dst = a.dQ + b * a.grad.sb + h * a.grad.sh + (int64_t)i * a.grad.si + 4 * c4;
+  float* dst = a.dQ + ebase(a, a.grad, b) + h * a.grad.sh + (int64_t)i * a.grad.si + 4 * c4;
   dst[0] = acc.x * a.scale;
   dst[1] = acc.y * a.scale;
   dst[2] = acc.z * a.scale;
@@ -398,11 +408,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
   __shared__ float Ks[TK][KST], Vs[TK][KST];
   __shared__ float Ds[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int bh = blockIdx.y, b = bh / a.H, n = a.n;
+  const int bh = blockIdx.y, b = bh / a.H, ns = a.n;
   const int q0 = blockIdx.x * TQ;
   const int len = a.lens[b];
+  const int n = a.ep_off ? min(len, ns) : ns;   // packed rows: the episode's own length
   const int h = bh - b * a.H;
-  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  if (q0 >= n) return;   // (packed rows: a query tile past the episode; workgroup-uniform)
+  const int64_t ib = ebase(a, a.in, b) + h * a.in.sh, ob = ebase(a, a.out, b) + h * a.out.sh, gb = ebase(a, a.grad, b) + h * a.grad.sh;
   const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
@@ -420,8 +432,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(const AttnArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = q0 + 16 * w + 4 * lg + r;
-    lse[r] = i < n ? a.LSE[(int64_t)bh * n + i] : 0.f;
-    dl[r] = i < n ? a.Dl[(int64_t)bh * n + i] : 0.f;
+    lse[r] = i < n ? a.LSE[(int64_t)bh * ns + i] : 0.f;
+    dl[r] = i < n ? a.Dl[(int64_t)bh * ns + i] : 0.f;
   }
   f32x4v dq[ND];
 #pragma unroll
@@ -497,10 +509,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
   __shared__ float Ls[TQ], Dls[TQ];
   __shared__ float Ps[4][16][PST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int bh = blockIdx.x, b = bh / a.H, n = a.n;
+  const int bh = blockIdx.x, b = bh / a.H, ns = a.n;
   const int len = a.lens[b];
+  const int n = a.ep_off ? min(len, ns) : ns;   // packed rows: the episode's own length
   const int h = bh - b * a.H;
-  const int64_t ib = b * a.in.sb + h * a.in.sh, ob = b * a.out.sb + h * a.out.sh, gb = b * a.grad.sb + h * a.grad.sh;
+  const int64_t ib = ebase(a, a.in, b) + h * a.in.sh, ob = ebase(a, a.out, b) + h * a.out.sh, gb = ebase(a, a.grad, b) + h * a.grad.sh;
   const int isi = a.in.si, osi = a.out.si, gsi = a.grad.si;
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t off = a.offset + (uint32_t)bh;
@@ -543,7 +556,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
         float orow[DH];
         if (tid < TQ) {
           const int ii = qt * TQ + tid;
-          Ls[tid] = ii < n ? a.LSE[(int64_t)bh * n + ii] : 0.f;
+          Ls[tid] = ii < n ? a.LSE[(int64_t)bh * ns + ii] : 0.f;
 #pragma unroll
           for (int c = 0; c < DH; ++c) orow[c] = ii < n ? a.O[ob + (int64_t)ii * osi + c] : 0.f;
         }
@@ -554,7 +567,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_fused(const AttnArgs a) {
           for (int c = 0; c < DH; ++c) dsum += dOs[tid][c] * orow[c];
           Dls[tid] = dsum;
           const int ii = qt * TQ + tid;
-          if (kt == 0 && ii < n) a.Dout[(int64_t)bh * n + ii] = dsum;   // as k_attn_bwd_dkdv's key tile 0
+          if (kt == 0 && ii < n) a.Dout[(int64_t)bh * ns + ii] = dsum;   // as k_attn_bwd_dkdv's key tile 0
         }
         __syncthreads();
         float dsr[4][4];
@@ -671,6 +684,7 @@ int fill_args(AttnArgs& a, const AttnProblem& p) {
   XTRL_REQUIRE(p.sub < (1u << 23), "attn: dropout stream sub-index %u does not fit 23 bits", p.sub);
   a.c3 = rng_c3(FIELD_DROPOUT, a.thresh8 ? (p.sub | (1u << 23)) : p.sub);
   a.causal = p.causal;
+  a.ep_off = p.ep_off;
   return XTRL_OK;
 }
 

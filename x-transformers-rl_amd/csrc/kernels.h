@@ -207,6 +207,9 @@ struct AttnProblem {
   // partials of the dK / dV kernel with the dQ pass folded in (attn_dq_part_floats); NULL: the pair
   float* dq_part = nullptr;
   int64_t dq_part_floats = 0;
+  // packed rows (the learn step without padding, XtrlTrainDesc.packed): episode b's min(lens[b], n)
+  // tokens are rows ep_off[b] .. of the token-major layouts (their sb unused); NULL: rows b * n + i
+  const int32_t* ep_off = nullptr;
 };
 int64_t attn_dq_part_floats(int b, int H, int n, int dh);
 

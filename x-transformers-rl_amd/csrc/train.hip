@@ -33,6 +33,7 @@ struct EmbedArgs {
   const float* ln_g;   // (k_embed_ln) layer 0's attention pre-norm: gamma, output rows, (mean, rstd)
   float *xn, *st;
   int rms;             // the pre-norm is x-transformers' RMSNorm (use_rmsnorm)
+  const int32_t* rows; // packed rows: token t is the minibatch's row rows[t] = episode * n + step (latent)
 };
 
 constexpr int EMB_TOK = 32, EMB_U = 8, EMB_MAXS = 32;
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void k_embed(const EmbedArgs a) {
           ap[u] = p >= 0 ? a.act_emb[(int64_t)p * a.d + c] : 0.f;
           an[u] = q >= 0 ? a.act_emb[(int64_t)q * a.d + c] : 0.f;
         }
-        le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + c] : 0.f;
+        le[u] = a.evolutionary ? a.lat_e[(int64_t)((a.rows ? a.rows[t] : t) / a.n) * a.d + c] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < EMB_U; ++u) {
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const EmbedArgs a) {
       }
       x[u] = on ? sp + (ap + (st[S] * re) * a.keep) : 0.f;
       se[u] = ss + bse;
-      le[u] = a.evolutionary ? a.lat_e[(int64_t)(t / a.n) * a.d + cc] : 0.f;
+      le[u] = a.evolutionary ? a.lat_e[(int64_t)((a.rows ? a.rows[t] : t) / a.n) * a.d + cc] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < EMB_U; ++u) {
@@ -356,6 +357,7 @@ struct PrepArgs {
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col;   // mix_col < 0: no mix
   int qk_norm;          // x-transformers qk norm: q, k l2-normalised per head before the rotary
   float xpos_base;      // rotary xPos scale base (0: off)
+  const int32_t* rows;  // packed rows (grid (pair blocks, T)): token t's position is rows[t] % n
 };
 
 // x-transformers RotaryEmbedding(use_xpos): rotated pair j (even channel) at position pos of an n-token
@@ -381,7 +383,8 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep(const PrepArgs a) {
   const int P = 3 * a.I / 2;
   const int pair = blockIdx.x * PREP_T + threadIdx.x;
   if (pair >= P) return;
-  const int pos = blockIdx.y, t = blockIdx.z * a.n + pos, col = 2 * pair;
+  const int t = a.rows ? (int)blockIdx.y : blockIdx.z * a.n + blockIdx.y;
+  const int pos = a.rows ? a.rows[t] % a.n : (int)blockIdx.y, col = 2 * pair;
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
   float2 x = *reinterpret_cast<const float2*>(a.proj + (int64_t)t * a.n_qkv + col);
   float2 y;
@@ -430,6 +433,7 @@ struct PrepBwdArgs {
   int T, n, H, dh, I, n_qkv, ld_vfirst, rot_dim, mix_col, first_layer, accumulate;
   int qk_norm;
   float xpos_base;
+  const int32_t* rows;  // packed rows, as PrepArgs
 };
 
 __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
@@ -437,7 +441,8 @@ __global__ __launch_bounds__(PREP_T) void k_qkv_prep_bwd(const PrepBwdArgs a) {
   const int pair0 = blockIdx.x * PREP_T + threadIdx.x;
   const bool valid = pair0 < P;
   const int pair = valid ? pair0 : 0;
-  const int pos = blockIdx.y, t = blockIdx.z * a.n + pos, col = 2 * pair;
+  const int t = a.rows ? (int)blockIdx.y : blockIdx.z * a.n + blockIdx.y;
+  const int pos = a.rows ? a.rows[t] % a.n : (int)blockIdx.y, col = 2 * pair;
   const int seg = col / a.I, within = col - seg * a.I, h = within / a.dh, j = within - h * a.dh;
   float* g = a.dproj + (int64_t)t * a.n_qkv + col;
   float dm = 0.f, m = 0.f;
@@ -657,15 +662,18 @@ __global__ __launch_bounds__(256) void k_embed_grad_part(const float* g1, int ld
 // in order (8 loads in flight per thread), then the group partials are added in group order (a
 // thread per column summing all n steps in turn took 107 us a launch at C2's n = 500)
 constexpr int LG_G = 16;
+// ep_off (packed rows): episode e's rows are ep_off[e] .. ep_off[e + 1] - 1
 __global__ __launch_bounds__(64 * LG_G) void k_latent_grad(const float* dac, int ld, int off, int b, int n, int d,
-                                                           float* dlat) {
+                                                           float* dlat, const int32_t* ep_off) {
   __shared__ float red[LG_G][64];
   const int e = blockIdx.x, cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + cl;
-  const int per = (n + LG_G - 1) / LG_G, t0 = grp * per, t1 = min(n, t0 + per);
+  const int64_t r0 = ep_off ? (int64_t)ep_off[e] : (int64_t)e * n;
+  const int ne = ep_off ? ep_off[e + 1] - ep_off[e] : n;
+  const int per = (ne + LG_G - 1) / LG_G, t0 = grp * per, t1 = min(ne, t0 + per);
   float s = 0.f;
   if (c < d) {
-    const float* col = dac + (int64_t)e * n * ld + off + c;
+    const float* col = dac + r0 * ld + off + c;
     int t = t0;
     for (; t + 8 <= t1; t += 8) {
       float v[8];
@@ -1136,6 +1144,7 @@ AttnProblem attn_problem(const Ctx& c, const XtrlTrainLayer& Ly, int li) {
   p.out = attn_layout_tokens(D->n, I, D->dh);
   p.grad = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
   p.gate = attn_layout_tokens(D->n, Ly.n_qkv, D->dh);
+  p.ep_off = D->packed ? D->ep_off : nullptr;
   p.dq_part = D->dq_part;
   p.dq_part_floats = D->dq_part_floats;
   return p;
@@ -1169,7 +1178,7 @@ constexpr int VR_MAXB = 4096;
 // never written and their rows scatter as padding, and list slots past the device count read row 0,
 // so a wrong Tv gives wrong heads outputs but no out-of-range or stale access.
 __global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b, int n, int Tv, int32_t* vrows,
-                                                     int32_t* vinv) {
+                                                     int32_t* vinv, int32_t* ep_off = nullptr) {
   __shared__ int off[VR_MAXB + 1];
   for (int e = threadIdx.x; e < b; e += 1024) off[e + 1] = min(max(lens[e], 0), n);
   __syncthreads();
@@ -1189,6 +1198,8 @@ __global__ __launch_bounds__(1024) void k_valid_rows(const int32_t* lens, int b,
     }
   }
   for (int j = off[b] + threadIdx.x; j < Tv; j += 1024) vrows[j] = 0;
+  if (ep_off)   // (the packed learn step's episode row offsets; the prefix is final after the barrier)
+    for (int e = threadIdx.x; e <= b; e += 1024) ep_off[e] = min(off[e], Tv);
 }
 // dst[i][0:cols] = src[rows[i]][0:cols] (V = 4: float4 columns)
 template <int V>
@@ -1327,7 +1338,7 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F, bool embed_cols = true)
   if (D->evolutionary) {
     XTRL_REQUIRE((int64_t)D->b * d <= D->part_floats, "train: partial-sum workspace too small");
     hipLaunchKernelGGL(k_latent_grad, dim3(D->b, (d + 63) / 64), dim3(64 * LG_G), 0, s, D->dac, D->in_dim, 2 * d,
-                       D->b, D->n, d, D->part);
+                       D->b, D->n, d, D->part, D->packed ? D->ep_off : nullptr);
     hipLaunchKernelGGL(k_latent_wgrad, dim3(blocks(d * (D->G + 1), 256)), dim3(256), 0, s, D->part, D->latent, D->b,
                        d, D->G, c.G(D->w_lat), c.G(D->b_lat));
     XTRL_LAUNCHED("train latent grad");
@@ -1356,9 +1367,10 @@ int heads_backward(const Ctx& c, const Ctx& cw, Fork& F, bool embed_cols = true)
 }
 
 // ============================================================================================
-int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
+int train_forward_rows(const XtrlTrainDesc* D, int Trows, hipStream_t s) {
   if (int rc = validate(D)) return rc;
-  const Ctx c{D, s, D->b * D->n};
+  const Ctx c{D, s, Trows};
+  const int32_t* rows = D->packed ? D->vrows : nullptr;
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D);
   int rc;
   // embeddings
@@ -1369,7 +1381,7 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
   EmbedArgs ea{D->swr, c.P(D->w_pin), c.P(D->act_emb), c.P(D->act_emb_b), c.P(D->reward_embed), c.P(D->w_se),
                c.P(D->b_se), D->lat_e, D->prev_action_f, D->next_action_f, D->prev_action, D->next_action,
                D->layers[0].x_attn, D->ac_in, D->ewa, T, D->n, D->S, D->A, d, D->in_dim, D->continuous,
-               D->evolutionary, D->reward_keep, nullptr, nullptr, nullptr, D->rms_norm};
+               D->evolutionary, D->reward_keep, nullptr, nullptr, nullptr, D->rms_norm, rows};
   // fused: every LayerNorm is formed by the kernel that completes its rows — layer 0's attention
   // pre-norm by the embedding, the others in the epilogue of the GEMM before them (out-projection +
   // residual, FF2 + residual)
@@ -1396,8 +1408,9 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
       return rc;
     const int mix_col = Ly.mix ? 3 * I + (D->gate_values ? I : 0) : -1;
     PrepArgs pa{Ly.proj, D->layers[0].proj, Ly.qkv, D->inv_freq, T, D->n, D->H, D->dh, I, Ly.n_qkv,
-                D->layers[0].n_qkv, D->rot_dim, mix_col, D->qk_norm, D->xpos_base};
-    hipLaunchKernelGGL(k_qkv_prep, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pa);
+                D->layers[0].n_qkv, D->rot_dim, mix_col, D->qk_norm, D->xpos_base, rows};
+    const dim3 pg = rows ? dim3(blocks(3 * I / 2, PREP_T), T) : dim3(blocks(3 * I / 2, PREP_T), D->n, D->b);
+    hipLaunchKernelGGL(k_qkv_prep, pg, dim3(PREP_T), 0, s, pa);
     XTRL_LAUNCHED("train qkv_prep");
     const AttnProblem ap = attn_problem(c, Ly, li);
     if ((rc = attn_fwd_ex(ap, Ly.qkv, Ly.qkv + I, Ly.qkv + 2 * I, Ly.o, Ly.lse,
@@ -1445,10 +1458,11 @@ int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
 }
 
 // ============================================================================================
-int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
+int train_backward_rows(const XtrlTrainDesc* D, int Trows, hipStream_t s) {
   if (int rc = validate(D)) return rc;
   XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "train: missing loss gradients");
-  const Ctx c{D, s, D->b * D->n};
+  const Ctx c{D, s, Trows};
+  const int32_t* rows = D->packed ? D->vrows : nullptr;
   const int T = c.T, d = D->d, I = D->H * D->dh, ff = D->ff, lf = ld_ff(D);
   int rc;
   SideStream& side = side_stream();
@@ -1603,8 +1617,9 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
     for (int j = li + 1; j < D->L; ++j) deeper_mix = deeper_mix || D->layers[j].mix;
     PrepBwdArgs pb{dproj, Ly.proj, D->layers[0].proj, D->dvfirst, D->inv_freq, T, D->n, D->H, D->dh, I,
                    Ly.n_qkv, D->layers[0].n_qkv, D->rot_dim, mix_col, li == 0 ? 1 : 0,
-                   (li == 0 ? any_mix : deeper_mix) ? 1 : 0, D->qk_norm, D->xpos_base};
-    hipLaunchKernelGGL(k_qkv_prep_bwd, dim3(blocks(3 * I / 2, PREP_T), D->n, D->b), dim3(PREP_T), 0, s, pb);
+                   (li == 0 ? any_mix : deeper_mix) ? 1 : 0, D->qk_norm, D->xpos_base, rows};
+    const dim3 pg = rows ? dim3(blocks(3 * I / 2, PREP_T), T) : dim3(blocks(3 * I / 2, PREP_T), D->n, D->b);
+    hipLaunchKernelGGL(k_qkv_prep_bwd, pg, dim3(PREP_T), 0, s, pb);
     XTRL_LAUNCHED("train qkv_prep_bwd");
     // q | k | v | gate | mix projection
     if ((rc = F.fork())) return rc;
@@ -1665,6 +1680,97 @@ int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
   XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L), "train: side events %d != %d", F.next,
                (int)side_events_needed(D->L));
   return XTRL_OK;
+}
+
+// ============================================================================================
+// Packed learn step (XtrlTrainDesc.packed): the minibatch without its padding.  With the per-token
+// critic reduction every loss term is a masked mean over the valid tokens (xtrl.py:944-978) and a
+// valid token sees only earlier valid keys (causal + key padding), so the padded tokens change
+// neither the loss nor any gradient: the step runs on the Tv valid tokens, episode after episode.
+namespace {
+struct PackBufs {   // carved from pack_ws, 16-byte aligned segments of T rows each
+  float *swr, *pa, *na, *raw, *values, *pred, *done, *d_raw, *d_values, *d_pred, *d_done;
+  int64_t floats;
+};
+int64_t r4(int64_t x) { return (x + 3) & ~int64_t(3); }
+PackBufs pack_bufs(float* base, int T, int S, int A, int n_out, int B) {
+  PackBufs P{};
+  int64_t at = 0;
+  auto take = [&](int cols) {
+    float* q = base ? base + at : nullptr;
+    at += r4((int64_t)T * cols);
+    return q;
+  };
+  const int a = std::max(A, 1);
+  P.swr = take(S + 1); P.pa = take(a); P.na = take(a);
+  P.raw = take(n_out); P.values = take(B); P.pred = take(2 * (S + 1)); P.done = take(1);
+  P.d_raw = take(n_out); P.d_values = take(B); P.d_pred = take(2 * (S + 1)); P.d_done = take(1);
+  P.floats = at;
+  return P;
+}
+// the descriptor the row-wise step runs on: packed inputs / outputs, no compact heads (every row valid)
+int packed_view(const XtrlTrainDesc* D, XtrlTrainDesc& P, PackBufs& B) {
+  XTRL_REQUIRE(D->Tv > 0 && D->Tv <= D->b * D->n, "train (packed): Tv = %d outside (0, b n = %d]", D->Tv, D->b * D->n);
+  XTRL_REQUIRE(D->b <= VR_MAXB && D->vrows && D->vinv && D->ep_off && D->pack_ws, "train (packed): row list buffers");
+  XTRL_REQUIRE(D->Tv <= 65535, "train (packed): %d tokens exceed the prep kernels' grid", D->Tv);
+  B = pack_bufs(D->pack_ws, D->Tv, D->S, D->A, D->n_out, D->B);
+  XTRL_REQUIRE(B.floats <= D->pack_ws_floats, "train (packed): pack_ws %lld < %lld floats",
+               (long long)D->pack_ws_floats, (long long)B.floats);
+  P = *D;
+  P.swr = B.swr;
+  if (D->continuous) {
+    P.prev_action_f = B.pa;
+    P.next_action_f = B.na;
+  } else {
+    P.prev_action = reinterpret_cast<const int32_t*>(B.pa);
+    P.next_action = reinterpret_cast<const int32_t*>(B.na);
+  }
+  P.raw = B.raw; P.values = B.values; P.pred = B.pred; P.done = B.done;
+  P.d_raw = B.d_raw; P.d_values = B.d_values; P.d_pred = B.d_pred; P.d_done = B.d_done;
+  P.Tv = 0;
+  return XTRL_OK;
+}
+}  // namespace
+
+int train_forward(const XtrlTrainDesc* D, hipStream_t s) {
+  if (!D || !D->packed) return train_forward_rows(D, D ? D->b * D->n : 0, s);
+  if (int rc = validate(D)) return rc;
+  XtrlTrainDesc P;
+  PackBufs B;
+  if (int rc = packed_view(D, P, B)) return rc;
+  const int T = D->b * D->n, Tv = D->Tv, S1 = D->S + 1, A = D->continuous ? D->A : 1;
+  hipLaunchKernelGGL(k_valid_rows, dim3(1), dim3(1024), 0, s, D->lens, D->b, D->n, Tv, D->vrows, D->vinv, D->ep_off);
+  gather_rows(D->swr, S1, D->vrows, Tv, S1, B.swr, S1, s);
+  // (discrete actions: int32 moved as 4-byte words)
+  gather_rows(D->continuous ? D->prev_action_f : reinterpret_cast<const float*>(D->prev_action), A, D->vrows, Tv, A,
+              B.pa, A, s);
+  gather_rows(D->continuous ? D->next_action_f : reinterpret_cast<const float*>(D->next_action), A, D->vrows, Tv, A,
+              B.na, A, s);
+  XTRL_LAUNCHED("train packed gather");
+  if (int rc = train_forward_rows(&P, Tv, s)) return rc;
+  // the heads' outputs back to the minibatch's [b][n] layout for the loss kernels (zeros on the padding)
+  scatter_rows(B.raw, D->n_out, D->vinv, T, D->n_out, D->raw, D->n_out, s);
+  scatter_rows(B.values, D->B, D->vinv, T, D->B, D->values, D->B, s);
+  scatter_rows(B.pred, 2 * S1, D->vinv, T, 2 * S1, D->pred, 2 * S1, s);
+  scatter_rows(B.done, 1, D->vinv, T, 1, D->done, 1, s);
+  XTRL_LAUNCHED("train packed scatter");
+  return XTRL_OK;
+}
+
+int train_backward(const XtrlTrainDesc* D, hipStream_t s) {
+  if (!D || !D->packed) return train_backward_rows(D, D ? D->b * D->n : 0, s);
+  if (int rc = validate(D)) return rc;
+  XTRL_REQUIRE(D->d_raw && D->d_values && D->d_pred && D->d_done, "train: missing loss gradients");
+  XtrlTrainDesc P;
+  PackBufs B;
+  if (int rc = packed_view(D, P, B)) return rc;
+  const int Tv = D->Tv, S1 = D->S + 1;
+  gather_rows(D->d_raw, D->n_out, D->vrows, Tv, D->n_out, B.d_raw, D->n_out, s);
+  gather_rows(D->d_values, D->B, D->vrows, Tv, D->B, B.d_values, D->B, s);
+  gather_rows(D->d_pred, 2 * S1, D->vrows, Tv, 2 * S1, B.d_pred, 2 * S1, s);
+  gather_rows(D->d_done, 1, D->vrows, Tv, 1, B.d_done, 1, s);
+  XTRL_LAUNCHED("train packed gradient gather");
+  return train_backward_rows(&P, Tv, s);
 }
 
 // ============================================================================================
@@ -2057,6 +2163,11 @@ extern "C" int64_t xtrl_train_part_floats(int T, int b, int d, int A) {
   const int64_t lat = (int64_t)std::max(b, 1) * d;                                      // latent gradient
   const int64_t emb = (int64_t)std::max(A, 1) * d;                                      // >= 1 embedding chunk
   return std::max(std::max(ln, cs), std::max(lat, emb));
+}
+
+extern "C" int64_t xtrl_train_pack_floats(int T, int S, int A, int n_out, int B) {
+  if (T <= 0) return 0;
+  return xtrl::pack_bufs(nullptr, T, S, A, n_out, B).floats;
 }
 
 extern "C" int xtrl_linear_gelu_drop(const float* X, int ldx, const float* W, const float* bias, float* Y, int ldy,

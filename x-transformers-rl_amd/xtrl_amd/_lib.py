@@ -105,7 +105,8 @@ class TrainDesc(C.Structure):
                    ('scratch_per_layer', I32), ('ff_glu', I32), ('ld_u2', I32), ('glu_dh', P),
                    ('qk_norm', I32), ('xpos_base', F32), ('rms_norm', I32),
                    ('Tv', I32), ('vrows', P), ('vinv', P), ('ewa_v', P), ('hp_v', P), ('zp_v', P), ('pred_v', P),
-                   ('d_pred_v', P), ('dzp_v', P), ('dewa_v', P), ('dq_part', P), ('dq_part_floats', I64)])
+                   ('d_pred_v', P), ('dzp_v', P), ('dewa_v', P), ('dq_part', P), ('dq_part_floats', I64),
+                   ('packed', I32), ('ep_off', P), ('pack_ws', P), ('pack_ws_floats', I64)])
 
 
 class FractalTrainLevel(C.Structure):
@@ -162,6 +163,7 @@ SIGNATURES = {
     'xtrl_attn_fwd': (I32, [P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd': (I32, [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, F32, F32, U64, U32, U32, P]),
     'xtrl_attn_bwd_part_floats': (I64, [I32, I32, I32, I32]),
+    'xtrl_train_pack_floats': (I64, [I32, I32, I32, I32, I32]),
     'xtrl_attn_bwd_part': (I32, [P, P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, I32, I32, F32, F32, U64, U32, U32,
                                   P]),
     'xtrl_loss_fwd': (I32, [C.POINTER(LossDesc), P]),

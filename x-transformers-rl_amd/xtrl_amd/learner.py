@@ -106,7 +106,8 @@ class Agent(nn.Module):
                  actor_loss_weight=1., critic_loss_weight=1., autoregressive_loss_weight=1.,
                  # extensions (decision log in DESIGN.md)
                  reward_dropout=0.5, seed=0, rotary_abs_rollout=False, hl_reduction_mean=True, hl_sigma_ratio=2.0,
-                 fused_learn=True, device=None, truncation_bootstrap=True, policy_body='decoder', fractal_levels=None):
+                 fused_learn=True, device=None, truncation_bootstrap=True, policy_body='decoder', fractal_levels=None,
+                 packed_learn=False):
         super().__init__()
         self.accelerator = accelerator if accelerator is not None else dist_.DistContext(device)
         dev = self.accelerator.device
@@ -151,6 +152,12 @@ class Agent(nn.Module):
                         rotary_abs_rollout=rotary_abs_rollout,
                         hl_reduction_mean=hl_reduction_mean, hl_sigma_ratio=hl_sigma_ratio)
         self.cfg = c
+        # the learn step without the minibatch's padding (XtrlTrainDesc.packed): exact only with the
+        # per-token critic reduction, where no loss term or gradient involves a padded token
+        if packed_learn and (hl_reduction_mean or not fused_learn or policy_body != 'decoder'):
+            raise ValueError('packed_learn needs hl_reduction_mean=False, fused_learn=True and the decoder policy body: '
+                             'with the scalar HL-Gauss mean the padded tokens carry critic gradient')
+        self.packed_learn = bool(packed_learn)
         # policy body: the x-transformers Decoder (x_transformers_rl.py) or the per-timestep causal
         # fractal encoder (fractal_rl.py:349-619 made causal, fractal.FractalPolicyActorCritic)
         if policy_body == 'fractal':
@@ -440,7 +447,8 @@ class Agent(nn.Module):
                     # the minibatch's valid-token count, from the host copies (no device read)
                     n_valid = int(lens_host[perms_host[epoch, k:k + self.batch_size]].clamp(max=n).sum())
                     step.forward(swr, prev_act, mb_act, latent, mb_lens, keep, attn_seed, attn_off, ff_off,
-                                 c.dropout, Tv=n_valid if self.heads_compact else 0)
+                                 c.dropout, Tv=n_valid if (self.heads_compact or self.packed_learn) else 0,
+                                 packed=self.packed_learn)
                 else:
                     act_in = prev_act if c.continuous else prev_act.long()
                     nxt = mb_act if c.continuous else mb_act.long()

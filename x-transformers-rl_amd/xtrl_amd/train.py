@@ -44,6 +44,9 @@ def _compact_bufs(D, c, T, dev, b_max, n_max):
     for k, t in bufs.items():
         setattr(D, k, t.data_ptr())
     D.Tv = 0
+    # the packed learn step's episode row offsets and its packed inputs / outputs (allocated on first use)
+    bufs['ep_off'] = torch.zeros(b_max + 1, device=dev, dtype=torch.int32)
+    D.ep_off, D.packed, D.pack_ws, D.pack_ws_floats = bufs['ep_off'].data_ptr(), 0, None, 0
     # long episodes (n > 128, dh 16): the attention backward's per-key-tile dQ partials (xtrl_attn_bwd_part)
     D.dq_part, D.dq_part_floats = None, 0
     if n_max > 128 and c.dim_head == 16:
@@ -176,14 +179,26 @@ class FusedTrainStep:
 
     # ------------------------------------------------------------------------------------------
     def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                dropout, Tv=0):
+                dropout, Tv=0, packed=False):
         """swr [b][n][S+1] normalised states | previous reward; actions [b][n] int32 (discrete) or
         [b][n][A] float (continuous); latent [b][G] or None; lens [b] int32.  ``Tv``: the number of
         valid tokens (sum of min(lens, n), known on the host) — the world-model heads then run on
-        those rows only and pred / done hold zeros on the padding; 0: every row.
+        those rows only and pred / done hold zeros on the padding; 0: every row.  ``packed``: the
+        whole step on the Tv valid tokens (XtrlTrainDesc.packed; per-token critic reduction only —
+        Agent(packed_learn=True)); the outputs come back in the [b][n] layout, zeros on the padding.
         Returns views raw [b][n][n_out], values [b][n][B], pred [b][n][2(S+1)], done [b][n]."""
         self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
                           dropout, Tv)
+        D = self.D
+        D.packed = 0
+        if packed:
+            assert 0 < Tv <= D.b * D.n, (Tv, D.b, D.n)
+            D.Tv, D.packed = int(Tv), 1
+            if self.cbuf.get('pack_ws') is None:
+                c = self.cfg
+                nf = int(L.lib().xtrl_train_pack_floats(self.T_max, c.state_dim, c.num_actions, D.n_out, c.num_bins))
+                self.cbuf['pack_ws'] = torch.empty(nf, device=self.dev, dtype=torch.float32)
+                D.pack_ws, D.pack_ws_floats = self.cbuf['pack_ws'].data_ptr(), nf
         L.check(L.lib().xtrl_train_forward(C.byref(self.D), L.stream()), 'train_forward')
         return self._outputs()
 
@@ -358,7 +373,8 @@ class FractalTrainStep(FusedTrainStep):
         self.Fd = Fd
 
     def forward(self, swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
-                dropout, Tv=0):
+                dropout, Tv=0, packed=False):
+        assert not packed, 'the packed learn step is built for the decoder policy body'
         self._bind_inputs(swr, prev_action, next_action, latent, lens, reward_keep, seed, attn_offset, ff_offset,
                           dropout, Tv)
         L.check(L.lib().xtrl_fractal_train_forward(C.byref(self.D), C.byref(self.Fd), L.stream()),
