@@ -70,6 +70,13 @@ CONFIGS = {
     'c2': dict(workload='C2: LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 steps, depth-2 d=128 EPO',
                S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,
                batch=32, hazard_log2=6, dropout=0.25, mode='lander'),
+    # C2 with the per-token critic reduction and the packed learn step (85 % of C2's padded token slots
+    # are padding: T = 500, mean episode length ~ 64)
+    'c2_tok': dict(workload='C2 with the per-token HL-Gauss critic reduction (hl_reduction_mean=False) and the packed '
+                            'learn step (valid tokens only): LunarLander-shaped VecSim, 256 episodes x 3 genes x 500 '
+                            'steps, depth-2 d=128 EPO',
+                   S=8, A=4, episodes=256, T=500, depth=2, dim=128, heads=4, dim_head=16, gates=True, evo=True,
+                   batch=32, hazard_log2=6, dropout=0.25, mode='lander', tok=True),
     # configs[4] — EPO population 8, one gene per GPU at 8 GPUs, the fractal policy body (causal per
     # timestep, x-transformers-rl_amd/xtrl_amd/fractal.py); per GPU 1024 (episode, gene) pairs
     'c5': dict(workload='C5 (per GPU): LunarLander-shaped VecSim, EPO population 8 gene-sharded (gene g on GPU g at '
