@@ -1412,8 +1412,12 @@ bool use_ws() {   // XTRL_GEMM_WS=0: the register-staged X6 kernel instead of th
 }
 
 // the warp-specialised X6 kernel takes whole 32-deep slabs (K and the split span) and no LN prologue
+// (ta: the weight-gradient "T" x "T" layout, whose staging loads every k row on its own — a K that is not
+// a multiple of 32 (the packed learn step's token count) takes the KT variant, the last slab's rows past K
+// zeroed; spans stay multiples of 32)
 bool ws_ok(const GemmArgs& a, bool ta, bool ln) {
-  if (!(use_ws() && !ln && a.K % 32 == 0 && (a.kspan == 0 || a.kspan % 32 == 0) && (!a.rowsum || ta))) return false;
+  if (!(use_ws() && !ln && (a.K % 32 == 0 || ta) && (a.kspan == 0 || a.kspan % 32 == 0) && (!a.rowsum || ta)))
+    return false;
   // one workgroup per CU: it wins only when the whole grid is one resident round and K is long
   // (16384 x 256 x 1024: 59 vs 72 us); with several rounds or K = 256 the register-staged kernel's
   // two workgroups per CU overlap one tile's prologue / epilogue with another's main loop
@@ -1517,7 +1521,7 @@ void dispatch_geom(const GemmArgs& a, bool vec, hipStream_t s) {
   else if (tiles128 >= 192 && a.K > 64) {
     bool done = false;
     if constexpr (EPI != EPI_DGATE && !LN) {   // (the gate epilogue needs more than 256 registers)
-      if (use_x6() && ws_ok(a, TA, LN)) {
+      if (use_x6() && ws_ok(a, TA, LN) && a.K % 32 == 0) {
         launch_ws<TA, TB, EPI, RES>(a, s);
         done = true;
       }
@@ -1717,7 +1721,10 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
       const char* e = getenv("XTRL_WGRAD_WS");
       return !(e && atoi(e) == 0);
     }();
-    if (use_x6() && wgrad_ws && ws_ok(a, true, false)) launch_ws<true, true, EPI_NONE, false>(a, s);
+    if (use_x6() && wgrad_ws && ws_ok(a, true, false)) {
+      if (a.K % 32 == 0) launch_ws<true, true, EPI_NONE, false>(a, s);
+      else launch_ws<true, true, EPI_NONE, false, 128, 128, true>(a, s);
+    }
     else if (use_x6()) launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true, true>(a, s);
     else launch<2, 2, 1, 2, 2, true, true, EPI_NONE, false, false, true>(a, s);
     if (timed) {
