@@ -1540,8 +1540,12 @@ def _first_minibatch_state(agent, traj, lens, genes, fit):
     return out
 
 
-@pytest.mark.parametrize('evo,gates,T,dim', [(True, True, 40, 64), (False, True, 150, 48), (True, False, 130, 64)])
-def test_packed_learn_matches_padded_step(evo, gates, T, dim):
+@pytest.mark.parametrize('evo,gates,T,dim,cont,wm', [
+    (True, True, 40, 64, False, None), (False, True, 150, 48, False, None), (True, False, 130, 64, False, None),
+    (False, True, 40, 64, True, None),                                            # continuous actions
+    (True, True, 40, 64, False, dict(ff_glu=True, attn_qk_norm=True, rotary_xpos=True)),
+    (False, False, 70, 64, False, dict(use_rmsnorm=True))])
+def test_packed_learn_matches_padded_step(evo, gates, T, dim, cont, wm):
     """The packed learn step (Agent(packed_learn=True): only the minibatch's valid tokens, episode after
     episode — packed inputs, per-episode attention row ranges, rotary positions from the row list, the
     latent broadcast and gradient per episode range) against the padded fused step on the same
@@ -1550,9 +1554,12 @@ def test_packed_learn_matches_padded_step(evo, gates, T, dim):
     gradient tensor within 1e-4 of its own scale.  T 150: key tiles past 128 (the long-episode
     attention backward with per-episode rows)."""
     res = {}
+    glu = bool((wm or {}).get('ff_glu', False))
+    extra = {k: v for k, v in (wm or {}).items() if k != 'ff_glu'} or None
     for packed in (False, True):
         learner, env, _ = make_learner(depth=2, gates=gates, evo=evo, T=T, episodes=8, batch=8, seed=5, hazard=5,
-                                       dim=dim, agent_extra=dict(hl_reduction_mean=False, packed_learn=packed))
+                                       dim=dim, cont=cont, ff_glu=glu, wm_extra=extra,
+                                       agent_extra=dict(hl_reduction_mean=False, packed_learn=packed))
         agent = learner.agent
         traj, lens, genes, cum = learner.rollout_device(env, 0, T)
         res[packed] = _first_minibatch_state(agent, traj, lens, genes, learner.fitness(cum, genes))
