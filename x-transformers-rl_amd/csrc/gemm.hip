@@ -1424,7 +1424,10 @@ bool ws_ok(const GemmArgs& a, bool ta, bool ln) {
   // (16384 x 1024 x 256: 94 vs 70 us; tools/gemm_bench.py, XTRL_GEMM_WS=0)
   const int splits = a.kspan > 0 ? (a.K + a.kspan - 1) / a.kspan : 1;
   const int64_t wgs = (int64_t)((a.N + 127) / 128) * ((a.M + 127) / 128) * splits;
-  return wgs <= 256 && (a.kspan > 0 ? a.kspan : a.K) >= 512;
+  // (weight gradients, "T" x "T": the warp-specialised kernel wins at every split span measured, down to
+  // 352 tokens — tools/wgrad_span_lab.hip, 256 x 256 over 16384 tokens: 25.4 vs 31.2 us at 47 splits,
+  // 35.5 vs 48.1 at 24; the C5 fractal step's 256 x 256 / 192 x 256 weights)
+  return wgs <= 256 && (a.kspan > 0 ? a.kspan : a.K) >= (ta ? 64 : 512);
 }
 
 template <bool TA, bool TB, int EPI, bool RES, int BM = 128, int BN = 128, bool KT = false>
