@@ -485,6 +485,12 @@ def ppo_loss_delta(learner, env, cfg, check=True):
     def probe(epoch, mbi, idx, loss, stats):
         if out or not check:
             return
+        try:   # (never raise out of the learn loop: at N > 1 the other ranks are inside its collectives)
+            compare(epoch, mbi, idx, loss)
+        except Exception as e:
+            out['error'] = repr(e)
+
+    def compare(epoch, mbi, idx, loss):
         idx_c = idx.cpu()
         n = int(lens.max())
         sel = lambda t: t[idx_c][:, :n].cpu()
@@ -514,6 +520,8 @@ def ppo_loss_delta(learner, env, cfg, check=True):
     c.dropout = saved_p
     if not check:
         return None
+    if 'error' in out:
+        return dict(error=out['error'])
     out['rel_delta'] = abs(out['gpu'] - out['cpu']) / max(abs(out['cpu']), 1e-12)
     return out
 
