@@ -228,6 +228,48 @@ def test_gemm_ragged_extent_padded_rows(K):
     assert float(((dw.double().cpu() - ad.t() @ x).abs() / _dot_scale(ad.t(), x)).max()) < 1e-6
 
 
+@pytest.mark.parametrize('N,K,ldy,ldx,M,bias,m0', [
+    (256, 8, 256, 9, 16384, False, 0),     # project_in over [states | reward] rows (tall, S 8)
+    (256, 8, 517, 9, 16384, True, 0),      # to_state_embed, dY a column slice of the head input grad
+    (18, 256, 18, 260, 7001, True, 0),     # to_pred.2: 2 (S + 1) outputs (wide, two lanes per index)
+    (4, 500, 4, 500, 4100, True, 0),       # action-logit shaped (wide, float4-aligned operands)
+    (300, 5, 301, 7, 77, True, 3),         # ragged: tall with two indices per lane, a short token range
+    (3, 31, 5, 33, 1000, False, 0),        # every extent off the float4 grid
+])
+def test_wgrad_skinny(N, K, ldy, ldx, M, bias, m0):
+    """Skinny weight gradients (k_wgrad_skinny: one side <= 32 wide with the bias column, the other
+    <= 512) against fp64: dW accumulates (beta 1) onto its old value, db[n - m0] += sum_m dY[m][n]
+    for n >= m0.  Bound: 2^-20 of sum |dy x| (fp32 FMAs over a 64-token span, then the fixed
+    reduction tree)."""
+    from xtrl_amd import _lib as L
+    g = torch.Generator(device='cpu').manual_seed(N * 1000 + K)
+    dy = torch.randn(M, ldy, generator=g)
+    x = torch.randn(M, ldx, generator=g)
+    dw0 = torch.randn(N, K, generator=g)
+    db0 = torch.randn(N - m0, generator=g)
+    dw, db = dw0.to(DEV), db0.to(DEV)
+    ws = torch.empty(32 << 20, device=DEV)
+    dyd, xd = dy.to(DEV), x.to(DEV)
+    if bias:
+        rc = L.lib().xtrl_gemm_wgrad_db(L.ptr(dyd), ldy, L.ptr(xd), ldx, L.ptr(dw), K, M, N, K, 1., L.ptr(ws),
+                                        ws.numel(), L.ptr(db), m0, L.stream())
+    else:
+        rc = L.lib().xtrl_gemm_wgrad(L.ptr(dyd), ldy, L.ptr(xd), ldx, L.ptr(dw), K, M, N, K, 1., L.ptr(ws),
+                                     ws.numel(), L.stream())
+    L.check(rc, 'gemm_wgrad')
+    torch.cuda.synchronize()
+    a, b = dy[:, :N].double().t(), x[:, :K].double()
+    ref = dw0.double() + a @ b
+    err = ((dw.double().cpu() - ref).abs() / (_dot_scale(a, b) + dw0.double().abs())).max().item()
+    assert err < 2.0 ** -20, f'dW: {err / 2.0 ** -24:.1f} x 2^-24'
+    if bias:
+        rb = db0.double() + a.sum(1)[m0:]
+        eb = ((db.double().cpu() - rb).abs() / (a.abs().sum(1)[m0:] + db0.double().abs())).max().item()
+        assert eb < 2.0 ** -20, f'db: {eb / 2.0 ** -24:.1f} x 2^-24'
+    else:
+        assert torch.equal(db.cpu(), db0)
+
+
 # ----------------------------------------------------------------------------------------------
 # training attention
 # ----------------------------------------------------------------------------------------------

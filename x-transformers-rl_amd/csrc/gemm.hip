@@ -1251,16 +1251,28 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* X, int ldx, cons
 // partial z goes to accumulator z % 8, the eight are summed as a fixed tree; eight loads per
 // thread in flight).  Partials are dense [S][M][N]; each thread owns one float4 of C.  Optional
 // row sums (bias gradient): rowsum[m - m0] += sum_z rws[z][m], spread over the grid.
+// sum_z p[z * stride] for z < S in z order, sixteen loads in flight (a serial loop waits out one
+// load latency per split: 64 splits cost tens of microseconds)
+__device__ __forceinline__ float sum_splits(const float* p, int S, int64_t stride) {
+  float acc = 0.f;
+  int z = 0;
+  for (; z + 16 <= S; z += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p[(int64_t)(z + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += v[u];
+  }
+  for (; z < S; ++z) acc += p[(int64_t)z * stride];
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, int M, int N, float* C, int ldc,
                                                        float beta, const float* rws, float* rowsum, int m0) {
   const int64_t MN = (int64_t)M * N;
   const int64_t gtid = (int64_t)blockIdx.x * 256 + threadIdx.x, gsz = (int64_t)gridDim.x * 256;
   if (rowsum) {
-    for (int64_t m = m0 + gtid; m < M; m += gsz) {
-      float acc = rws[m];
-      for (int z = 1; z < S; ++z) acc += rws[(int64_t)z * M + m];
-      rowsum[m - m0] += acc;
-    }
+    for (int64_t m = m0 + gtid; m < M; m += gsz) rowsum[m - m0] += sum_splits(rws + m, S, M);
   }
   if ((N & 3) == 0) {
     // four lanes per float4 of C: lane g sums partials g, g + 4, g + 8, ... (eight loads in
@@ -1303,8 +1315,7 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* ws, int S, i
     return;
   }
   for (int64_t i = gtid; i < MN; i += gsz) {
-    float acc = ws[i];
-    for (int z = 1; z < S; ++z) acc += ws[z * MN + i];
+    const float acc = sum_splits(ws + i, S, MN);
     const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
     float* dst = C + (int64_t)m * ldc + n;
     *dst = (beta != 0.f) ? beta * (*dst) + acc : acc;
@@ -1357,9 +1368,7 @@ __global__ __launch_bounds__(256) void k_splitk_reduce_multi(const SplitKJobs J)
       while (j + 1 < J.n && J.job[j + 1].r0 <= r) ++j;
       const SplitKJob& b = J.job[j];
       const int m = b.m0 + (int)(r - b.r0);
-      float acc = 0.f;
-      for (int z = 0; z < b.S; ++z) acc += b.rws[(int64_t)z * b.M + m];
-      b.rowsum[m - b.m0] += acc;
+      b.rowsum[m - b.m0] += sum_splits(b.rws + m, b.S, b.M);
     }
   }
 }
@@ -1627,6 +1636,189 @@ int gemm_ex(int trans_a, int trans_b, const float* A, int lda, const float* B, i
   return gemm_run(a, trans_a, trans_b, act, s);
 }
 
+// ---- skinny weight gradients: dW [N][K] (+ db) where one side — N, or K plus the bias column — is
+// at most 32 and the other at most 512 (the state / world-model heads: to_state_embed and
+// project_in over the [states | reward] rows of S + 1 floats, to_pred's 2 (S + 1) outputs, the
+// actor's action logits).  The 64 x 64 GEMM tile wastes most of its MFMA work on these and, with
+// rows off the float4 grid, stages them with scalar loads: 58-123 us a launch at C3, on the side
+// stream that bounds the backward's tail.  Here each workgroup owns `span` tokens: it stages SKW_R
+// token rows of dY and X (+ a ones column for the bias) in LDS, a lane owns one index of the long
+// side and accumulates the whole short side against LDS broadcasts (S FMAs per lane-row), and the
+// workgroup's partial goes to ws in the split-K layout ([split][N][K] + bias rows [split][N]), so
+// the same fixed-order reduction (immediate or deferred) finishes it.  Deterministic; the products
+// are plain fp32 FMAs (a token span of 64 per partial, then the reduction's fixed tree).
+constexpr int SKW_R = 64;   // token rows staged per LDS round (the whole default span: one round)
+template <bool TALL, int S, int LJ>
+__global__ __launch_bounds__(256) void k_wgrad_skinny(const float* __restrict__ dY, int ldy, const float* __restrict__ X,
+                                                      int ldx, int M, int N, int K, int bias, int span,
+                                                      float* __restrict__ P, float* __restrict__ PR) {
+  constexpr int R = SKW_R / LJ;   // (the two-index lanes stage half the rows: registers)
+  extern __shared__ float skw_lds[];
+  const int tid = threadIdx.x, Kx = K + bias;
+  const int YS = (N + 3) & ~3, XS = (Kx + 3) & ~3;   // LDS row strides (the broadcast side reads float4)
+  float* Ys = skw_lds;
+  // (pads: a lane past the long side, and the broadcast past the short side, read in-bounds)
+  float* Xs = skw_lds + R * YS + (TALL ? 0 : 256 * LJ);
+  const int t_lo = blockIdx.x * span, t_hi = min(M, t_lo + span);
+  // a round: the long side lane-per-column (row offsets uniform: every load of a lane in flight at
+  // once), the short side flat over its [R][cols] block; rows past the span stage zeros
+  auto stage = [&](int t0) {
+    const float* Lg = TALL ? dY : X;
+    const int ldl = TALL ? ldy : ldx, Ln = TALL ? N : Kx, LSd = TALL ? YS : XS;
+    float* Ld = TALL ? Ys : Xs;
+#pragma unroll
+    for (int j = 0; j < LJ; ++j) {
+      const int c = tid + 256 * j;
+      const bool in = c < Ln, ld = in && (TALL || c < K);
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (t0 + r < t_hi && ld) ? Lg[(int64_t)(t0 + r) * ldl + c] : 0.f;
+      if (!TALL && c == K)   // the bias column
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = t0 + r < t_hi ? 1.f : 0.f;
+      if (in)
+#pragma unroll
+        for (int r = 0; r < R; ++r) Ld[r * LSd + c] = v[r];
+    }
+    const float* Sg = TALL ? X : dY;
+    const int lds_ = TALL ? ldx : ldy, Sn = TALL ? Kx : N, SSd = TALL ? XS : YS;
+    float* Sd = TALL ? Xs : Ys;
+    for (int e = tid; e < R * Sn; e += 256) {
+      const int r = e / Sn, c = e - r * Sn, t = t0 + r;
+      float v = 0.f;
+      if (t < t_hi) v = (!TALL || c < K) ? Sg[(int64_t)t * lds_ + c] : 1.f;   // (TALL: the bias column)
+      Sd[r * SSd + c] = v;
+    }
+  };
+  float acc[LJ][S];
+#pragma unroll
+  for (int j = 0; j < LJ; ++j)
+#pragma unroll
+    for (int c = 0; c < S; ++c) acc[j][c] = 0.f;
+  const float* Ls = TALL ? Ys : Xs;   // the long side: one lane per index
+  const float* Bs = TALL ? Xs : Ys;   // the short side: LDS broadcasts
+  const int LS = TALL ? YS : XS, BSd = TALL ? XS : YS;
+  for (int t0 = t_lo; t0 < t_hi; t0 += R) {
+    if (t0 > t_lo) __syncthreads();   // the previous round's reads are done
+    stage(t0);
+    __syncthreads();
+#pragma unroll 4
+    for (int r = 0; r < R; ++r) {
+      float b[S];
+#pragma unroll
+      for (int c4 = 0; c4 < S / 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(Bs + r * BSd + 4 * c4);
+        b[4 * c4] = v.x; b[4 * c4 + 1] = v.y; b[4 * c4 + 2] = v.z; b[4 * c4 + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < LJ; ++j) {
+        const float l = Ls[r * LS + tid + 256 * j];
+#pragma unroll
+        for (int c = 0; c < S; ++c) acc[j][c] = fmaf(l, b[c], acc[j][c]);
+      }
+    }
+  }
+  // partial [split][N][K] (+ bias rows [split][N])
+  float* Pb = P + (int64_t)blockIdx.x * N * K;
+#pragma unroll
+  for (int j = 0; j < LJ; ++j) {
+    const int li = tid + 256 * j;
+    if (TALL) {
+      if (li < N) {
+#pragma unroll
+        for (int c = 0; c < S; ++c) {
+          if (c < K) Pb[(int64_t)li * K + c] = acc[j][c];
+          else if (c == K && bias) PR[(int64_t)blockIdx.x * N + li] = acc[j][c];
+        }
+      }
+    } else if (li < Kx) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) {
+        if (c < N) {
+          if (li < K) Pb[(int64_t)c * K + li] = acc[j][c];
+          else PR[(int64_t)blockIdx.x * N + c] = acc[j][c];
+        }
+      }
+    }
+  }
+}
+
+// the skinny shape class of a weight gradient (0: not skinny), see k_wgrad_skinny
+struct SkinnyPick {
+  bool tall = false;
+  int S = 0, LJ = 0;
+};
+static SkinnyPick skinny_pick(int N, int Kx) {
+  SkinnyPick p;
+  static const bool on = [] {   // XTRL_WGRAD_SKINNY=0: the 64 x 64 GEMM for these too
+    const char* e = getenv("XTRL_WGRAD_SKINNY");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on) return p;
+  auto s_of = [](int x) { return x <= 4 ? 4 : x <= 8 ? 8 : x <= 12 ? 12 : x <= 16 ? 16 : x <= 24 ? 24 : x <= 32 ? 32 : 0; };
+  if (Kx <= N && s_of(Kx) && N <= 512) {
+    p.tall = true; p.S = s_of(Kx); p.LJ = (N + 255) / 256;
+  } else if (N < Kx && s_of(N) && Kx <= 512) {
+    p.tall = false; p.S = s_of(N); p.LJ = (Kx + 255) / 256;
+  }
+  return p;
+}
+static void launch_skinny(const SkinnyPick& p, const float* dY, int ldy, const float* X, int ldx, int M, int N, int K,
+                          int bias, int span, int splits, float* P, float* PR, hipStream_t s) {
+  const int Kx = K + bias, YS = (N + 3) & ~3, XS = (Kx + 3) & ~3;
+  const size_t lds = sizeof(float) * ((size_t)SKW_R * (YS + XS) + 512 * p.LJ + 32);
+  const dim3 g(splits), b(256);
+#define SKW(T, SS, L)                                                                                   \
+  if (p.tall == T && p.S == SS && p.LJ == L) {                                                          \
+    hipLaunchKernelGGL((k_wgrad_skinny<T, SS, L>), g, b, lds, s, dY, ldy, X, ldx, M, N, K, bias, span, P, PR); \
+    return;                                                                                             \
+  }
+#define SKW_L(T, L) SKW(T, 4, L) SKW(T, 8, L) SKW(T, 12, L) SKW(T, 16, L) SKW(T, 24, L) SKW(T, 32, L)
+  SKW_L(true, 1) SKW_L(true, 2) SKW_L(false, 1) SKW_L(false, 2)
+#undef SKW_L
+#undef SKW
+}
+
+// phase 2 of k_wgrad_skinny: dW = beta dW + sum_z P[z], db[n - m0] += sum_z PR[z][n].  A workgroup
+// per 64 consecutive outputs; wave w sums the splits z = w, w + 4, ... (16 loads in flight), the
+// four wave sums combine in LDS in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void k_skinny_reduce(const float* __restrict__ P, const float* __restrict__ PR, int S,
+                                                       int N, int K, float* dW, int ldw, float beta, float* db, int m0) {
+  __shared__ float part[4][64];
+  const int NK = N * K, nbw = (NK + 63) / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool isb = (int)blockIdx.x >= nbw;
+  const int o = ((int)blockIdx.x - (isb ? nbw : 0)) * 64 + lane;
+  const int len = isb ? N : NK;
+  const float* src = isb ? PR : P;
+  constexpr int U = 16;
+  float acc = 0.f;
+  if (o < len) {
+    for (int z0 = w; z0 < S; z0 += 4 * U) {
+      float p[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int z = z0 + 4 * u;
+        p[u] = z < S ? src[(int64_t)z * len + o] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += p[u];
+    }
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && o < len) {
+    const float sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (isb) {
+      if (o >= m0) db[o - m0] += sum;
+    } else {
+      const int n = o / K, k = o - n * K;
+      float* d = dW + (int64_t)n * ldw + k;
+      *d = beta != 0.f ? beta * *d + sum : sum;
+    }
+  }
+}
+
 // weight gradient dW[N][K] = beta dW + sum_m dY[m][n] X[m][k] (reduction over the M tokens):
 // split the token range over workgroups (partial 64x64 tiles in ws), then a fixed-order sum
 int splitk_flush(SplitKQueue& q, hipStream_t s) {
@@ -1656,6 +1848,45 @@ int gemm_wgrad(const float* dY, int ldy, const float* X, int ldx, float* dW, int
   XTRL_REQUIRE(dY && X && dW && M > 0 && N > 0 && K > 0, "gemm_wgrad: bad arguments");
   XTRL_REQUIRE(ldy >= N && ldx >= K && ldw >= K, "gemm_wgrad: leading dims too small");
   XTRL_REQUIRE(!db || beta == 1.f, "gemm_wgrad: the bias gradient accumulates (beta = 1)");
+  // skinny shapes (k_wgrad_skinny): a workgroup per `span` tokens (XTRL_SKINNY_SPAN, default 64; at
+  // most 1024 partials), reduced at once behind any queued split-K partials in ws
+  if (const SkinnyPick sk = ws ? skinny_pick(N, K + (db ? 1 : 0)) : SkinnyPick{}; sk.S && M >= 64) {
+    static const int sk_span = [] {
+      const char* e = getenv("XTRL_SKINNY_SPAN");
+      return std::max(32, ((e ? atoi(e) : 64) + 31) / 32 * 32);
+    }();
+    int span = std::max(sk_span, (int)(((M + 1023) / 1024 + 31) / 32 * 32));
+    int sp = (M + span - 1) / span;
+    const int64_t per = (int64_t)N * K + (db ? N : 0);
+    float* w = ws;
+    int64_t wf = ws_floats;
+    if (defer && defer->n > 0) {
+      bool overlap = false;   // a queued job that writes this dW / db sums first (its beta may be 0)
+      for (int j = 0; j < defer->n; ++j) {
+        const SplitKJob& o = defer->job[j];
+        const float *a0 = dW, *a1 = dW + (int64_t)(N - 1) * ldw + K, *b0 = o.C, *b1 = o.C + (int64_t)(o.M - 1) * o.ldc + o.N;
+        if (a0 < b1 && b0 < a1) overlap = true;
+        if (db && o.rowsum && db < o.rowsum + (o.M - o.m0) && o.rowsum < db + (N - db_n0)) overlap = true;
+      }
+      if (overlap) {
+        if (int rc = splitk_flush(*defer, s)) return rc;
+      }
+      w += defer->used;
+      wf -= defer->used;
+    }
+    while (sp > 1 && sp * per > wf) {
+      span *= 2;
+      sp = (M + span - 1) / span;
+    }
+    if (sp * per <= wf) {
+      launch_skinny(sk, dY, ldy, X, ldx, M, N, K, db ? 1 : 0, span, sp, w, w + (int64_t)sp * N * K, s);
+      const int nbw = (N * K + 63) / 64, nbb = db ? (N + 63) / 64 : 0;
+      hipLaunchKernelGGL(k_skinny_reduce, dim3(nbw + nbb), dim3(256), 0, s, (const float*)w,
+                         (const float*)(w + (int64_t)sp * N * K), sp, N, K, dW, ldw, beta, db, db_n0);
+      XTRL_LAUNCHED("gemm_wgrad (skinny)");
+      return XTRL_OK;
+    }
+  }
   // GEMM view: C = dW [N x K], A[n][m] = dY[m][n] ("T", lda = ldy), B[m][k] = X[m][k] ("T", ldb = ldx)
   // 128 x 128 tiles (2 workgroups / CU by registers) when the weight is large, else 64 x 64 (4 / CU);
   // split the tokens until 192 workgroups (three quarters of a resident round: the learn step runs
