@@ -27,7 +27,7 @@ extern "C" {
 #define XTRL_E_ARG 1    /* invalid argument / unsupported shape */
 #define XTRL_E_HIP 2    /* HIP launch or runtime error */
 
-#define XTRL_ABI_VERSION 20
+#define XTRL_ABI_VERSION 21
 
 int xtrl_abi_version(void);
 /* sizeof(struct) of a descriptor type named by its C name (-1: unknown); host-only */
@@ -280,6 +280,20 @@ int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, const float* ne
 int xtrl_host_decode(const XtrlDecodeDesc* desc, int t, int rows_max, void* act_host, void* stream);
 int xtrl_host_feedback(const XtrlDecodeDesc* desc, int t, const void* host_stage, void* dev_stage, int t_limit,
                        int bootstrap, void* stream);
+/* The gated form of the scalar-env loop (one row, E == 1, the row-resident step; ABI 21): step t is
+ * queued ahead of the host's env step.  gate = pinned uint32 [3], zeroed per wave: gate[0] the host's
+ * step counter ("go"), gate[1] the last completed step + 1 ("done"), gate[2] the last step + 1 that
+ * gave up.  The launch waits ON THE DEVICE until gate[0] >= t + 1, applies step t - 1's env results
+ * from the pinned stage (xtrl_host_feedback's layout and arithmetic; none at t = 0), runs decode step
+ * t (desc->act_host receives the action) and stores gate[1] = t + 1.  gate[0] = 0xFFFFFFFF cancels every
+ * queued step (they exit untouched); no go within XTRL_HOST_GATE_WAIT_MS (default 4000 ms): the launch
+ * exits untouched and stores gate[2] = t + 1.  xtrl_host_wait(gate + 1, value, timeout_s) spins on the
+ * host until gate[1] >= value (returns 0), gate[2] >= value (1: the device gave up; cancel, feed back
+ * and run the step the ungated way) or timeout_s passed (-1).  Replaces the per-step launch + stream
+ * synchronisation + feedback launch of the reference loop's device half (xtrl.py:1284-1341). */
+int xtrl_host_row_step(const XtrlDecodeDesc* desc, int t, const void* host_stage, int t_limit, int bootstrap,
+                       uint32_t* gate, void* stream);
+int xtrl_host_wait(const uint32_t* done, uint32_t value, double timeout_s);
 
 /* Decode-step projection (the rollout's GEMM):
  *   C[dst(m), n] = act( LN?(A)[m, :] . W[n, :] + bias[n] ) (+ R[m, n])   for m < (m_dev ? *m_dev : M)

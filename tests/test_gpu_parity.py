@@ -6,6 +6,8 @@ import contextlib
 import itertools
 import math
 
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -1915,6 +1917,56 @@ def test_host_env_scalar_contract_matches_oracle(ret, limit, decode_path):
                                                HostLander(ret=ret, limit=limit), 9)
     if limit is not None:
         assert any(ep['boot'] is not None for ep in episodes)     # some episodes truncated
+
+
+class SlowHostLander(HostLander):
+    """HostLander whose env step sleeps ``pause`` seconds at step ``at`` of every ``every``-th episode."""
+
+    def __init__(self, at, pause, every=2, **kw):
+        super().__init__(**kw)
+        self.at, self.pause, self.every = at, pause, every
+
+    def step(self, action):
+        if self.t == self.at and (self.count - 1) % self.every == 0:
+            time.sleep(self.pause)
+        return super().step(action)
+
+
+@pytest.mark.parametrize('ret,limit', [(5, None), (5, 5), (4, 9), (3, None)])
+def test_host_env_gated_step_equals_ungated(ret, limit, monkeypatch):
+    """The gated scalar-env loop (xtrl_host_row_step: decode launches queued ahead, each waiting on the
+    device for the host's go and applying the previous env results itself) against the launch-per-step
+    loop (XTRL_HOST_GATE=0): every trajectory tensor, length, return and bootstrap value bit-identical,
+    with truncation bootstraps (limit 5 / 9) and old-gym returns."""
+    monkeypatch.setenv('XTRL_DECODE_ROWS', '1')
+    runs = []
+    for gate in ('1', '0'):
+        monkeypatch.setenv('XTRL_HOST_GATE', gate)
+        learner, _, _ = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2)
+        eng_w = learner._engine_for_host(1, 9)
+        assert eng_w.rows_max > 0
+        traj, lens, _, cum = learner.rollout_host(HostLander(ret=ret, limit=limit), 0, 9)
+        torch.cuda.synchronize()
+        runs.append((traj, lens.cpu(), cum.clone()))
+    (a, la, ca), (b, lb, cb) = runs
+    assert torch.equal(la, lb) and torch.equal(ca, cb)
+    for k in a:
+        if a[k] is None:
+            assert b[k] is None
+        else:
+            assert torch.equal(torch.nan_to_num(a[k], nan=-7.), torch.nan_to_num(b[k], nan=-7.)), k
+
+
+def test_host_env_gated_step_device_timeout_resumes_ungated(monkeypatch):
+    """A host env step slower than the device's wait (XTRL_HOST_GATE_WAIT_MS=30, a 0.25 s step in
+    every other episode): the queued step reports that it gave up, the wave resumes on the
+    launch-per-step loop from that step (the previous results fed back first) — the rollout still
+    reproduces the oracle's reference loop, bootstraps included."""
+    monkeypatch.setenv('XTRL_DECODE_ROWS', '1')
+    monkeypatch.setenv('XTRL_HOST_GATE', '1')
+    monkeypatch.setenv('XTRL_HOST_GATE_WAIT_MS', '30')
+    learner, _, oracle = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2)
+    _compare_host(learner, oracle, SlowHostLander(at=2, pause=0.25, limit=5), HostLander(limit=5), 9)
 
 
 @pytest.mark.parametrize('frac,dim', [(None, 48), (2, 48), (None, 256)])

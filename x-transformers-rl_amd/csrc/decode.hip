@@ -27,6 +27,7 @@
 // Layouts in HBM: per-step activations are [live row][.] row-major; KV caches [E][H][Tmax][dh]
 // (per episode slot) so one (episode, head) streams a contiguous Tmax*dh block; trajectories
 // [E][Tmax][.] so the learner reads whole episodes contiguously.
+#include <chrono>
 #include "dgemm_body.h"
 #include "kernels.h"
 #include "x6.h"
@@ -796,10 +797,9 @@ __global__ __launch_bounds__(256) void k_heads_sample(const DGemmArgs a, const X
 // done = terminated | truncated ends the episode; a truncated (not terminated) episode with
 // `bootstrap` stays for one more decode step (alive = 2) whose critic logits land in the padding
 // slot traj_values[e][t + 1] — the value of the next state the reference computes at :1323-1336.
-__global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
-                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D.E) return;
+__device__ __forceinline__ void env_feedback_row(const XtrlDecodeDesc& D, int e, int t, const float* next_state,
+                                                 const float* reward, const uint8_t* terminated,
+                                                 const uint8_t* truncated, int t_limit, int bootstrap) {
   const uint8_t al = D.alive[e];
   if (al == 2) {   // its bootstrap step ran (the row-resident step leaves the flag to this kernel)
     D.alive[e] = 0;
@@ -818,6 +818,11 @@ __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_
   if (term) D.alive[e] = 0;
   else if (trunc && bootstrap && t + 1 < D.Tmax) D.alive[e] = 2;
   else if (trunc || t + 1 >= t_limit) D.alive[e] = 0;
+}
+__global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
+                               const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < D.E) env_feedback_row(D, e, t, next_state, reward, terminated, truncated, t_limit, bootstrap);
 }
 
 __global__ void k_rollout_begin(const XtrlDecodeDesc D) {
@@ -1805,13 +1810,32 @@ __device__ uint64_t g_row_stamps[2 * ROW_STAMP_MAX];   // wall clock | shader cl
 constexpr int ROW_G = 4;      // workgroups per row at most (the heads split across them)
 constexpr int ROW_CUS = 256;  // (rows x workgroups per row kept within one workgroup per CU)
 
+// The gated host-env step (xtrl_host_row_step; one workgroup, E == 1): the launch is queued ahead of
+// the host's env step; thread 0 waits for the host's step counter in pinned memory (go >= go_val,
+// system-scope acquire loads, s_sleep between polls), the workgroup applies the env's results of step
+// t - 1 from the pinned stage (k_env_feedback's arithmetic), runs decode step t, and thread 0 — the
+// thread whose sampling stored the action into pinned memory — publishes go_val in `done` (system
+// release).  So neither the launch nor a stream synchronisation sits between the env step and the
+// decode.  go == HG_CANCEL: exit at once (the host ends the wave); no go within wait_ticks: exit
+// untouched, done[1] = go_val (the host falls back to launching the step itself).  done[0] only ever
+// holds completed steps, so a later launch giving up cannot hide an earlier completion.
+struct HostGate {
+  const uint32_t* go;   // null: not gated
+  uint32_t* done;        // [0] the last completed step's go_val, [1] the last go_val that gave up
+  const float* stage;   // [E][S] next state | [E] reward | [E] terminated u8 | [E] truncated u8
+  uint32_t go_val;
+  int t_prev, t_limit, bootstrap;
+  uint64_t wait_ticks;   // of the 100 MHz constant clock (XTRL_HOST_GATE_WAIT_MS, default 4000)
+};
+constexpr uint32_t HG_CANCEL = 0xFFFFFFFFu;
+
 // G > 1: with few live rows, Ge in {4, 2} (<= G, rows x Ge <= 256) workgroups carry each row — every one runs the
 // row's embedding and layers (identical arithmetic; only the first stores the shared state), then
 // takes 4 d / Ge of the heads' hidden units and its partial of the last Linear; the partials meet
 // through k_mlp's hand-off (sc1 stores, one counter per row) and the last arriver sums them in
 // workgroup order, adds b2 and samples.  The heads are ~40 % of a row's weight bytes (C2).
 template <int DH, int KP = (DH == 16 ? 2 : 1)>   // KP: 64-key K passes per round trip
-__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t, int G) {
+__global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, int t, int G, const HostGate hg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ int rows_sh[EMB_MAX_E];
   __shared__ int wsum[ROW_T / 64];
@@ -1819,6 +1843,33 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   float *xs = lds + Lo.x, *xn = lds + Lo.xn, *qkv = lds + Lo.qkv, *att = lds + Lo.att, *v1s = lds + Lo.v1;
   float *hs = lds + Lo.h, *ac = lds + Lo.ac, *part = lds + Lo.part, *lg = lds + Lo.lg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (hg.go) {   // the gated host-env step: the host's go, then the env's results of step t - 1
+    __shared__ uint32_t go_sh;
+    if (tid == 0) {
+      const uint64_t c0 = wall_clock64();
+      uint32_t v = __hip_atomic_load(hg.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      while (v < hg.go_val) {
+        if (wall_clock64() - c0 > hg.wait_ticks) break;
+        __builtin_amdgcn_s_sleep(4);
+        v = __hip_atomic_load(hg.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      go_sh = v;
+    }
+    __syncthreads();
+    const uint32_t v = go_sh;
+    if (v == HG_CANCEL) return;
+    if (v < hg.go_val) {   // the host never came: nothing done, the host takes the step over
+      if (tid == 0) __hip_atomic_store(hg.done + 1, hg.go_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    if (hg.t_prev >= 0 && tid < D.E) {
+      const int E = D.E, S = D.S;
+      const uint8_t* fl = reinterpret_cast<const uint8_t*>(hg.stage + (int64_t)E * (S + 1));
+      env_feedback_row(D, tid, hg.t_prev, hg.stage, hg.stage + (int64_t)E * S, fl, fl + E, hg.t_limit, hg.bootstrap);
+    }
+    __threadfence();   // (agent-scope acquire: no stale L1 line of the fed-back alive / state bytes)
+    __syncthreads();
+  }
   bool stamp = blockIdx.x == 0 && tid == 0 && g_row_stamp_on;
   int ns = 0;
   auto mark = [&]() {
@@ -2096,6 +2147,13 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
     mark();
     stamp = false;   // (the first row only)
   }
+  if (hg.go) {   // thread 0 stored the row's action into pinned memory (sample_row): publish the step
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence_system();
+      __hip_atomic_store(hg.done, hg.go_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 bool row_ok(const XtrlDecodeDesc* D) {
@@ -2157,7 +2215,7 @@ int decode_step(const XtrlDecodeDesc* D, int t, hipStream_t s) {
 
 
 // the row-resident step over the live rows (workgroup b: rows b, b + grid, ...)
-int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s) {
+int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s, const HostGate& hg = HostGate{}) {
   if (int rc = check_desc(D)) return rc;
   XTRL_REQUIRE(t >= 0 && t < D->Tmax, "decode rows: t=%d outside [0, %d)", t, D->Tmax);
   XTRL_REQUIRE(row_ok(D), "decode rows: the row-resident step needs the k-major weights (w_*_t), d <= 256, "
@@ -2175,9 +2233,11 @@ int decode_step_rows(const XtrlDecodeDesc* D, int t, int max_rows, hipStream_t s
   const int G = (D->row_part && D->row_cnt && D->d % 4 == 0) ? g_env : 1;
   const dim3 grid(std::min(max_rows, D->E) * G);
   const size_t lds = (size_t)row_lds(*D).tot * sizeof(float);
-  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, t, G);
-  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, t, G);
-  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, t, G);
+  if (hg.go) XTRL_REQUIRE(grid.x == 1 && D->act_host, "decode rows: the gated host step takes one row (E == 1) "
+                                                       "and the pinned action buffer");
+  if (D->dh == 16) hipLaunchKernelGGL(k_decode_row<16>, grid, dim3(ROW_T), lds, s, *D, t, G, hg);
+  else if (D->dh == 32) hipLaunchKernelGGL(k_decode_row<32>, grid, dim3(ROW_T), lds, s, *D, t, G, hg);
+  else hipLaunchKernelGGL(k_decode_row<64>, grid, dim3(ROW_T), lds, s, *D, t, G, hg);
   XTRL_LAUNCHED("decode_row");
   return XTRL_OK;
 }
@@ -2290,6 +2350,27 @@ int host_decode(const XtrlDecodeDesc* D, int t, int rows_max, void* act_host, hi
   return XTRL_OK;
 }
 
+// the gated form of a host-env step (one row, E == 1): queued ahead, waits on the device for the
+// host's go (gate[0] >= t + 1), applies step t - 1's env results from the pinned stage, runs decode
+// step t and publishes gate[1] = t + 1 (k_decode_row's HostGate)
+int host_row_step(const XtrlDecodeDesc* D, int t, const void* host_stage, int t_limit, int bootstrap, uint32_t* gate,
+                  hipStream_t s) {
+  XTRL_REQUIRE(host_stage && gate && D && D->E == 1 && t >= 0 && t_limit > 0 && t_limit <= D->Tmax,
+               "host_row_step: bad arguments (one row, pinned stage and gate)");
+  HostGate hg;
+  hg.go = gate;
+  hg.done = gate + 1;
+  hg.stage = static_cast<const float*>(host_stage);
+  hg.go_val = (uint32_t)t + 1u;
+  hg.t_prev = t - 1;
+  hg.t_limit = t_limit;
+  hg.bootstrap = bootstrap;
+  const char* we = getenv("XTRL_HOST_GATE_WAIT_MS");   // (read per call: tests shorten it)
+  const long wait_ms = we && atol(we) > 0 ? atol(we) : 4000;
+  hg.wait_ticks = (uint64_t)wait_ms * 100000ull;
+  return decode_step_rows(D, t, 1, s, hg);
+}
+
 // ... and the env's results back: the pinned stage [E][S] next state | [E] reward | [E] terminated
 // (u8) | [E] truncated (u8) to the device stage (same layout), then the feedback kernel on it
 int host_feedback(const XtrlDecodeDesc* D, int t, const void* host_stage, void* dev_stage, int t_limit, int bootstrap,
@@ -2350,6 +2431,23 @@ extern "C" int xtrl_rollout_env_feedback(const XtrlDecodeDesc* desc, int t, cons
 }
 extern "C" int xtrl_host_decode(const XtrlDecodeDesc* desc, int t, int rows_max, void* act_host, void* stream) {
   return xtrl::host_decode(desc, t, rows_max, act_host, xtrl::as_stream(stream));
+}
+extern "C" int xtrl_host_row_step(const XtrlDecodeDesc* desc, int t, const void* host_stage, int t_limit, int bootstrap,
+                                  uint32_t* gate, void* stream) {
+  return xtrl::host_row_step(desc, t, host_stage, t_limit, bootstrap, gate, xtrl::as_stream(stream));
+}
+// the host half: spin until done[0] >= value (0), done[1] >= value — the awaited launch (or, once it
+// gave up, a later one) found no go in time (1) — or timeout_s passed on the host (-1)
+extern "C" int xtrl_host_wait(const uint32_t* done, uint32_t value, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; ++spin) {
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) >= value) return 0;
+    if (__atomic_load_n(done + 1, __ATOMIC_ACQUIRE) >= value) return 1;
+    if ((spin & 1023u) == 0u &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      return -1;
+    __builtin_ia32_pause();
+  }
 }
 extern "C" int xtrl_host_feedback(const XtrlDecodeDesc* desc, int t, const void* host_stage, void* dev_stage,
                                   int t_limit, int bootstrap, void* stream) {

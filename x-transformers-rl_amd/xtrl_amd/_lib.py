@@ -13,7 +13,7 @@ from pathlib import Path
 import torch   # noqa: F401  (load torch's HIP runtime first so the library binds to the same one)
 
 LIB_PATH = Path(os.environ.get('XTRL_LIB', Path(__file__).resolve().parent / 'libxtrl_hip.so'))   # override: A/B experiments
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 P = C.c_void_p
 I32, I64, U32, U64, F32 = C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
@@ -149,6 +149,8 @@ SIGNATURES = {
     'xtrl_host_decode': (I32, [C.POINTER(DecodeDesc), I32, I32, P, P]),
     'xtrl_host_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, I32, I32, P]),
     'xtrl_rollout_env_feedback': (I32, [C.POINTER(DecodeDesc), I32, P, P, P, P, I32, I32, P]),
+    'xtrl_host_row_step': (I32, [C.POINTER(DecodeDesc), I32, P, I32, I32, P, P]),
+    'xtrl_host_wait': (I32, [P, C.c_uint32, C.c_double]),
     'xtrl_dgemm': (I32, [P, I32, P, P, P, I32, P, I32, P, I32, P, P, I32, I32, I32, I32, P]),
     'xtrl_dgemm_pack': (I32, [P, I32, I32, I32, P, P]),
     'xtrl_fractal_decode_step': (I32, [C.POINTER(DecodeDesc), C.POINTER(FractalDesc), I32, P]),

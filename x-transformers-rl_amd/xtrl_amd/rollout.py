@@ -468,19 +468,13 @@ class RolloutEngine:
         # the env step, the feedback (staging + H2D copy + kernel launch) — bench.py reports them
         ht = self.host_times = dict(decode=0., env=0., feedback=0., steps=0)
         clock = time.perf_counter
-        for t in range(T + 1):
-            if not live.any() and not pending.any():
-                break
-            if not live.any():   # only bootstrap rows: their decode step, no env step
-                self.step(t, rows_max > 0)
-                self.alive.zero_()   # (the row-resident step leaves them at 2 for a feedback that never comes)
-                break
-            c0 = clock()
-            self._host_decode(t, rows_max, desc, act_p, stream)
-            c1 = clock()
+
+        def env_half(t, c1):
+            """The env step on step t's actions and its results staged (pinned); lens / totals / live /
+            pending bookkeeping.  Returns the staging end time."""
+            nonlocal live, pending
             pending[:] = False
-            act = act_np
-            ns, r, term, trunc = env_step(act, live.copy())
+            ns, r, term, trunc = env_step(act_np, live.copy())
             c2 = clock()
             ns = np.asarray(ns, dtype=np.float32).reshape(E, S)
             r = np.asarray(r, dtype=np.float64).reshape(E)
@@ -492,19 +486,96 @@ class RolloutEngine:
             st_rew[:] = r
             flags[:E] = term
             flags[E:2 * E] = trunc
+            ht['env'] += c2 - c1
+            ended = live & (term | trunc | (t + 1 >= T))
+            boot_now = live & trunc & ~term & bool(bootstrap)     # the last step (t + 1 == T) included
+            boot_rows[:] |= boot_now
+            pending = boot_now
+            live = live & ~ended
+            return clock()
+
+        t0 = 0
+        if E == 1 and rows_max > 0 and os.environ.get('XTRL_HOST_GATE', '1') != '0':
+            t0 = self._run_host_gated(T, bootstrap, desc, stream, st_p, dst_p, env_half, lambda: live, lambda: pending)
+        for t in range(t0, T + 1):
+            if not live.any() and not pending.any():
+                break
+            if not live.any():   # only bootstrap rows: their decode step, no env step
+                self.step(t, rows_max > 0)
+                self.alive.zero_()   # (the row-resident step leaves them at 2 for a feedback that never comes)
+                break
+            c0 = clock()
+            self._host_decode(t, rows_max, desc, act_p, stream)
+            c1 = clock()
+            c2 = env_half(t, c1)
             L.check(lib.xtrl_host_feedback(desc, t, st_p, dst_p, T, int(bootstrap), stream), 'host_feedback')
             c3 = clock()
             ht['decode'] += c1 - c0
-            ht['env'] += c2 - c1
             ht['feedback'] += c3 - c2
             ht['steps'] += 1
-            ended = live & (term | trunc | (t + 1 >= T))
-            boot_now = live & trunc & ~term & bool(bootstrap)     # the last step (t + 1 == T) included
-            boot_rows |= boot_now
-            pending = boot_now
-            live = live & ~ended
         torch.cuda.current_stream().synchronize()   # the pinned staging buffer is reused next wave
         return self.traj, lens, totals, boot_rows
+
+    HOST_GATE_AHEAD = 2   # gated steps queued ahead of the host (one decode in flight, the next waiting)
+
+    def _run_host_gated(self, T, bootstrap, desc, stream, st_p, dst_p, env_half, live_of, pending_of):
+        """The scalar-env wave (E == 1) on gated steps (xtrl_host_row_step): each decode launch is
+        queued ahead and waits on the device for the host's go, applies the previous env step's
+        results from the pinned stage itself, and publishes its completion in pinned memory — no
+        launch, stream synchronisation or feedback launch between an env step and the next decode.
+        Returns the step from which the ungated loop continues (T + 1: the wave is done)."""
+        lib = L.lib()
+        if getattr(self, '_host_gate', None) is None:
+            self._host_gate = torch.zeros(3, dtype=torch.int32, pin_memory=True)   # go | done | gave up
+        g = self._host_gate.numpy()
+        gate_p = self._host_gate.data_ptr()
+        done_p = gate_p + 4
+        g[:] = 0
+        ht, clock = self.host_times, time.perf_counter
+
+        def enqueue(t):
+            L.check(lib.xtrl_host_row_step(desc, t, st_p, T, int(bootstrap), gate_p, stream), f'host_row_step(t={t})')
+
+        def wait(v):
+            rc = lib.xtrl_host_wait(done_p, v, 120.0)
+            if rc < 0:
+                g[0] = -1
+                raise RuntimeError(f'host_row_step: step {v - 1} did not complete')
+            return rc == 0
+
+        nxt = 0
+        while nxt < min(self.HOST_GATE_AHEAD, T + 1):
+            enqueue(nxt)
+            nxt += 1
+        resume = T + 1
+        t = 0
+        g[0] = 1   # go: step 0 (no env results yet)
+        while True:
+            c0 = clock()
+            if nxt <= T:   # (queued while the device runs step t)
+                enqueue(nxt)
+                nxt += 1
+            if not wait(t + 1):   # the device gave up waiting: steps t - 1's results unapplied, t not run
+                resume = t
+                break
+            c1 = clock()
+            c2 = env_half(t, c1)
+            ht['decode'] += c1 - c0
+            ht['steps'] += 1
+            g[0] = t + 2   # go: step t + 1 (it applies step t's results first)
+            ht['feedback'] += clock() - c2
+            if not live_of().any():   # step t + 1 only applies the results (and decodes a bootstrap row)
+                if not wait(t + 2):
+                    resume = t + 1
+                elif pending_of().any():
+                    self.alive.zero_()   # (the bootstrap step leaves alive 2 for a feedback that never comes)
+                break
+            t += 1
+        g[0] = -1   # cancel the steps still queued
+        torch.cuda.current_stream().synchronize()
+        if resume <= T and resume > 0:   # the ungated loop resumes at `resume`: its previous results first
+            L.check(lib.xtrl_host_feedback(desc, resume - 1, st_p, dst_p, T, int(bootstrap), stream), 'host_feedback')
+        return resume
 
 
 class FractalRolloutEngine(RolloutEngine):
