@@ -797,10 +797,11 @@ __global__ __launch_bounds__(256) void k_heads_sample(const DGemmArgs a, const X
 // done = terminated | truncated ends the episode; a truncated (not terminated) episode with
 // `bootstrap` stays for one more decode step (alive = 2) whose critic logits land in the padding
 // slot traj_values[e][t + 1] — the value of the next state the reference computes at :1323-1336.
-__device__ __forceinline__ void env_feedback_row(const XtrlDecodeDesc& D, int e, int t, const float* next_state,
-                                                 const float* reward, const uint8_t* terminated,
-                                                 const uint8_t* truncated, int t_limit, int bootstrap) {
-  const uint8_t al = D.alive[e];
+// (al: the row's alive byte as loaded by the caller; copy_state false: the caller copies the state)
+__device__ __forceinline__ void env_feedback_row(const XtrlDecodeDesc& D, int e, uint8_t al, int t,
+                                                 const float* next_state, const float* reward,
+                                                 const uint8_t* terminated, const uint8_t* truncated, int t_limit,
+                                                 int bootstrap, bool copy_state = true) {
   if (al == 2) {   // its bootstrap step ran (the row-resident step leaves the flag to this kernel)
     D.alive[e] = 0;
     return;
@@ -812,7 +813,8 @@ __device__ __forceinline__ void env_feedback_row(const XtrlDecodeDesc& D, int e,
   D.prev_reward[e] = reward[e];
   D.cum_reward[e] += (double)reward[e];
   D.lens[e] = t + 1;
-  for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = next_state[(int64_t)e * D.S + i];
+  if (copy_state)
+    for (int i = 0; i < D.S; ++i) D.state[(int64_t)e * D.S + i] = next_state[(int64_t)e * D.S + i];
   // the bootstrap is taken on any truncated, not terminated step — the last allowed step included
   // (an env TimeLimit equal to max_timesteps: the engine holds Tmax = max_timesteps + 1 positions)
   if (term) D.alive[e] = 0;
@@ -822,7 +824,7 @@ __device__ __forceinline__ void env_feedback_row(const XtrlDecodeDesc& D, int e,
 __global__ void k_env_feedback(const XtrlDecodeDesc D, int t, const float* next_state, const float* reward,
                                const uint8_t* terminated, const uint8_t* truncated, int t_limit, int bootstrap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < D.E) env_feedback_row(D, e, t, next_state, reward, terminated, truncated, t_limit, bootstrap);
+  if (e < D.E) env_feedback_row(D, e, D.alive[e], t, next_state, reward, terminated, truncated, t_limit, bootstrap);
 }
 
 __global__ void k_rollout_begin(const XtrlDecodeDesc D) {
@@ -1862,10 +1864,14 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
       if (tid == 0) __hip_atomic_store(hg.done + 1, hg.go_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
-    if (hg.t_prev >= 0 && tid < D.E) {
-      const int E = D.E, S = D.S;
-      const uint8_t* fl = reinterpret_cast<const uint8_t*>(hg.stage + (int64_t)E * (S + 1));
-      env_feedback_row(D, tid, hg.t_prev, hg.stage, hg.stage + (int64_t)E * S, fl, fl + E, hg.t_limit, hg.bootstrap);
+    if (hg.t_prev >= 0 && tid < 64) {   // (E == 1; wave 0: one load of the alive byte for every lane)
+      const int S = D.S;
+      const uint8_t al = D.alive[0];
+      if (al == 1 && tid < S) D.state[tid] = hg.stage[tid];   // (the next state, a lane per column)
+      if (tid == 0) {
+        const uint8_t* fl = reinterpret_cast<const uint8_t*>(hg.stage + (S + 1));
+        env_feedback_row(D, 0, al, hg.t_prev, hg.stage, hg.stage + S, fl, fl + 1, hg.t_limit, hg.bootstrap, false);
+      }
     }
     __threadfence();   // (agent-scope acquire: no stale L1 line of the fed-back alive / state bytes)
     __syncthreads();
