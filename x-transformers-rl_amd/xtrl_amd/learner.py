@@ -696,14 +696,16 @@ class Learner(nn.Module):
                 seeds = [int(episode_seeds[e]) for e, _ in wave]
             reset, step = (_vector_env_fns if vector else _scalar_env_fns)(env, W, seeds, c.continuous)
             latent = None
-            if agent.evolutionary:
-                latent = agent.latent(torch.tensor([g for _, g in wave] + [0] * (W - rows), device=dev))
+            if agent.evolutionary:   # (the wave's genes sliced on the device: no upload per wave)
+                gw = genes[w0:w0 + rows]
+                if rows < W:
+                    gw = torch.cat((gw, gw.new_zeros(W - rows)))
+                latent = agent.latent(gw)
             slots = [self._slot(w0 + i) for i in range(rows)] + [0] * (W - rows)
             traj, wl, wt, wb = eng.run_host_wave(reset, step, agent.seed, update, rows, latent, slots, T,
                                                  bootstrap=agent.truncation_bootstrap)
-            for k, v in traj.items():
-                if v is not None:
-                    out[k][w0:w0 + rows].copy_(v[:rows, :T])
+            keys = [k for k, v in traj.items() if v is not None]
+            torch._foreach_copy_([out[k][w0:w0 + rows] for k in keys], [traj[k][:rows, :T] for k in keys])
             lens[w0:w0 + rows] = torch.from_numpy(wl[:rows])
             cum[w0:w0 + rows] = torch.from_numpy(wt[:rows])
             for i in map(int, wb[:rows].nonzero()[0]):
@@ -800,6 +802,10 @@ def _scalar_env_fns(env, W, seeds, continuous):
         ns, r, term, trunc = _parse_step(env.step(a))
         return (np.asarray(ns, dtype=np.float32)[None], np.asarray(r, dtype=np.float64).reshape(-1)[:1],
                 np.array([bool(term)]), np.array([bool(trunc)]))
+
+    def step_scalar(a):   # (the gated one-row loop: Python scalars, no per-step arrays)
+        return _parse_step(env.step(a))
+    step.scalar = step_scalar
     return reset, step
 
 

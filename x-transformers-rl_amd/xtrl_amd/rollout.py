@@ -21,6 +21,7 @@ import dataclasses
 import os
 import time
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -297,15 +298,30 @@ class RolloutEngine:
     def _begin(self, seed, update, slot_offset, episode_of_slot, latent, slots=None):
         """``slots``: per-row global pair indices keying the sampling stream (gene-sharded ranks);
         None: rows are the contiguous pairs slot_offset, slot_offset + 1, ..."""
+        # the small per-rollout uploads (rng words, slots, episode ids) through one pinned stage and
+        # asynchronous copies: a pageable upload blocks the host (host-env waves begin every episode)
+        E = self.E
+        st = getattr(self, '_begin_stage', None)
+        if st is None:
+            st = self._begin_stage = torch.empty(4 + 2 * E, dtype=torch.int32, pin_memory=True)
+            self._begin_np = st.numpy()
+            self._begin_done = torch.cuda.Event()
+        else:
+            self._begin_done.synchronize()   # (the previous rollout's copies out of the stage are done)
+        a = self._begin_np
+        a[:4].view(np.int64)[:] = (seed & 0x7FFFFFFFFFFFFFFF, (int(update) & 0xFFFFFFFF) | (int(slot_offset) << 32))
+        self.rng.copy_(st[:4].view(torch.int64), non_blocking=True)
         if slots is not None:
-            self.slot_of_row.copy_(torch.as_tensor(slots, dtype=torch.int32))
+            a[4:4 + E] = slots
+            self.slot_of_row.copy_(st[4:4 + E], non_blocking=True)
         self.desc.slot_of_row = self.slot_of_row.data_ptr() if slots is not None else None
-        for t in self.traj.values():
-            if t is not None:
-                t.zero_()
-        self.rng.copy_(torch.tensor([seed & 0x7FFFFFFFFFFFFFFF, (int(update) & 0xFFFFFFFF) | (int(slot_offset) << 32)],
-                                    dtype=torch.int64))
-        self.episode_of_slot.copy_(episode_of_slot.to(torch.int32))
+        if episode_of_slot.is_cuda:
+            self.episode_of_slot.copy_(episode_of_slot.to(torch.int32))
+        else:
+            a[4 + E:4 + 2 * E] = episode_of_slot.numpy()
+            self.episode_of_slot.copy_(st[4 + E:4 + 2 * E], non_blocking=True)
+        self._begin_done.record()
+        torch._foreach_zero_([t for t in self.traj.values() if t is not None])
         if self.c.evolutionary:
             self.lat_embed.copy_(F.linear(latent, *self.w_lat))
         L.check(L.lib().xtrl_rollout_begin(C.byref(self.desc), L.stream()), 'rollout_begin')
@@ -444,8 +460,13 @@ class RolloutEngine:
         self.desc.act_host = self._host_act.data_ptr()
         st = self._host_stage
         state0 = np.asarray(env_reset(), dtype=np.float32).reshape(E, S)
-        self.state.copy_(torch.from_numpy(state0))
-        eps = torch.arange(E, dtype=torch.int32)
+        # (through the pinned stage, asynchronously: the stage's state rows are next written after the
+        #  first decode step has completed)
+        st[:E * S].numpy()[:] = state0.reshape(-1)
+        self.state.copy_(st[:E * S].view(E, S), non_blocking=True)
+        eps = getattr(self, '_host_eps', None)
+        if eps is None:
+            eps = self._host_eps = torch.arange(E, dtype=torch.int32)
         self._begin(seed, update, 0, eps, latent, slots)
         live = np.arange(E) < rows
         if rows < E:
@@ -494,9 +515,37 @@ class RolloutEngine:
             live = live & ~ended
             return clock()
 
+        scalar_step = getattr(env_step, 'scalar', None)
+
+        def env_half1(t, c1):
+            """env_half for one row of a scalar env (the reference contract) on Python scalars: the
+            same staging and bookkeeping without the per-step numpy temporaries (~10 us a step)."""
+            a = act_np[0].tolist() if self.c.continuous else int(act_np[0])
+            ns, r, term, trunc = scalar_step(a)
+            c2 = clock()
+            r, term, trunc = float(np.asarray(r, dtype=np.float64).reshape(-1)[0]), bool(term), bool(trunc)
+            st_state[0] = np.asarray(ns, dtype=np.float32).reshape(S)
+            st_rew[0] = r
+            flags[0] = term
+            flags[1] = trunc
+            ht['env'] += c2 - c1
+            was = bool(live[0])
+            if was:
+                totals[0] += r
+                lens[0] = t + 1
+            boot = was and trunc and not term and bool(bootstrap)
+            if boot:
+                boot_rows[0] = True
+            pending[0] = boot
+            if was and (term or trunc or t + 1 >= T):
+                live[0] = False
+            return clock()
+
         t0 = 0
         if E == 1 and rows_max > 0 and os.environ.get('XTRL_HOST_GATE', '1') != '0':
-            t0 = self._run_host_gated(T, bootstrap, desc, stream, st_p, dst_p, env_half, lambda: live, lambda: pending)
+            t0 = self._run_host_gated(T, bootstrap, desc, stream, st_p, dst_p,
+                                      env_half1 if scalar_step is not None else env_half, lambda: live,
+                                      lambda: pending)
         for t in range(t0, T + 1):
             if not live.any() and not pending.any():
                 break
