@@ -1957,6 +1957,35 @@ def test_host_env_gated_step_equals_ungated(ret, limit, monkeypatch):
             assert torch.equal(torch.nan_to_num(a[k], nan=-7.), torch.nan_to_num(b[k], nan=-7.)), k
 
 
+class RaisingHostLander(HostLander):
+    """HostLander whose env step raises (once) at the first step ``at`` of any episode."""
+
+    def __init__(self, at, **kw):
+        super().__init__(**kw)
+        self.at, self.raised = at, False
+
+    def step(self, action):
+        if self.t == self.at and not self.raised:
+            self.raised = True
+            raise ValueError('env failure')
+        return super().step(action)
+
+
+def test_host_env_gated_step_env_exception_releases_queued_steps(monkeypatch):
+    """An env step that raises inside the gated loop: the exception reaches the caller at once, the
+    queued decode launches are released (cancel word) instead of waiting out the device timeout, and
+    the same learner then rolls out again and matches the oracle."""
+    monkeypatch.setenv('XTRL_DECODE_ROWS', '1')
+    monkeypatch.setenv('XTRL_HOST_GATE', '1')
+    learner, _, oracle = make_learner(depth=2, gates=True, T=9, episodes=6, batch=2)
+    t0 = time.perf_counter()
+    with pytest.raises(ValueError, match='env failure'):
+        learner.rollout_host(RaisingHostLander(at=1), 0, 9)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 2.0   # (not the 4 s device wait of each queued step)
+    _compare_host(learner, oracle, HostLander(), HostLander(), 9)
+
+
 def test_host_env_gated_step_device_timeout_resumes_ungated(monkeypatch):
     """A host env step slower than the device's wait (XTRL_HOST_GATE_WAIT_MS=30, a 0.25 s step in
     every other episode): the queued step reports that it gave up, the wave resumes on the

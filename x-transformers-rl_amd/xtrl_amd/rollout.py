@@ -599,27 +599,32 @@ class RolloutEngine:
         resume = T + 1
         t = 0
         g[0] = 1   # go: step 0 (no env results yet)
-        while True:
-            c0 = clock()
-            if nxt <= T:   # (queued while the device runs step t)
-                enqueue(nxt)
-                nxt += 1
-            if not wait(t + 1):   # the device gave up waiting: steps t - 1's results unapplied, t not run
-                resume = t
-                break
-            c1 = clock()
-            c2 = env_half(t, c1)
-            ht['decode'] += c1 - c0
-            ht['steps'] += 1
-            g[0] = t + 2   # go: step t + 1 (it applies step t's results first)
-            ht['feedback'] += clock() - c2
-            if not live_of().any():   # step t + 1 only applies the results (and decodes a bootstrap row)
-                if not wait(t + 2):
-                    resume = t + 1
-                elif pending_of().any():
-                    self.alive.zero_()   # (the bootstrap step leaves alive 2 for a feedback that never comes)
-                break
-            t += 1
+        try:
+            while True:
+                c0 = clock()
+                if nxt <= T:   # (queued while the device runs step t)
+                    enqueue(nxt)
+                    nxt += 1
+                if not wait(t + 1):   # the device gave up waiting: steps t - 1's results unapplied, t not run
+                    resume = t
+                    break
+                c1 = clock()
+                c2 = env_half(t, c1)
+                ht['decode'] += c1 - c0
+                ht['steps'] += 1
+                g[0] = t + 2   # go: step t + 1 (it applies step t's results first)
+                ht['feedback'] += clock() - c2
+                if not live_of().any():   # step t + 1 only applies the results (and decodes a bootstrap row)
+                    if not wait(t + 2):
+                        resume = t + 1
+                    elif pending_of().any():
+                        self.alive.zero_()   # (the bootstrap step leaves alive 2 for a feedback that never comes)
+                    break
+                t += 1
+        except BaseException:
+            g[0] = -1   # an env that raised (or an interrupt): release the queued steps at once, and
+            torch.cuda.current_stream().synchronize()   # let them drain before the gate is reused
+            raise
         g[0] = -1   # cancel the steps still queued
         torch.cuda.current_stream().synchronize()
         if resume <= T and resume > 0:   # the ungated loop resumes at `resume`: its previous results first
