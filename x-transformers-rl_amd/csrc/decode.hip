@@ -1690,6 +1690,13 @@ int decode_heads(const XtrlDecodeDesc* D, int t, bool final_norm, hipStream_t s)
 // ---------------------------------------------------------------------------------------------
 constexpr int ROW_T = 512;      // 8 waves (2 per SIMD, up to 256 VGPRs: no spills), 8 float4 loads in flight per lane
 constexpr int ROW_PART = 4096;  // GEMV partial sums: k-groups x N <= 8 x ROW_T floats
+// k-groups of a row GEMV at most: fewer groups = a longer per-thread chain of in-flight loads and
+// FMAs but fewer partial rows to sum after the barrier.  32 / 16 / 8 / 4 (tools/r06_kg*.sh, phase
+// stamps at the lander_host shape): 63.8 / 62.2 / 59.6 / 64.1 us a step (the out-projection 1.44 ->
+// 0.96 us, FF2 2.04 -> 1.72; at 4 FF2's 48-deep chains lose), C2 rollout 27.3 / 26.9 / 27.0 / 29.0 ms
+#ifndef ROW_KG_MAX
+#define ROW_KG_MAX 8
+#endif
 
 // out[n] = act(sum_k x[k] WT[k ldw + n] + bias[n]) (+ res[n]) for n < N (N % 4 == 0, k-major WT, 16-byte
 // aligned rows).  The ROW_T threads form KG = ROW_T / (N / 4) k-groups (at most 32) x N / 4 float4
@@ -1699,7 +1706,7 @@ template <int ACT>
 __device__ __forceinline__ void row_gemv(const float* x, int K, const float* WT, int ldw, const float* bias, int N,
                                          float* out, float* part, const float* res = nullptr) {
   const int tid = threadIdx.x, NC4 = N >> 2;
-  const int KG = NC4 >= ROW_T ? 1 : min(32, ROW_T / NC4);
+  const int KG = NC4 >= ROW_T ? 1 : min(ROW_KG_MAX, ROW_T / NC4);
   const int Kc = (K + KG - 1) / KG;
   // the bias of this thread's first two output columns, loaded beside the weights (after the
   // barrier below it would be one more dependent round trip)
