@@ -60,23 +60,47 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+#ifndef XTRL_DPP_BCAST
+#define XTRL_DPP_BCAST 1
+#endif
+// a row's value broadcast into the next row(s) (row_bcast:15 into rows 1 and 3, row_bcast:31 into
+// rows 2 and 3; the other rows get 0 / -inf): the cross-row steps on the VALU instead of two LDS
+// permutes.  The last lane then holds ((r3 + r2) + (r1 + r0)) — the xor-shuffle form's
+// ((r0 + r1) + (r2 + r3)) with each add commuted, so the same bits — and readlane broadcasts it.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_bcast(float v, float fill) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, fill), __builtin_bit_cast(int, v),
+                                                                CTRL, ROWS, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_mov<0xB1>(v);    // quad_perm [1, 0, 3, 2]
   v += dpp_mov<0x4E>(v);    // quad_perm [2, 3, 0, 1]
   v += dpp_mov<0x141>(v);   // row_half_mirror
   v += dpp_mov<0x140>(v);   // row_mirror
+#if XTRL_DPP_BCAST
+  v += dpp_bcast<0x142, 0xA>(v, 0.f);   // row_bcast:15 -> rows 1, 3
+  v += dpp_bcast<0x143, 0xC>(v, 0.f);   // row_bcast:31 -> rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+#else
   v += __shfl_xor(v, 16, kWave);
   v += __shfl_xor(v, 32, kWave);
   return v;
+#endif
 }
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_mov<0xB1>(v));
   v = fmaxf(v, dpp_mov<0x4E>(v));
   v = fmaxf(v, dpp_mov<0x141>(v));
   v = fmaxf(v, dpp_mov<0x140>(v));
+#if XTRL_DPP_BCAST
+  v = fmaxf(v, dpp_bcast<0x142, 0xA>(v, -INFINITY));
+  v = fmaxf(v, dpp_bcast<0x143, 0xC>(v, -INFINITY));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+#else
   v = fmaxf(v, __shfl_xor(v, 16, kWave));
   v = fmaxf(v, __shfl_xor(v, 32, kWave));
   return v;
+#endif
 }
 
 // 4 x 4 transpose across the four lanes of a quad (lanes with equal lane >> 2): on entry lane
