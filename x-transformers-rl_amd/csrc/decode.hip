@@ -1909,17 +1909,29 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   //      ranks the rows live at the step's start, whichever value of the one byte it sees
   // (every chunk's alive byte loaded in one batch, then ranked chunk by chunk)
   int n_live = 0;
+  // E <= 64 (a scalar host env, small tests): every wave ballots the alive bytes itself and a row's
+  // slot is the r-th set bit of the live mask — no LDS scan, one barrier (the layer descriptors)
+  const bool small_e = D.E <= 64;
+  uint64_t live_mask = 0;
+  if (small_e) {
+    const uint8_t a = D.alive[min(lane, D.E - 1)];
+    const bool al = lane < D.E && live_at(a, t);
+    if (blockIdx.x == 0 && w == 0 && lane < D.E && ended_before(a, t)) D.alive[lane] = 0;
+    live_mask = __ballot(al);
+    n_live = __popcll(live_mask);
+    __syncthreads();
+  }
   constexpr int CH = EMB_MAX_E / ROW_T;
   uint8_t alv[CH];
 #pragma unroll
   for (int ci = 0; ci < CH; ++ci) {
     const int ec = min(ROW_T * ci + tid, D.E - 1);
-    alv[ci] = D.alive[ec];
+    alv[ci] = small_e ? 0 : D.alive[ec];
   }
 #pragma unroll
   for (int ci = 0; ci < CH; ++ci) {
     const int c0 = ROW_T * ci;
-    if (c0 >= D.E) break;   // (uniform)
+    if (small_e || c0 >= D.E) break;   // (uniform)
     const int e = c0 + tid;
     const bool al = e < D.E && live_at(alv[ci], t);
     // (a slot ended at step t - 1 is dead here: cleared before step t + 1 reads the same parity)
@@ -1948,7 +1960,14 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
   const bool lead = gs == 0;   // stores the row's shared state
   __shared__ int last_sh;
   for (int r = (int)blockIdx.x / Ge; r < n_live && (int)blockIdx.x < nrw * Ge; r += nrw) {
-    const int e = rows_sh[r];
+    int e;
+    if (small_e) {   // the r-th live slot: clear the r lowest set bits
+      uint64_t m = live_mask;
+      for (int i = 0; i < r; ++i) m &= m - 1ull;
+      e = __builtin_ctzll(m);
+    } else {
+      e = rows_sh[r];
+    }
     if (lead && tid == 0) D.live_rows[(t & 1) * D.E + r] = e;
     // ---- RSNorm of [state, prev reward], embeddings (k_embed's arithmetic and order)
     if (tid <= S) {
