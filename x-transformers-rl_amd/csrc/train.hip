@@ -1642,9 +1642,25 @@ int train_backward_rows(const XtrlTrainDesc* D, int Trows, hipStream_t s) {
     if ((rc = bucket_done())) return rc;   // bucket L - li: decoder block li
   }
   if ((rc = csq.flush(s))) return rc;   // (before the embeddings reuse the partial workspace)
-  // ---- embeddings: dx is d x0
-  if ((rc = F.fork())) return rc;
-  if ((rc = wgrad(cw, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
+  // ---- embeddings: dx is d x0.  The deferred split-K sums start now on the side stream, beside the
+  // embedding backward, and project_in's small weight gradient runs on the main stream into the
+  // workspace behind them (its immediate reduce; the backward's tail was that gradient waiting for its
+  // fork, then the whole flush).  XTRL_WPIN_MAIN=0: on the side stream, before the flush.
+  static const bool wpin_main = [] {
+    const char* e = getenv("XTRL_WPIN_MAIN");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool wpin_on_main = wpin_main && !D->continuous && !D->grad_events && skq.used < D->ws_floats;
+  if (wpin_on_main) {
+    const int64_t used0 = skq.used;
+    if ((rc = splitk_flush(skq, cw.s))) return rc;
+    if ((rc = gemm_wgrad(D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), D->S, T, d, D->S, 1.f, D->ws + used0,
+                         D->ws_floats - used0, s, nullptr, 0, nullptr, nullptr)))
+      return rc;
+  } else {
+    if ((rc = F.fork())) return rc;
+    if ((rc = wgrad(cw, D->dx, d, D->swr, D->S + 1, c.G(D->w_pin), T, d, D->S))) return rc;
+  }
   if ((rc = colsum(c, D->dx, d, T, d, c.G(D->reward_embed), D->swr + D->S, D->S + 1, D->reward_keep))) return rc;
   if (D->continuous) {
     if ((rc = wgrad(cw, D->dx, d, D->prev_action_f, D->A, c.G(D->act_emb), T, d, D->A))) return rc;
@@ -1677,8 +1693,8 @@ int train_backward_rows(const XtrlTrainDesc* D, int Trows, hipStream_t s) {
   if ((rc = bucket_done())) return rc;   // bucket L + 1: embeddings (and the flat buffer's tail)
   if ((rc = F.wait(F.mark()))) return rc;
   XTRL_REQUIRE(!F.failed, "train: side-stream event record failed");
-  XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L), "train: side events %d != %d", F.next,
-               (int)side_events_needed(D->L));
+  XTRL_REQUIRE(!F.on() || (size_t)F.next == side_events_needed(D->L) - (wpin_on_main ? 1 : 0),
+               "train: side events %d != %d", F.next, (int)side_events_needed(D->L) - (wpin_on_main ? 1 : 0));
   return XTRL_OK;
 }
 
