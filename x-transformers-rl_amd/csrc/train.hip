@@ -2141,16 +2141,31 @@ int fractal_train_backward(const XtrlTrainDesc* D, const XtrlFractalTrainDesc* F
     lddgn = d;
     if ((rc = bucket_done())) return rc;   // bucket Lv - l: level l's block and projection
   }
-  // input embedding (x_in,0 = state W_in^T + b_in + le[0]) and global_state_init (g_0 on every row)
-  if ((rc = Fk.fork())) return rc;
-  if ((rc = wgrad(cw, F->dxa, d, D->swr, S + 1, c.G(D->w_pin), T, d, S, c.G(F->b_in)))) return rc;
+  // input embedding (x_in,0 = state W_in^T + b_in + le[0]) and global_state_init (g_0 on every row).
+  // As the decoder step's backward: the queued split-K sums start on the side stream here and the
+  // small input-projection gradient runs on the main stream behind them in the workspace
+  static const bool wpin_main = [] {
+    const char* e = getenv("XTRL_WPIN_MAIN");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool wpin_on_main = wpin_main && !D->grad_events && skq.used < D->ws_floats;
+  if (wpin_on_main) {
+    const int64_t used0 = skq.used;
+    if ((rc = splitk_flush(skq, cw.s))) return rc;
+    if ((rc = gemm_wgrad(F->dxa, d, D->swr, S + 1, c.G(D->w_pin), S, T, d, S, 1.f, D->ws + used0,
+                         D->ws_floats - used0, c.s, c.G(F->b_in), 0, nullptr, nullptr)))
+      return rc;
+  } else {
+    if ((rc = Fk.fork())) return rc;
+    if ((rc = wgrad(cw, F->dxa, d, D->swr, S + 1, c.G(D->w_pin), T, d, S, c.G(F->b_in)))) return rc;
+  }
   if ((rc = colsum(c, dgn, lddgn, T, d, c.G(F->g_init)))) return rc;
   if ((rc = splitk_flush(skq, cw.s))) return rc;
   if ((rc = bucket_done())) return rc;   // bucket Lv + 1: embeddings, global state, level embeddings
   if ((rc = Fk.wait(Fk.mark()))) return rc;
   XTRL_REQUIRE(!Fk.failed, "fractal train: side-stream event record failed");
-  XTRL_REQUIRE(!Fk.on() || (size_t)Fk.next == fractal_events_needed(Lv), "fractal train: side events %d != %d", Fk.next,
-               (int)fractal_events_needed(Lv));
+  XTRL_REQUIRE(!Fk.on() || (size_t)Fk.next == fractal_events_needed(Lv) - (wpin_on_main ? 1 : 0),
+               "fractal train: side events %d != %d", Fk.next, (int)fractal_events_needed(Lv) - (wpin_on_main ? 1 : 0));
   return XTRL_OK;
 }
 
