@@ -2035,8 +2035,12 @@ __global__ __launch_bounds__(ROW_T) void k_decode_row(const XtrlDecodeDesc D, in
           att[h * DH + c] = q;           //  from LDS, its head's att slot is written only after the scores)
         }
         float kn = 0.f;
+        if constexpr (DH == 16) {   // a row of 16 lanes holds the head's q and k: DPP row sum (no permutes)
+          kn = kpi_sum<16>(q * k);
+        } else {
 #pragma unroll
-        for (int i = 0; i < DH; ++i) kn += __shfl(q, i, 64) * __shfl(k, i, 64);
+          for (int i = 0; i < DH; ++i) kn += __shfl(q, i, 64) * __shfl(k, i, 64);
+        }
         kn *= scale;   // the new key's score, k_attn_decode's channel order
         wave_sync();
         const float4* q4 = reinterpret_cast<const float4*>(att + h * DH);
