@@ -313,7 +313,7 @@ __device__ __forceinline__ void qk_l2norm(float& q, float& k) {
 __device__ __forceinline__ void rotary_row(const XtrlDecodeDesc& D, int t, int c, float& q, float& k) {
   const float f = (float)t * D.inv_freq[c >> 1];
   const float cs = cosf(f), sn = sinf(f);
-  const float qp = __shfl_xor(q, 1, 64), kp = __shfl_xor(k, 1, 64);
+  const float qp = dpp_mov<0xB1>(q), kp = dpp_mov<0xB1>(k);   // the pair partner (lane ^ 1; DPP, no permute)
   const float sgn = (c & 1) ? 1.f : -1.f;   // rotate_half: (-x2, x1)
   q = q * cs + (sgn * qp) * sn;
   k = k * cs + (sgn * kp) * sn;
